@@ -1,0 +1,206 @@
+"""Benchmark of the EGNO / SEGNO trajectory-rollout hot path on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` — one process per GPU (launched
+by torch.distributed.run for N > 1), W untimed steps, then exactly K timed steps bracketed by a
+barrier + synchronize, max over ranks; rank 0 prints ONE JSON line.
+
+A "step" is one pass of the hot path over one batch of synthetic input. Default workload
+(BASELINE.json configs[1], "C2"): EGNO 4 layers, charged N=20, T=10, B=512 per GPU, fp32 — one
+model call producing T=10 frames for all B trajectories. Ranks are independent replicas on their
+own batch shard (the path shards by sample; inference has no collective), so scaling is weak.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "N-body trajectories/s (B×T, N=20 rollout) + pos-MSE vs ref, 1/2/4/8 MI355X"
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = f32-input MFMA peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+# Algorithmic work of one egnn_layer_kernel launch (SURVEY §8d decomposed count):
+#   per edge: 8448 MAC (W2 64x64 + Wc1 64x64 + w_s/W_e/w_c2 vectors)
+#   per node: 24640 MAC (P, Q projections 2x64x64, node_v 64x64+64, node MLP 128x64+64x64)
+MAC_PER_EDGE = 8448
+MAC_PER_NODE = 24640
+
+
+def synthetic_charged(B, N, seed):
+    """SURVEY §8d generator: positions ~ N(0, sigma^2), sigma = (N/5)^(1/3); unit direction x 0.5
+    velocities; charges +-1 with p = 1/2."""
+    g = torch.Generator().manual_seed(seed)
+    sigma = (N / 5.0) ** (1.0 / 3.0)
+    loc = torch.randn(B, N, 3, generator=g) * sigma
+    vel = torch.randn(B, N, 3, generator=g)
+    vel = vel / vel.norm(dim=-1, keepdim=True) * 0.5
+    q = (torch.randint(0, 2, (B, N, 1), generator=g) * 2 - 1).float()
+    return loc, vel, q
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    dev = torch.device(f"cuda:{local}" if torch.cuda.is_available() else "cpu")
+    return world, rank, dev
+
+
+def barrier_sync(world, dev):
+    if world > 1:
+        dist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(world, v, dev):
+    if world == 1:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def build_egno_case(B, N, T, seed, dev):
+    import no_node_comparison_amd as pkg
+    loc, vel, q = synthetic_charged(B, N, seed)
+    edges = pkg.harness.get_edges(B, N, dev)
+    loc, vel, q = loc.to(dev), vel.to(dev), q.to(dev)
+    qq = q.reshape(-1, 1)
+    eao = qq[edges[0]] * qq[edges[1]]
+    x, v, ea, nodes, lm = pkg.harness.prepare_inputs(loc, vel, eao, edges, N, 1, q)
+    t_out = torch.arange(1, T + 1, device=dev).repeat(B, 1)
+    return dict(x=x, h=nodes, edges=edges, edge_fea=ea, v=v, loc_mean=lm, t_out=t_out)
+
+
+def cpu_baseline_egno(model, case, N, T, budget_s=12.0, max_b=64):
+    """Oracle (numpy restatement, test infrastructure) on the host cores over a bounded sample of
+    the same workload: the first samples of rank 0's batch."""
+    from oracle import egno as oe
+    from oracle import harness as oh
+    try:
+        import threadpoolctl
+        cores = max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
+    except Exception:
+        cores = os.cpu_count() or 1
+    p = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    Bc = max_b
+    r, c = oh.full_edges(Bc, N)
+    sl = lambda t, w: t[: Bc * w].detach().cpu().numpy()  # noqa: E731
+    args = dict(x=sl(case["x"], N), h=sl(case["h"], N), row=r, col=c, edge_fea=sl(case["edge_fea"], N * (N - 1)),
+                v=sl(case["v"], N), loc_mean=sl(case["loc_mean"], N), t_out=case["t_out"][:Bc].cpu().numpy())
+    done, t0, out = 0, time.perf_counter(), None
+    while True:
+        out = oe.egno_forward(p, **args, T=T)
+        done += 1
+        if time.perf_counter() - t0 > budget_s or done >= 20:
+            break
+    el = time.perf_counter() - t0
+    return {"value": Bc * done / el, "unit": "trajectories/s", "cores": int(cores), "kind": "port",
+            "sample": f"oracle/egno.py (numpy fp32) EGNO forward, B={Bc} of the same synthetic batch, "
+                      f"N={N}, T={T}, {done} calls in {el:.1f} s"}, out, Bc
+
+
+def run_egno(args, world, rank, dev):
+    import no_node_comparison_amd as pkg
+    B, N, T = args.batch, 20, 10
+    torch.manual_seed(0)
+    model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                     num_timesteps=T, time_emb_dim=32, device=dev).eval()
+    case = build_egno_case(B, N, T, seed=1234 + rank, dev=dev)
+    from no_node_comparison_amd import _lib
+    call = lambda: model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],  # noqa: E731
+                         loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = call()
+        barrier_sync(world, dev)
+        if args.kernel_events:
+            _lib.profile_begin(16 * args.steps + 64)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = call()
+        barrier_sync(world, dev)
+        el = time.perf_counter() - t0
+        records = _lib.profile_end() if args.kernel_events else []
+    layer_events = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
+    tconv_ms = [ms for kind, ms in records if kind in (2, 3)]
+    el = max_over_ranks(world, el, dev)
+    ms = el / args.steps * 1e3
+    value = B * world * args.steps / el
+    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d charged generator, seeded)",
+           "frames_per_s": value * T,
+           "config": {"workload": "C2: EGNO forward (4 layers, hidden 64, 2 modes), charged N=20, T=10, "
+                                  f"B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world, "n_balls": N,
+                      "num_timesteps": T, "parallelism": f"batch-sharded replicas x{world} (no collective)"}}
+    # dominant kernel: egnn_layer_kernel, timed live with HIP events on the launch stream
+    if layer_events:
+        durs = layer_events
+        avg_ms = float(np.mean(durs))
+        E = T * B * N * (N - 1)
+        n = T * B * N
+        flop = 2.0 * (E * MAC_PER_EDGE + n * MAC_PER_NODE)
+        achieved = flop / (avg_ms * 1e-3) / 1e12
+        res["roofline"] = {"kernel": "egnn_layer_kernel<EGNO>", "bound": "mfma", "achieved": achieved,
+                           "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+                           "traffic": pmc_traffic("egnn_layer_kernel"), "avg_launch_ms": avg_ms,
+                           "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(durs),
+                           "tconv_avg_launch_ms": float(np.mean(tconv_ms)) if tconv_ms else None}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, ref_out, Bc = cpu_baseline_egno(model, case, N, T)
+        res["cpu_baseline"] = cb
+        x = out[0].view(T, B, N, 3)[:, :Bc].reshape(-1, 3).double().cpu().numpy()
+        xr = ref_out[0]
+        res["parity"] = {"pos_mse_vs_oracle": float(np.mean((x - xr) ** 2)),
+                         "pos_maxnorm_rel_vs_oracle": float(np.abs(x - xr).max() / np.abs(xr).max()),
+                         "samples_checked": Bc}
+    return res
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=512, help="samples per GPU")
+    ap.add_argument("--workload", default="egno", choices=["egno"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", dest="kernel_events", action="store_false")
+    args = ap.parse_args()
+    world, rank, dev = setup_dist()
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    res = run_egno(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(res))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

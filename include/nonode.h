@@ -1,0 +1,154 @@
+/*
+ * nonode.h — C ABI of the MI355X-native EGNO / SEGNO trajectory-rollout hot path.
+ *
+ * Drop-in boundary for simone7monaco/NO-NODE-comparison (reference @ 2025-07-04).
+ * The reference has no FFI of its own: its boundary is the pair of torch.nn.Module
+ * classes EGNO (EGNO/model/egno.py:8-111) and SEGNO (SEGNO/models/model.py:6-102).
+ * These entry points are what the Python mirror of those classes (package
+ * no-node-comparison_amd, loaded through ctypes) binds; INTEGRATION.md shows the
+ * binding. Every pointer is a DEVICE pointer unless the comment says "host";
+ * every call is asynchronous on `stream` (a hipStream_t passed as void*), never
+ * allocates, never synchronises, and returns 0 on success or a nonzero
+ * nonode_status (the reason is in nonode_last_error()).
+ *
+ * Layouts (fp32, row-major, no padding):
+ *   node arrays     [n_nodes][C]; EGNO nodes are time-major: row = t*B*N + b*N + n
+ *   edge features   [n_graphs_ef * N*(N-1)][n_edge_feat] in the reference edge order
+ *                   (b, i, j != i)  (EGNO/simulation/dataset_simple.py:64-71,101-111)
+ *   graphs          fully connected, equal size N, no self loops; row = receiver i,
+ *                   col = sender j (basic.py:168-186, gcl.py:111-119)
+ */
+#ifndef NONODE_H_
+#define NONODE_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  NONODE_OK = 0,
+  NONODE_EINVAL = 1,       /* bad argument (shape, null pointer, unsupported size) */
+  NONODE_ELAUNCH = 2,      /* HIP launch / runtime error */
+  NONODE_EUNSUPPORTED = 3  /* configuration outside what the kernels implement */
+} nonode_status;
+
+/* Variant of the shared E(n)-equivariant layer. */
+enum { NONODE_VARIANT_EGNO = 0, NONODE_VARIANT_SEGNO = 1 };
+
+const char* nonode_version(void);
+/* Thread-local message describing the last nonzero status. */
+const char* nonode_last_error(void);
+
+/*
+ * Raw nn.Linear parameters of ONE layer, exactly as stored in the reference state_dict.
+ *  EGNO  EGNN_Layer (EGNO/model/basic.py:147-165):
+ *    edge_w1/b1 = edge_message_net.scalar_net.mlp.0  [64][1+64+64+E] input order [s,h_i,h_j,e]
+ *    edge_w2/b2 = edge_message_net.scalar_net.mlp.2  [64][64]
+ *    coord_*    = coord_net.mlp.{0,2}                [64][64], [1][64]
+ *    vel_*      = node_v_net.mlp.{0,2}               [64][64], [1][64]
+ *    node_*     = node_net.mlp.{0,2}                 [64][128], [64][64]
+ *  SEGNO SEGNO_GCL (SEGNO/models/models/gcl.py:26-69):
+ *    edge_w1/b1 = edge_mlp.0  [64][64+64+1+E] input order [h_i,h_j,s,e]
+ *    edge_w2/b2 = edge_mlp.2, coord_* = coord_mlp.{0,2}, node_* = node_mlp.{0,2};
+ *    vel_* unused (pass NULL; coord_mlp_vel is dead in the reference forward).
+ */
+typedef struct {
+  const float* edge_w1; const float* edge_b1;
+  const float* edge_w2; const float* edge_b2;
+  const float* coord_w1; const float* coord_b1;
+  const float* coord_w2; const float* coord_b2;
+  const float* vel_w1; const float* vel_b1;
+  const float* vel_w2; const float* vel_b2;
+  const float* node_w1; const float* node_b1;
+  const float* node_w2; const float* node_b2;
+} nonode_layer_weights;
+
+/* Floats in one packed layer blob (MFMA fragment order). */
+size_t nonode_layer_blob_floats(void);
+
+/* Pack one layer's weights into the kernel's fragment layout (device -> device).
+ * Replaces nothing in the reference (weights are read in place by nn.Linear there);
+ * call it again after every optimizer step. hidden must be 64, n_edge_feat <= 4. */
+int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
+                      float* blob, void* stream);
+
+/* Workspace bytes nonode_egno_forward needs. */
+size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt);
+
+/*
+ * EGNO.forward (EGNO/model/egno.py:37-111) for num_inputs == 1, with_v=True, norm=False,
+ * flat=False, use_time_conv=True, hidden 64.
+ *   x, v, loc_mean [B*N][3]; h [B*N][in_node]; edge_fea [B*N*(N-1)][n_edge_feat];
+ *   t_out [Bt][T] (float; row b' feeds node rows r with r % Bt == b', egno.py:66);
+ *   emb_w [64][in_node+time_emb_dim], emb_b [64];
+ *   blobs[l]   (host array of device ptrs) packed layers from nonode_pack_layer(EGNO);
+ *   tconv_w[l] (host array) time_conv_modules.l.t_conv.weights1   [64][64][modes][2];
+ *   tconvx_w[l](host array) time_conv_x_modules.l.t_conv.weights1 [2][2][modes][2];
+ *   outputs x_out, v_out [T*B*N][3], h_out [T*B*N][64] (time-major, egno.py:89-96).
+ * Limits: N >= 2, T <= 16, modes <= 4, time_emb_dim even <= 64, in_node <= 8.
+ */
+int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                        int time_emb_dim, int modes, int Bt,
+                        const float* x, const float* h, const float* v, const float* loc_mean,
+                        const float* edge_fea, const float* t_out,
+                        const float* emb_w, const float* emb_b,
+                        const float* const* blobs, const float* const* tconv_w,
+                        const float* const* tconvx_w,
+                        float* x_out, float* v_out, float* h_out,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* Workspace bytes nonode_segno_forward_step needs. */
+size_t nonode_segno_workspace_bytes(int B, int N);
+
+/*
+ * SEGNO.embedding + SEGNO.forward_step (SEGNO/models/model.py:73,95-102): h = Linear(his),
+ * then T substeps of SEGNO_GCL.forward (gcl.py:111-119) with dt = 1/T, recurrent=True,
+ * tanh=False, attention=False, the per-edge clamp(+-100) and the segment mean.
+ *   his [B*N][in_node]; x, v [B*N][3]; edge_attr [B*N*(N-1)][n_edge_feat] (frozen over the
+ *   substeps, as in the reference); blob from nonode_pack_layer(SEGNO).
+ *   h_in: if non-NULL, used as the already-embedded h [B*N][64] and emb_w/his are ignored.
+ *   recurrent: h <- h + node_mlp(.) (gcl.py:93-94) when nonzero.
+ *   outputs x_out, v_out [B*N][3], h_out [B*N][64].
+ */
+int nonode_segno_forward_step(int B, int N, int T, int in_node, int n_edge_feat,
+                              const float* his, const float* h_in, const float* x, const float* v,
+                              const float* edge_attr, const float* emb_w, const float* emb_b,
+                              const float* blob, float coords_weight, int recurrent,
+                              float* x_out, float* v_out, float* h_out,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Building blocks (the forwards above are sequences of these).
+ */
+/* TimeConv + TimeConv_x of one EGNO layer (layer_no.py:96-126,152-178, egno.py:100-108) on
+ * time-major [T][BN] arrays; h_out/x_out/v_out may alias h/x/v (in place per column). */
+int nonode_egno_tconv(int BN, int T, int modes, const float* h, const float* x, const float* v,
+                      const float* loc_mean, const float* tconv_w, const float* tconvx_w,
+                      float* h_out, float* x_out, float* v_out, void* stream);
+
+/* One fused E(n)-equivariant layer over n_graphs fully connected graphs of N nodes:
+ * EGNN_Layer.forward (basic.py:167-186) for variant EGNO, SEGNO_GCL.forward (gcl.py:111-119)
+ * for variant SEGNO. Edge features of graph g come from sample g % ef_mod.
+ * dt: SEGNO integrator step 1/n_layers (ignored for EGNO). v_out: SEGNO only. */
+int nonode_egnn_layer(int variant, int n_graphs, int N, int n_edge_feat, int ef_mod,
+                      const float* h, const float* x, const float* v, const float* edge_fea,
+                      const float* blob, float dt, float coords_weight, int recurrent,
+                      float* h_out, float* x_out, float* v_out, void* stream);
+
+/*
+ * Launch timing for benchmarks (not part of the reference boundary). After
+ * nonode_profile_begin(n), the next n kernel launches of egnn_layer (kind 0 = EGNO, 1 = SEGNO)
+ * and tconv (kind 2, 3 = first layer with embedding) are bracketed by hipEvents recorded on
+ * their own stream. nonode_profile_end synchronises those events, writes each launch's duration
+ * in ms and its kind, stops recording, and returns the number of records (or < 0 on error).
+ */
+int nonode_profile_begin(int max_records);
+int nonode_profile_end(float* ms_out, int* kind_out, int max_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NONODE_H_ */

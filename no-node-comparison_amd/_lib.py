@@ -1,0 +1,108 @@
+"""ctypes binding of the C ABI in include/nonode.h (libnonode.so, built for gfx950).
+
+This is the reference-side binding a Python caller needs. The product path has
+no CPU fallback: if the library is missing or the tensors are not on a ROCm device, calls raise.
+"""
+import ctypes
+import os
+
+import torch  # load torch's HIP runtime first so libnonode.so binds to the same libamdhip64
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnonode.so")
+
+# every symbol include/nonode.h declares (tests check the .so exports exactly these)
+SYMBOLS = (
+    "nonode_version", "nonode_last_error", "nonode_layer_blob_floats", "nonode_pack_layer",
+    "nonode_egno_workspace_bytes", "nonode_egno_forward", "nonode_segno_workspace_bytes",
+    "nonode_segno_forward_step", "nonode_egno_tconv", "nonode_egnn_layer", "nonode_profile_begin",
+    "nonode_profile_end",
+)
+
+VARIANT_EGNO = 0
+VARIANT_SEGNO = 1
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+
+class NonodeError(RuntimeError):
+    """A nonzero nonode_status, or the HIP extension is unavailable."""
+
+
+class LayerWeights(ctypes.Structure):
+    """nonode_layer_weights."""
+    _fields_ = [(n, _vp) for n in (
+        "edge_w1", "edge_b1", "edge_w2", "edge_b2", "coord_w1", "coord_b1", "coord_w2", "coord_b2",
+        "vel_w1", "vel_b1", "vel_w2", "vel_b2", "node_w1", "node_b1", "node_w2", "node_b2")]
+
+
+_lib = None
+
+
+def lib():
+    """Load libnonode.so once (raises NonodeError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NonodeError(f"HIP extension not built: {LIB_PATH} is missing "
+                          "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.nonode_version.restype = ctypes.c_char_p
+    L.nonode_last_error.restype = ctypes.c_char_p
+    L.nonode_layer_blob_floats.restype = _sz
+    L.nonode_pack_layer.argtypes = [ctypes.POINTER(LayerWeights), _i, _i, _i, _vp, _vp]
+    L.nonode_egno_workspace_bytes.argtypes = [_i, _i, _i, _i]
+    L.nonode_egno_workspace_bytes.restype = _sz
+    L.nonode_egno_forward.argtypes = ([_i] * 9 + [_vp] * 8 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
+                                      + [_sz, _vp])
+    L.nonode_segno_workspace_bytes.argtypes = [_i, _i]
+    L.nonode_segno_workspace_bytes.restype = _sz
+    L.nonode_segno_forward_step.argtypes = ([_i] * 5 + [_vp] * 8 + [_f, _i] + [_vp] * 4 + [_sz, _vp])
+    L.nonode_egno_tconv.argtypes = [_i, _i, _i] + [_vp] * 10
+    L.nonode_egnn_layer.argtypes = [_i] * 5 + [_vp] * 5 + [_f, _f, _i] + [_vp] * 4
+    L.nonode_profile_begin.argtypes = [_i]
+    L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
+    for s in SYMBOLS:
+        if not hasattr(L, s):
+            raise NonodeError(f"{LIB_PATH} does not export {s}")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise NonodeError(f"nonode status {rc}: {lib().nonode_last_error().decode()}")
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_of(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and (not t.is_cuda):
+            raise NonodeError("no CPU path: the EGNO/SEGNO hot path runs only on a ROCm GPU "
+                              "(move the model and inputs to 'cuda'); the CPU restatement lives "
+                              "in oracle/ and is test infrastructure")
+
+
+def profile_begin(max_records):
+    check(lib().nonode_profile_begin(int(max_records)))
+
+
+def profile_end(max_records=1 << 16):
+    """Return [(kind, ms)] for the launches recorded since profile_begin (synchronises)."""
+    ms = (_f * max_records)()
+    kd = (_i * max_records)()
+    n = lib().nonode_profile_end(ms, kd, max_records)
+    if n < 0:
+        check(-n)
+    return [(kd[i], ms[i]) for i in range(n)]

@@ -1,0 +1,961 @@
+// nonode.hip — MI355X (gfx950, CDNA4) kernels for the EGNO / SEGNO trajectory-rollout hot path.
+//
+// Written for CDNA4 directly: wave64, f32-input MFMA (v_mfma_f32_16x16x4_f32, exact fp32
+// k-ordered FMA chains), LDS-resident sender tables, one workgroup per CU walking a contiguous
+// range of receiver tiles. See DESIGN.md for the data layout and the roofline of each kernel.
+//
+// Reference semantics (simone7monaco/NO-NODE-comparison @ 2025-07-04):
+//   egnn_layer_kernel<EGNO>   EGNN_Layer.forward        EGNO/model/basic.py:167-186
+//   egnn_layer_kernel<SEGNO>  SEGNO_GCL.forward          SEGNO/models/models/gcl.py:111-119
+//   tconv_kernel              TimeConv / TimeConv_x      EGNO/model/layer_no.py:80-178,
+//                             + EGNO.forward glue        EGNO/model/egno.py:99-108
+//   temb_kernel               get_timestep_embedding     EGNO/model/layer_no.py:8-17
+//                             + embedding Linear        EGNO/model/egno.py:50-76
+//   embed_kernel              SEGNO.embedding            SEGNO/models/model.py:73
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "nonode.h"
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
+constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
+constexpr int NW = 8;      // waves per workgroup of the layer kernel
+constexpr int TMAX = 16;   // max trajectory length handled by tconv_kernel
+constexpr int MMAX = 4;    // max Fourier modes
+
+// ---- packed layer blob (floats) --------------------------------------------------------------
+// Fragment matrices: W[64][I] used as the A operand of v_mfma_f32_16x16x4_f32 with the B operand
+// in the "edge-column layout" (ECL): lane l = 16*g + e holds, for channel group mt and q in 0..3,
+// channel 16*mt + 4*g + q of column e. frag(mo, mt)[lane][q] = W[16*mo + (l&15)][16*mt + 4*(l>>4) + q]
+// so one MFMA's output accumulator IS the next MFMA's B operand (no lane movement).
+enum : int {
+  OFF_WA = 0,        // edge W1 h_i columns  [64x64]
+  OFF_WB = 4096,     // edge W1 h_j columns  [64x64]
+  OFF_W2 = 8192,     // edge W2              [64x64]
+  OFF_WC1 = 12288,   // coord W1             [64x64]
+  OFF_WV1 = 16384,   // node_v W1            [64x64] (EGNO)
+  OFF_WN1 = 20480,   // node W1              [64x128]
+  OFF_WN2 = 28672,   // node W2              [64x64]
+  OFF_VEC = 32768,   // vectors, 64 floats each, in "vp" order vp[16*g + 4*mt + q] = v[16*mt + 4*g + q]
+};
+enum : int { V_B1 = 0, V_WS, V_WE0, V_WE1, V_WE2, V_WE3, V_B2, V_BC1, V_WC2, V_BV1, V_WV2, V_BN1, V_BN2,
+             V_COUNT };
+constexpr int OFF_SCAL = OFF_VEC + V_COUNT * 64;  // [0] = coord b2, [1] = node_v b2
+constexpr int BLOB_FLOATS = OFF_SCAL + 64;
+constexpr int EDGE_VEC_FIRST = V_WS;              // ws, we0..3, b2, bc1, wc2 staged to LDS
+constexpr int EDGE_VEC_COUNT = 8;
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NONODE_ELAUNCH, "%s: %s", what, hipGetErrorString(e));
+  return NONODE_OK;
+}
+
+int num_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// ---- optional launch timing (bench.py): hipEvents around every layer / tconv launch ------------
+struct ProfState {
+  std::mutex mu;
+  bool on = false;
+  int cap = 0, n = 0;
+  hipEvent_t* ev = nullptr;   // 2*cap events
+  int* kind = nullptr;
+} g_prof;
+
+struct ProfScope {
+  int slot = -1;
+  hipStream_t s;
+  ProfScope(int kind, hipStream_t stream) : s(stream) {
+    if (!g_prof.on) return;
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    if (g_prof.n >= g_prof.cap) return;
+    slot = g_prof.n++;
+    g_prof.kind[slot] = kind;
+    (void)hipEventRecord(g_prof.ev[2 * slot], s);
+  }
+  ~ProfScope() {
+    if (slot >= 0) (void)hipEventRecord(g_prof.ev[2 * slot + 1], s);
+  }
+};
+
+// ---- device helpers ---------------------------------------------------------------------------
+__device__ __forceinline__ float silu(float x) {  // nn.SiLU
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
+
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc[mo] += sum over the KT*16 input channels of W frag(mo, .) * in (ECL); wf = blob section.
+// UNR bounds how many fragment groups the compiler may keep in flight (register pressure):
+// LDS-resident weights use the full unroll, L2-streamed weights a shallow one.
+template <int KT, int UNR = KT>
+__device__ __forceinline__ void mfma_dense(f4 (&acc)[4], const float* __restrict__ wf, const f4* in,
+                                           int lane) {
+#pragma unroll UNR
+  for (int mt = 0; mt < KT; ++mt) {
+    f4 a[4];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) a[mo] = *reinterpret_cast<const f4*>(wf + ((mo * KT + mt) * 64 + lane) * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma(a[mo][q], in[mt][q], acc[mo]);
+    }
+  }
+}
+
+__device__ __forceinline__ void load_ecl(f4 (&d)[4], const float* row, int g) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) d[mt] = *reinterpret_cast<const f4*>(row + 16 * mt + 4 * g);
+}
+__device__ __forceinline__ void store_ecl(float* row, const f4 (&s)[4], int g) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) *reinterpret_cast<f4*>(row + 16 * mt + 4 * g) = s[mt];
+}
+// vector in vp order: lane group g reads its 16 channels as 4 float4
+__device__ __forceinline__ void load_vp(f4 (&d)[4], const float* vp, int g) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) d[mt] = *reinterpret_cast<const f4*>(vp + 16 * g + 4 * mt);
+}
+__device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[mt][q] = silu(a[mt][q]);
+}
+// sum over the 4 lane groups (lanes e, e+16, e+32, e+48): the full 64-channel dot product
+__device__ __forceinline__ float group_sum(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+__device__ __forceinline__ float dot_vp(const f4 (&a)[4], const float* vp, int g) {
+  f4 w[4];
+  load_vp(w, vp, g);
+  float s = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = fmaf(a[mt][q], w[mt][q], s);
+  return group_sum(s);
+}
+
+// ---- weight packing ---------------------------------------------------------------------------
+struct PackArgs {
+  const float* w1; int ld1; int colA, colB, colS;   // edge W1 [64][ld1]
+  const float* b1; const float* w2; const float* b2;
+  const float* cw1; const float* cb1; const float* cw2; const float* cb2;
+  const float* vw1; const float* vb1; const float* vw2; const float* vb2;  // may be null
+  const float* nw1; const float* nb1; const float* nw2; const float* nb2;
+  int ne;
+  float* blob;
+};
+
+__device__ __forceinline__ void pack_frag(float* dst, const float* src, int ld, int col0, int KT, int d) {
+  const int q = d & 3, l = (d >> 2) & 63, rest = d >> 8;
+  const int mt = rest % KT, mo = rest / KT;
+  dst[d] = src[(16 * mo + (l & 15)) * ld + col0 + 16 * mt + 4 * (l >> 4) + q];
+}
+__device__ __forceinline__ float vp_src(const float* src, int stride, int d) {
+  const int g = d >> 4, mt = (d >> 2) & 3, q = d & 3;
+  return src ? src[(16 * mt + 4 * g + q) * stride] : 0.f;
+}
+
+__global__ void pack_kernel(PackArgs a) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
+  const int sec = blockIdx.y;
+  float* B = a.blob;
+  switch (sec) {
+    case 0: if (d < 4096) pack_frag(B + OFF_WA, a.w1, a.ld1, a.colA, 4, d); break;
+    case 1: if (d < 4096) pack_frag(B + OFF_WB, a.w1, a.ld1, a.colB, 4, d); break;
+    case 2: if (d < 4096) pack_frag(B + OFF_W2, a.w2, 64, 0, 4, d); break;
+    case 3: if (d < 4096) pack_frag(B + OFF_WC1, a.cw1, 64, 0, 4, d); break;
+    case 4: if (d < 4096) { if (a.vw1) pack_frag(B + OFF_WV1, a.vw1, 64, 0, 4, d); else B[OFF_WV1 + d] = 0.f; } break;
+    case 5: pack_frag(B + OFF_WN1, a.nw1, 128, 0, 8, d); break;
+    case 6: if (d < 4096) pack_frag(B + OFF_WN2, a.nw2, 64, 0, 4, d); break;
+    case 7:
+      if (d < V_COUNT * 64) {
+        const int v = d >> 6, i = d & 63;
+        float val = 0.f;
+        switch (v) {
+          case V_B1: val = vp_src(a.b1, 1, i); break;
+          case V_WS: val = vp_src(a.w1 + a.colS, a.ld1, i); break;
+          case V_WE0: case V_WE1: case V_WE2: case V_WE3: {
+            const int f = v - V_WE0;
+            val = f < a.ne ? vp_src(a.w1 + 129 + f, a.ld1, i) : 0.f;
+            break;
+          }
+          case V_B2: val = vp_src(a.b2, 1, i); break;
+          case V_BC1: val = vp_src(a.cb1, 1, i); break;
+          case V_WC2: val = vp_src(a.cw2, 1, i); break;
+          case V_BV1: val = vp_src(a.vb1, 1, i); break;
+          case V_WV2: val = vp_src(a.vw2, 1, i); break;
+          case V_BN1: val = vp_src(a.nb1, 1, i); break;
+          case V_BN2: val = vp_src(a.nb2, 1, i); break;
+        }
+        B[OFF_VEC + d] = val;
+      } else if (d < V_COUNT * 64 + 64) {
+        const int i = d - V_COUNT * 64;
+        B[OFF_SCAL + i] = (i == 0) ? a.cb2[0] : (i == 1 && a.vb2) ? a.vb2[0] : 0.f;
+      }
+      break;
+  }
+}
+
+// ---- fused E(n)-equivariant layer ------------------------------------------------------------
+enum { EGNO = 0, SEGNO = 1 };
+
+struct LayerArgs {
+  const float* __restrict__ h; const float* __restrict__ x; const float* __restrict__ v;
+  const float* __restrict__ ef; const float* __restrict__ blob;
+  float* h_out; float* x_out; float* v_out;
+  int n_total, N, ne, ef_mod, n_tiles, ct, s_max, recurrent;
+  float inv_deg, dt, cw;
+};
+
+size_t layer_lds_floats(int ct, int N, int* s_max_out) {
+  const int s_max = ((16 * ct - 1) / N + 2) * N;
+  if (s_max_out) *s_max_out = s_max;
+  return 8192 + EDGE_VEC_COUNT * 64 + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * (ROWP + 4) +
+         (size_t)ct * 16 * 4;
+}
+
+// One workgroup (8 waves) walks a contiguous range of 16-receiver tiles in chunks of `ct` tiles.
+// Per chunk:  A) P = W1[h_i] h + b1 for receivers, Q = W1[h_j] h for every sender of the touched
+//                graphs (LDS tables), sender positions;
+//             B) (tile, k) units split evenly over the waves: receiver r (lane column) meets
+//                sender (n + k) mod N of its graph; edge MLP + coord MLP on MFMA; partial
+//                message / force sums flushed into LDS accumulators;
+//             C) node update per tile: x (and v) update, node MLP, stores.
+template <int VARIANT>
+__global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
+  const int N = p.N, Nm1 = N - 1;
+  float* sW = smem;                              // W2 | Wc1 fragments (8192)
+  float* sV = sW + 8192;                         // ws, we0..3, b2, bc1, wc2 (vp order)
+  float* sP = sV + EDGE_VEC_COUNT * 64;          // [ct*16][ROWP]
+  float* sQ = sP + p.ct * 16 * ROWP;             // [s_max][ROWP]
+  float* sX = sQ + p.s_max * ROWP;               // [s_max][4]
+  float* sM = sX + p.s_max * 4;                  // [ct*16][ROWP] message sums
+  float* sF = sM + p.ct * 16 * ROWP;             // [ct*16][4]   force sums
+
+  for (int i = tid; i < 2048; i += 512) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_W2)[i];
+  if (tid < EDGE_VEC_COUNT * 16)
+    reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_VEC + EDGE_VEC_FIRST * 64)[tid];
+  const float bc2 = p.blob[OFF_SCAL + 0];
+  const float bv2 = p.blob[OFF_SCAL + 1];
+  const float* vWS = sV + (V_WS - EDGE_VEC_FIRST) * 64;
+  const float* vB2 = sV + (V_B2 - EDGE_VEC_FIRST) * 64;
+  const float* vBC1 = sV + (V_BC1 - EDGE_VEC_FIRST) * 64;
+  const float* vWC2 = sV + (V_WC2 - EDGE_VEC_FIRST) * 64;
+
+  const int G = gridDim.x;
+  const int t_begin = (int)(((long long)blockIdx.x * p.n_tiles) / G);
+  const int t_end = (int)(((long long)(blockIdx.x + 1) * p.n_tiles) / G);
+  __syncthreads();
+
+  for (int c0 = t_begin; c0 < t_end; c0 += p.ct) {
+    const int ctc = min(p.ct, t_end - c0);
+    const int rbase = c0 * 16;
+    const int r_last = min(rbase + ctc * 16, p.n_total) - 1;
+    const int g_lo = rbase / N, g_hi = r_last / N;
+    const int s0 = g_lo * N;
+    const int S = (g_hi - g_lo + 1) * N;
+    const int nsT = (S + 15) >> 4;
+
+    // ---------------- phase A: node projections into LDS ----------------
+    for (int i = tid; i < ctc * 16 * ROWP; i += 512) sM[i] = 0.f;
+    for (int i = tid; i < ctc * 16 * 4; i += 512) sF[i] = 0.f;
+    for (int i = tid; i < S * 3; i += 512) {
+      const int s = i / 3, d = i - 3 * s;
+      sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
+    }
+    for (int job = wave; job < ctc + nsT; job += NW) {
+      const bool isP = job < ctc;                       // wave-uniform
+      const int local = (isP ? job : job - ctc) * 16 + e;
+      int node = isP ? rbase + local : s0 + local;
+      const bool valid = isP ? (node < p.n_total) : (local < S);
+      node = valid ? node : (isP ? p.n_total - 1 : s0);
+      f4 hin[4];
+      load_ecl(hin, p.h + (size_t)node * HID, g);
+      f4 acc[4];
+      if (isP) {
+        load_vp(acc, p.blob + OFF_VEC + V_B1 * 64, g);
+      } else {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      }
+      mfma_dense<4, 1>(acc, p.blob + (isP ? OFF_WA : OFF_WB), hin, lane);
+      if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
+    }
+    __syncthreads();
+
+    // ---------------- phase B: edges ----------------
+    {
+      const int U = ctc * Nm1;
+      const int u0 = (wave * U) / NW, u1 = ((wave + 1) * U) / NW;
+      if (u0 < u1) {
+        int tau = u0 / Nm1;
+        int k = u0 - tau * Nm1 + 1;
+        int rl = 0, n = 0, sb = 0;
+        size_t ebase = 0;
+        bool rvalid = false;
+        float xr0 = 0.f, xr1 = 0.f, xr2 = 0.f, fs0 = 0.f, fs1 = 0.f, fs2 = 0.f;
+        f4 P[4], msum[4];
+        auto setup = [&](int t) {
+          rl = 16 * t + e;
+          const int r = rbase + rl;
+          rvalid = r < p.n_total;
+          const int rc = rvalid ? r : p.n_total - 1;
+          const int gr = rc / N;
+          n = rc - gr * N;
+          sb = gr * N - s0;
+          ebase = ((size_t)(gr % p.ef_mod) * N + n) * Nm1;
+          load_ecl(P, sP + rl * ROWP, g);
+          const float* xs = sX + (sb + n) * 4;
+          xr0 = xs[0]; xr1 = xs[1]; xr2 = xs[2];
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) msum[mt] = f4{0.f, 0.f, 0.f, 0.f};
+          fs0 = fs1 = fs2 = 0.f;
+        };
+        auto flush = [&]() {
+          if (rvalid) {
+            float* mrow = sM + rl * ROWP + 4 * g;
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) atomicAdd(mrow + 16 * mt + q, msum[mt][q]);
+            if (g == 0) {
+              atomicAdd(sF + rl * 4 + 0, fs0);
+              atomicAdd(sF + rl * 4 + 1, fs1);
+              atomicAdd(sF + rl * 4 + 2, fs2);
+            }
+          }
+        };
+        setup(tau);
+        for (int u = u0; u < u1; ++u) {
+          int j = n + k;
+          j = (j >= N) ? j - N : j;
+          const int sl = sb + j;
+          const int jj = (j < n) ? j : j - 1;               // reference edge order (i, j != i)
+          const float* xs = sX + sl * 4;
+          const float r0 = xr0 - xs[0], r1 = xr1 - xs[1], r2 = xr2 - xs[2];
+          const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+          const float* efp = p.ef + (ebase + jj) * p.ne;
+          float ev[4];
+#pragma unroll
+          for (int f = 0; f < 4; ++f) ev[f] = (f < p.ne) ? efp[f] : 0.f;
+          // layer 1 (decomposed): P_i + Q_j + w_s*|r|^2 + W_e e_ij
+          f4 a[4], q4[4], w4[4];
+          load_ecl(q4, sQ + sl * ROWP, g);
+          load_vp(w4, vWS, g);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) a[mt] = P[mt] + q4[mt] + w4[mt] * d2;
+#pragma unroll
+          for (int f = 0; f < 4; ++f) {
+            if (f < p.ne) {
+              load_vp(w4, vWS + (1 + f) * 64, g);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) a[mt] += w4[mt] * ev[f];
+            }
+          }
+          silu_ecl(a);
+          // layer 2: m = SiLU(W2 a + b2)
+          f4 m[4];
+          load_vp(m, vB2, g);
+          mfma_dense<4>(m, sW, a, lane);
+          silu_ecl(m);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
+          // coord MLP: c = w_c2 . SiLU(Wc1 m + bc1) + bc2
+          f4 c1[4];
+          load_vp(c1, vBC1, g);
+          mfma_dense<4>(c1, sW + 4096, m, lane);
+          silu_ecl(c1);
+          const float c = dot_vp(c1, vWC2, g) + bc2;
+          float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
+          if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
+            f0 = fminf(fmaxf(f0, -100.f), 100.f);
+            f1 = fminf(fmaxf(f1, -100.f), 100.f);
+            f2 = fminf(fmaxf(f2, -100.f), 100.f);
+          }
+          fs0 += f0; fs1 += f1; fs2 += f2;
+          if (++k == N) {
+            flush();
+            k = 1;
+            ++tau;
+            if (u + 1 < u1) setup(tau);
+          }
+        }
+        if (k != 1) flush();
+      }
+    }
+    __syncthreads();
+
+    // ---------------- phase C: node update ----------------
+    for (int tau = wave; tau < ctc; tau += NW) {
+      const int rl = 16 * tau + e;
+      const int r = rbase + rl;
+      const bool rvalid = r < p.n_total;
+      const int rc = rvalid ? r : p.n_total - 1;
+      f4 in8[8];
+      f4 hr[4], Mr[4];
+      load_ecl(hr, p.h + (size_t)rc * HID, g);
+      load_ecl(Mr, sM + rl * ROWP, g);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
+      const float F0 = sF[rl * 4 + 0], F1 = sF[rl * 4 + 1], F2 = sF[rl * 4 + 2];
+      const float* xp = p.x + (size_t)rc * 3;
+      const float* vpn = p.v + (size_t)rc * 3;
+      const float x0 = xp[0], x1 = xp[1], x2 = xp[2];
+      const float v0 = vpn[0], v1 = vpn[1], v2 = vpn[2];
+      float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
+      if (VARIANT == EGNO) {
+        // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
+        f4 t[4];
+        load_vp(t, p.blob + OFF_VEC + V_BV1 * 64, g);
+        mfma_dense<4, 1>(t, p.blob + OFF_WV1, hr, lane);
+        silu_ecl(t);
+        const float phi = dot_vp(t, p.blob + OFF_VEC + V_WV2 * 64, g) + bv2;
+        nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
+        nx1 = x1 + phi * v1 + fminf(fmaxf(F1 * p.inv_deg, -100.f), 100.f);
+        nx2 = x2 + phi * v2 + fminf(fmaxf(F2 * p.inv_deg, -100.f), 100.f);
+      } else {
+        // v <- v + agg/T ; x <- x + v/T   (gcl.py:255-257 with coords_weight, gcl.py:242)
+        nv0 = v0 + (F0 * p.inv_deg * p.cw) * p.dt;
+        nv1 = v1 + (F1 * p.inv_deg * p.cw) * p.dt;
+        nv2 = v2 + (F2 * p.inv_deg * p.cw) * p.dt;
+        nx0 = x0 + nv0 * p.dt;
+        nx1 = x1 + nv1 * p.dt;
+        nx2 = x2 + nv2 * p.dt;
+      }
+      // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
+      f4 z[4];
+      load_vp(z, p.blob + OFF_VEC + V_BN1 * 64, g);
+      mfma_dense<8, 1>(z, p.blob + OFF_WN1, in8, lane);
+      silu_ecl(z);
+      f4 hn[4];
+      load_vp(hn, p.blob + OFF_VEC + V_BN2 * 64, g);
+      mfma_dense<4, 1>(hn, p.blob + OFF_WN2, z, lane);
+      if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
+      }
+      if (rvalid) {
+        store_ecl(p.h_out + (size_t)r * HID, hn, g);
+        if (g == 0) {
+          float* xo = p.x_out + (size_t)r * 3;
+          xo[0] = nx0; xo[1] = nx1; xo[2] = nx2;
+          if (VARIANT == SEGNO) {
+            float* vo = p.v_out + (size_t)r * 3;
+            vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- temporal spectral layers -----------------------------------------------------------------
+struct TconvArgs {
+  int BN, T, M, Mfull;
+  const float* h; const float* x; const float* v; const float* lm;
+  const float* w; const float* wx;
+  float* h_out; float* x_out; float* v_out;
+  // FIRST layer only: h0 = embedding([h_in, temb]) built on the fly (egno.py:63-76)
+  const float* hin; int din; const float* emb_w; int emb_ld; const float* etab; int Bt;
+};
+
+// Closed form of irfft(pad(Y[:M]), n=T) used here (pocketfft c2r semantics):
+//   y[t] = (1/T) * sum_{m<M} c_m * (Re Y_m cos(2 pi m t/T) - Im Y_m sin(2 pi m t/T)),
+//   c_0 = 1, c_{T/2} = 1 (T even), else 2 — the imaginary parts at DC / Nyquist drop out since
+//   their sine vanishes.
+template <bool FIRST>
+__global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = p.T, M = p.M, BN = p.BN;
+  float* sWh = smem;                          // [(i*64 + o) * 2M + 2m + c]
+  float* sCos = sWh + 64 * 64 * 2 * M;        // [m][TMAX]
+  float* sSin = sCos + MMAX * TMAX;
+  float* sXf = sSin + MMAX * TMAX;            // per wave [2M][64]
+  for (int i = tid; i < 64 * 64 * M; i += 256) {
+    const int io = i / M, m = i - io * M;
+    sWh[io * 2 * M + 2 * m + 0] = p.w[((size_t)io * p.Mfull + m) * 2 + 0];
+    sWh[io * 2 * M + 2 * m + 1] = p.w[((size_t)io * p.Mfull + m) * 2 + 1];
+  }
+  if (tid < M * T) {
+    const int m = tid / T, t = tid - (tid / T) * T;
+    const double ang = 2.0 * (double)m * (double)t / (double)T;
+    sCos[m * TMAX + t] = (float)cospi(ang);
+    sSin[m * TMAX + t] = (float)sinpi(ang);
+  }
+  __syncthreads();
+  const float invT = 1.0f / (float)T;
+  float cm[MMAX];
+#pragma unroll
+  for (int m = 0; m < MMAX; ++m) cm[m] = (m == 0 || 2 * m == T) ? 1.f : 2.f;
+  float* sX = sXf + wave * 2 * M * 64;
+
+  for (int cc = 0; cc < 4; ++cc) {
+    const int col = blockIdx.x * 16 + wave * 4 + cc;
+    const bool cvalid = col < BN;
+    const int c = cvalid ? col : BN - 1;
+    // ---- x / v channels (TimeConv_x): lanes 0..2 own spatial dim d ----
+    if (lane < 3 && cvalid) {
+      const int d = lane;
+      const float lmv = p.lm[(size_t)c * 3 + d];
+      float xs[TMAX], vs[TMAX];
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < T) {
+          const size_t row = FIRST ? (size_t)c : ((size_t)t * BN + c);
+          xs[t] = p.x[row * 3 + d] - lmv;
+          vs[t] = p.v[row * 3 + d];
+        }
+      }
+      float yr[MMAX][2], yi[MMAX][2];
+#pragma unroll
+      for (int m = 0; m < MMAX; ++m) {
+        if (m < M) {
+          float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f};
+#pragma unroll
+          for (int t = 0; t < TMAX; ++t) {
+            if (t < T) {
+              const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
+              Xr[0] = fmaf(xs[t], cs, Xr[0]); Xi[0] = fmaf(-xs[t], sn, Xi[0]);
+              Xr[1] = fmaf(vs[t], cs, Xr[1]); Xi[1] = fmaf(-vs[t], sn, Xi[1]);
+            }
+          }
+#pragma unroll
+          for (int o = 0; o < 2; ++o) {
+            float ar = 0.f, ai = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+              const float wr = p.wx[(((size_t)i * 2 + o) * p.Mfull + m) * 2 + 0];
+              const float wi = p.wx[(((size_t)i * 2 + o) * p.Mfull + m) * 2 + 1];
+              ar += Xr[i] * wr - Xi[i] * wi;
+              ai += Xr[i] * wi + Xi[i] * wr;
+            }
+            yr[m][o] = ar; yi[m][o] = ai;
+          }
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < T) {
+          float y0 = 0.f, y1 = 0.f;
+#pragma unroll
+          for (int m = 0; m < MMAX; ++m) {
+            if (m < M) {
+              const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
+              y0 += cm[m] * (yr[m][0] * cs - yi[m][0] * sn);
+              y1 += cm[m] * (yr[m][1] * cs - yi[m][1] * sn);
+            }
+          }
+          const size_t row = (size_t)t * BN + c;
+          p.x_out[row * 3 + d] = xs[t] + y0 * invT + lmv;
+          p.v_out[row * 3 + d] = vs[t] + y1 * invT;
+        }
+      }
+    }
+    // ---- hidden channels (TimeConv): lane = channel ----
+    float hc[TMAX];
+    if (FIRST) {
+      float base = 0.f;
+      for (int k = 0; k < p.din; ++k) base = fmaf(p.emb_w[lane * p.emb_ld + k], p.hin[(size_t)c * p.din + k], base);
+      const float* et = p.etab + ((size_t)(c % p.Bt) * T) * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t)
+        if (t < T) hc[t] = et[t * 64] + base;
+    } else {
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t)
+        if (t < T) hc[t] = p.h[((size_t)t * BN + c) * 64 + lane];
+    }
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) {
+      if (m < M) {
+        float Xr = 0.f, Xi = 0.f;
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+          if (t < T) {
+            Xr = fmaf(hc[t], sCos[m * TMAX + t], Xr);
+            Xi = fmaf(-hc[t], sSin[m * TMAX + t], Xi);
+          }
+        }
+        sX[(2 * m) * 64 + lane] = Xr;
+        sX[(2 * m + 1) * 64 + lane] = Xi;
+      }
+    }
+    __syncthreads();
+    float yr[MMAX], yi[MMAX];
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) { yr[m] = 0.f; yi[m] = 0.f; }
+    for (int i = 0; i < 64; ++i) {
+      const float* wrow = sWh + (i * 64 + lane) * 2 * M;
+#pragma unroll
+      for (int m = 0; m < MMAX; ++m) {
+        if (m < M) {
+          const float Xr = sX[(2 * m) * 64 + i], Xi = sX[(2 * m + 1) * 64 + i];
+          const float wr = wrow[2 * m], wi = wrow[2 * m + 1];
+          yr[m] += Xr * wr - Xi * wi;
+          yi[m] += Xr * wi + Xi * wr;
+        }
+      }
+    }
+    if (cvalid) {
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < T) {
+          float y = 0.f;
+#pragma unroll
+          for (int m = 0; m < MMAX; ++m)
+            if (m < M) y += cm[m] * (yr[m] * sCos[m * TMAX + t] - yi[m] * sSin[m * TMAX + t]);
+          y *= invT;
+          p.h_out[((size_t)t * BN + c) * 64 + lane] = hc[t] + (y >= 0.f ? y : 0.01f * y);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// etab[b][t][o] = emb_b[o] + sum_k emb_w[o][din+k] * temb(t_out[b][t])[k]   (layer_no.py:8-17)
+__global__ void temb_kernel(int Bt, int T, int din, int dim, const float* t_out, const float* emb_w,
+                            int emb_ld, const float* emb_b, float* etab) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= Bt * T * 64) return;
+  const int o = idx & 63, bt = idx >> 6;
+  const float tv = t_out[bt];
+  const int half = dim / 2;
+  const float scale = (float)(log(10000.0) / (double)(half - 1));
+  float acc = emb_b[o];
+  for (int k = 0; k < half; ++k) {
+    const float fk = expf((float)k * -scale);
+    const float arg = tv * fk;
+    acc = fmaf(emb_w[o * emb_ld + din + k], sinf(arg), acc);
+    acc = fmaf(emb_w[o * emb_ld + din + half + k], cosf(arg), acc);
+  }
+  etab[idx] = acc;
+}
+
+// out[n][o] = b[o] + sum_k W[o][k] in[n][k]   (SEGNO embedding, model.py:73)
+__global__ void embed_kernel(int n_nodes, int din, const float* in, const float* w, const float* b,
+                             float* out) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_nodes * 64) return;
+  const int o = idx & 63, n = idx >> 6;
+  float acc = b[o];
+  for (int k = 0; k < din; ++k) acc = fmaf(w[o * din + k], in[(size_t)n * din + k], acc);
+  out[idx] = acc;
+}
+
+// ---- host-side launchers ----------------------------------------------------------------------
+template <int VARIANT>
+int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const float* x,
+                 const float* v, const float* ef, const float* blob, float dt, float cw, int recurrent,
+                 float* h_out, float* x_out, float* v_out, hipStream_t stream) {
+  const int n_total = n_graphs * N;
+  const int n_tiles = (n_total + 15) / 16;
+  const int cus = num_cus();
+  const int G = n_tiles < cus ? n_tiles : cus;
+  const int tiles_per = (n_tiles + G - 1) / G;
+  int ct = 8 < tiles_per ? 8 : tiles_per;
+  int s_max = 0;
+  while (ct > 1 && layer_lds_floats(ct, N, &s_max) * 4 > 160 * 1024) --ct;
+  const size_t lds = layer_lds_floats(ct, N, &s_max) * 4;
+  if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "N=%d too large for the LDS sender table", N);
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+  });
+  LayerArgs a;
+  a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
+  a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
+  a.n_total = n_total; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.n_tiles = n_tiles; a.ct = ct;
+  a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
+  ProfScope prof(VARIANT, stream);
+  hipLaunchKernelGGL(egnn_layer_kernel<VARIANT>, dim3(G), dim3(512), lds, stream, a);
+  return check_launch("egnn_layer_kernel");
+}
+
+int launch_tconv(bool first, const TconvArgs& a, hipStream_t stream) {
+  const size_t lds = (size_t)(64 * 64 * 2 * a.M + 2 * MMAX * TMAX + 4 * 2 * a.M * 64) * 4;
+  const int grid = (a.BN + 15) / 16;
+  ProfScope prof(first ? 3 : 2, stream);
+  if (first) {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute((const void*)tconv_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    hipLaunchKernelGGL(tconv_kernel<true>, dim3(grid), dim3(256), lds, stream, a);
+  } else {
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute((const void*)tconv_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    hipLaunchKernelGGL(tconv_kernel<false>, dim3(grid), dim3(256), lds, stream, a);
+  }
+  return check_launch("tconv_kernel");
+}
+
+int effective_modes(int T, int modes) {
+  const int half = T / 2 + 1;
+  return modes < half ? modes : half;
+}
+
+}  // namespace
+
+// ================================ C ABI ========================================================
+extern "C" {
+
+const char* nonode_version(void) { return "nonode-mi355x 0.1 (gfx950)"; }
+const char* nonode_last_error(void) { return g_err.c_str(); }
+size_t nonode_layer_blob_floats(void) { return BLOB_FLOATS; }
+
+int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
+                      float* blob, void* stream) {
+  if (!w || !blob) return fail(NONODE_EINVAL, "pack_layer: null pointer");
+  if (hidden != HID) return fail(NONODE_EUNSUPPORTED, "pack_layer: hidden=%d (only 64)", hidden);
+  if (n_edge_feat < 0 || n_edge_feat > 4) return fail(NONODE_EUNSUPPORTED, "pack_layer: n_edge_feat=%d", n_edge_feat);
+  if (!w->edge_w1 || !w->edge_b1 || !w->edge_w2 || !w->edge_b2 || !w->coord_w1 || !w->coord_b1 ||
+      !w->coord_w2 || !w->coord_b2 || !w->node_w1 || !w->node_b1 || !w->node_w2 || !w->node_b2)
+    return fail(NONODE_EINVAL, "pack_layer: missing weight pointer");
+  if (variant == NONODE_VARIANT_EGNO && (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2))
+    return fail(NONODE_EINVAL, "pack_layer: EGNO needs node_v_net weights");
+  PackArgs a;
+  a.ld1 = 2 * HID + 1 + n_edge_feat;
+  if (variant == NONODE_VARIANT_EGNO) { a.colS = 0; a.colA = 1; a.colB = 1 + HID; }       // [s,h_i,h_j,e]
+  else if (variant == NONODE_VARIANT_SEGNO) { a.colA = 0; a.colB = HID; a.colS = 2 * HID; }  // [h_i,h_j,s,e]
+  else return fail(NONODE_EINVAL, "pack_layer: variant %d", variant);
+  a.w1 = w->edge_w1; a.b1 = w->edge_b1; a.w2 = w->edge_w2; a.b2 = w->edge_b2;
+  a.cw1 = w->coord_w1; a.cb1 = w->coord_b1; a.cw2 = w->coord_w2; a.cb2 = w->coord_b2;
+  const bool egno = variant == NONODE_VARIANT_EGNO;
+  a.vw1 = egno ? w->vel_w1 : nullptr; a.vb1 = egno ? w->vel_b1 : nullptr;
+  a.vw2 = egno ? w->vel_w2 : nullptr; a.vb2 = egno ? w->vel_b2 : nullptr;
+  a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
+  a.ne = n_edge_feat;
+  a.blob = blob;
+  hipLaunchKernelGGL(pack_kernel, dim3(32, 8), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("pack_kernel");
+}
+
+int nonode_egno_tconv(int BN, int T, int modes, const float* h, const float* x, const float* v,
+                      const float* loc_mean, const float* tconv_w, const float* tconvx_w,
+                      float* h_out, float* x_out, float* v_out, void* stream) {
+  if (BN <= 0 || T <= 0 || T > TMAX || modes <= 0 || modes > MMAX)
+    return fail(NONODE_EUNSUPPORTED, "tconv: BN=%d T=%d modes=%d (T<=%d, modes<=%d)", BN, T, modes, TMAX, MMAX);
+  if (!h || !x || !v || !loc_mean || !tconv_w || !tconvx_w || !h_out || !x_out || !v_out)
+    return fail(NONODE_EINVAL, "tconv: null pointer");
+  TconvArgs a{};
+  a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
+  a.h = h; a.x = x; a.v = v; a.lm = loc_mean; a.w = tconv_w; a.wx = tconvx_w;
+  a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
+  return launch_tconv(false, a, (hipStream_t)stream);
+}
+
+int nonode_egnn_layer(int variant, int n_graphs, int N, int n_edge_feat, int ef_mod,
+                      const float* h, const float* x, const float* v, const float* edge_fea,
+                      const float* blob, float dt, float coords_weight, int recurrent,
+                      float* h_out, float* x_out, float* v_out, void* stream) {
+  if (n_graphs <= 0 || N < 2 || ef_mod <= 0 || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "egnn_layer: n_graphs=%d N=%d ef_mod=%d ne=%d", n_graphs, N, ef_mod, n_edge_feat);
+  if (!h || !x || !v || !blob || !h_out || !x_out || (n_edge_feat > 0 && !edge_fea))
+    return fail(NONODE_EINVAL, "egnn_layer: null pointer");
+  if (h_out == h || x_out == x) return fail(NONODE_EINVAL, "egnn_layer: outputs may not alias inputs");
+  if (variant == NONODE_VARIANT_EGNO)
+    return launch_layer<EGNO>(n_graphs, N, n_edge_feat, ef_mod, h, x, v, edge_fea, blob, dt, coords_weight,
+                              recurrent, h_out, x_out, v_out, (hipStream_t)stream);
+  if (variant == NONODE_VARIANT_SEGNO) {
+    if (!v_out || v_out == v) return fail(NONODE_EINVAL, "egnn_layer: SEGNO needs a distinct v_out");
+    return launch_layer<SEGNO>(n_graphs, N, n_edge_feat, ef_mod, h, x, v, edge_fea, blob, dt, coords_weight,
+                               recurrent, h_out, x_out, v_out, (hipStream_t)stream);
+  }
+  return fail(NONODE_EINVAL, "egnn_layer: variant %d", variant);
+}
+
+size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt) {
+  const size_t n = (size_t)B * N * T;
+  return (n * 64 + n * 3 + (size_t)Bt * T * 64 + 64) * sizeof(float);
+}
+
+int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                        int time_emb_dim, int modes, int Bt,
+                        const float* x, const float* h, const float* v, const float* loc_mean,
+                        const float* edge_fea, const float* t_out,
+                        const float* emb_w, const float* emb_b,
+                        const float* const* blobs, const float* const* tconv_w,
+                        const float* const* tconvx_w,
+                        float* x_out, float* v_out, float* h_out,
+                        void* workspace, size_t workspace_bytes, void* stream) {
+  if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || in_node < 0 || in_node > 8 ||
+      modes < 1 || modes > MMAX || time_emb_dim < 4 || time_emb_dim > 64 || (time_emb_dim & 1) ||
+      Bt <= 0 || (B * N) % Bt != 0)
+    return fail(NONODE_EUNSUPPORTED,
+                "egno_forward: B=%d N=%d T=%d layers=%d in_node=%d modes=%d temb=%d Bt=%d", B, N, T,
+                n_layers, in_node, modes, time_emb_dim, Bt);
+  if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_w || !tconvx_w ||
+      !x_out || !v_out || !h_out || !workspace)
+    return fail(NONODE_EINVAL, "egno_forward: null pointer");
+  if (workspace_bytes < nonode_egno_workspace_bytes(B, N, T, Bt))
+    return fail(NONODE_EINVAL, "egno_forward: workspace %zu < %zu", workspace_bytes,
+                nonode_egno_workspace_bytes(B, N, T, Bt));
+  hipStream_t s = (hipStream_t)stream;
+  const int BN = B * N;
+  const size_t n = (size_t)BN * T;
+  float* hB = (float*)workspace;
+  float* xB = hB + n * 64;
+  float* etab = xB + n * 3;
+  const int emb_ld = in_node + time_emb_dim;
+  {
+    const int tot = Bt * T * 64;
+    hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim,
+                       t_out, emb_w, emb_ld, emb_b, etab);
+    if (int rc = check_launch("temb_kernel")) return rc;
+  }
+  for (int l = 0; l < n_layers; ++l) {
+    TconvArgs a{};
+    a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
+    a.w = tconv_w[l]; a.wx = tconvx_w[l];
+    a.h_out = hB; a.x_out = xB; a.v_out = v_out;
+    if (l == 0) {
+      a.h = nullptr; a.x = x; a.v = v; a.lm = loc_mean;
+      a.hin = h; a.din = in_node; a.emb_w = emb_w; a.emb_ld = emb_ld; a.etab = etab; a.Bt = Bt;
+    } else {
+      a.h = h_out; a.x = x_out; a.v = v_out; a.lm = loc_mean;
+    }
+    if (int rc = launch_tconv(l == 0, a, s)) return rc;
+    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, B, hB, xB, v_out, edge_fea, blobs[l], 0.f, 1.f, 0,
+                                    h_out, x_out, nullptr, s))
+      return rc;
+  }
+  return NONODE_OK;
+}
+
+size_t nonode_segno_workspace_bytes(int B, int N) {
+  const size_t n = (size_t)B * N;
+  return (2 * n * 64 + 4 * n * 3 + 64) * sizeof(float);
+}
+
+int nonode_segno_forward_step(int B, int N, int T, int in_node, int n_edge_feat,
+                              const float* his, const float* h_in, const float* x, const float* v,
+                              const float* edge_attr, const float* emb_w, const float* emb_b,
+                              const float* blob, float coords_weight, int recurrent,
+                              float* x_out, float* v_out, float* h_out,
+                              void* workspace, size_t workspace_bytes, void* stream) {
+  if (B <= 0 || N < 2 || T < 0 || in_node < 0 || in_node > 8 || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "segno_forward_step: B=%d N=%d T=%d in_node=%d ne=%d", B, N, T, in_node,
+                n_edge_feat);
+  if (!x || !v || !blob || !x_out || !v_out || !h_out || !workspace || (!h_in && (!his || !emb_w || !emb_b)))
+    return fail(NONODE_EINVAL, "segno_forward_step: null pointer");
+  if (workspace_bytes < nonode_segno_workspace_bytes(B, N))
+    return fail(NONODE_EINVAL, "segno_forward_step: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)B * N;
+  float* hbuf[2] = {(float*)workspace, (float*)workspace + n * 64};
+  float* xbuf[2] = {hbuf[1] + n * 64, hbuf[1] + n * 64 + n * 3};
+  float* vbuf[2] = {xbuf[1] + n * 3, xbuf[1] + n * 6};
+  const float* hc = h_in;
+  if (!hc) {
+    hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, (int)n, in_node,
+                       his, emb_w, emb_b, hbuf[0]);
+    if (int rc = check_launch("embed_kernel")) return rc;
+    hc = hbuf[0];
+  }
+  if (T == 0) {
+    hipMemcpyAsync(h_out, hc, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+    hipMemcpyAsync(x_out, x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+    hipMemcpyAsync(v_out, v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+    return check_launch("segno T=0 copy");
+  }
+  const float* xc = x;
+  const float* vc = v;
+  const float dt = 1.0f / (float)T;
+  for (int it = 0; it < T; ++it) {
+    const bool last = it == T - 1;
+    float* ho = last ? h_out : (hc == hbuf[0] ? hbuf[1] : hbuf[0]);
+    float* xo = last ? x_out : (xc == xbuf[0] ? xbuf[1] : xbuf[0]);
+    float* vo = last ? v_out : (vc == vbuf[0] ? vbuf[1] : vbuf[0]);
+    if (int rc = launch_layer<SEGNO>(B, N, n_edge_feat, B, hc, xc, vc, edge_attr, blob, dt, coords_weight,
+                                     recurrent, ho, xo, vo, s))
+      return rc;
+    hc = ho; xc = xo; vc = vo;
+  }
+  return NONODE_OK;
+}
+
+int nonode_profile_begin(int max_records) {
+  std::lock_guard<std::mutex> lk(g_prof.mu);
+  if (max_records <= 0 || max_records > (1 << 20)) return fail(NONODE_EINVAL, "profile_begin: %d", max_records);
+  if (g_prof.ev) {
+    for (int i = 0; i < 2 * g_prof.cap; ++i) (void)hipEventDestroy(g_prof.ev[i]);
+    delete[] g_prof.ev;
+    delete[] g_prof.kind;
+  }
+  g_prof.ev = new hipEvent_t[2 * max_records];
+  g_prof.kind = new int[max_records];
+  for (int i = 0; i < 2 * max_records; ++i)
+    if (hipEventCreate(&g_prof.ev[i]) != hipSuccess) return fail(NONODE_ELAUNCH, "profile_begin: hipEventCreate");
+  g_prof.cap = max_records;
+  g_prof.n = 0;
+  g_prof.on = true;
+  return NONODE_OK;
+}
+
+int nonode_profile_end(float* ms_out, int* kind_out, int max_out) {
+  std::lock_guard<std::mutex> lk(g_prof.mu);
+  g_prof.on = false;
+  const int n = g_prof.n < max_out ? g_prof.n : max_out;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(g_prof.ev[2 * i + 1]) != hipSuccess) return -fail(NONODE_ELAUNCH, "profile_end: sync");
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, g_prof.ev[2 * i], g_prof.ev[2 * i + 1]);
+    if (ms_out) ms_out[i] = ms;
+    if (kind_out) kind_out[i] = g_prof.kind[i];
+  }
+  g_prof.n = 0;
+  return n;
+}
+
+}  // extern "C"
+

@@ -1,0 +1,152 @@
+"""Drop-in SEGNO (SEGNO/models/model.py:6-102) on the gfx950 kernels in libnonode.so.
+
+Same constructor and forward signatures, return order (x, h, v), state_dict keys, and RNG
+consumption order in __init__ (model.py:10-25, gcl.py:27-69).
+
+Semantics note: the reference's live ``forward`` (model.py:53-92)
+discards the integrator result for a single input and returns its inputs. This class returns
+the integrator result (what the shadowed forward at model.py:28-51 and ``forward_step`` compute);
+``bug_compat=True`` reproduces the reference's identity behaviour exactly.
+"""
+import ctypes
+
+import torch
+from torch import nn
+
+from . import _lib
+from .graph import check_full_graph
+
+
+class GCLParams(nn.Module):
+    """Parameters of SEGNO_GCL (gcl.py:26-69) in its registration and RNG order."""
+
+    def __init__(self, input_nf, output_nf, hidden_nf, edges_in_d=0, act_fn=nn.SiLU()):
+        super().__init__()
+        self.edge_mlp = nn.Sequential(nn.Linear(2 * input_nf + 1 + edges_in_d, hidden_nf), act_fn,
+                                      nn.Linear(hidden_nf, hidden_nf), act_fn)
+        self.node_mlp = nn.Sequential(nn.Linear(hidden_nf + input_nf, hidden_nf), act_fn,
+                                      nn.Linear(hidden_nf, output_nf))
+        layer = nn.Linear(hidden_nf, 1, bias=True)
+        torch.nn.init.xavier_uniform_(layer.weight, gain=0.001)
+        self.coord_mlp = nn.Sequential(nn.Linear(hidden_nf, hidden_nf), act_fn, layer)
+        # coord_mlp_vel exists in the reference state_dict but is never used in forward
+        self.coord_mlp_vel = nn.Sequential(nn.Linear(input_nf, hidden_nf), act_fn, nn.Linear(hidden_nf, 1))
+
+    def weight_struct(self):
+        e, c, n = self.edge_mlp, self.coord_mlp, self.node_mlp
+        ptrs = [e[0].weight, e[0].bias, e[2].weight, e[2].bias, c[0].weight, c[0].bias, c[2].weight,
+                c[2].bias, None, None, None, None, n[0].weight, n[0].bias, n[2].weight, n[2].bias]
+        return _lib.LayerWeights(*[t.data_ptr() if t is not None else None for t in ptrs])
+
+
+class SEGNO(nn.Module):
+    """SEGNO neural ODE (model.py:6-102) — drop-in, MI355X kernels underneath.
+
+    Supported: single input (x of shape [BN, 3]), SiLU, tanh=False, norm_diff=False,
+    hidden_nf=64, in_edge_nf <= 4. ``multiple_agg`` is accepted; num_inputs > 1 inputs raise.
+    """
+
+    def __init__(self, in_node_nf, in_edge_nf, hidden_nf, device='cpu', act_fn=nn.SiLU(), n_layers=4,
+                 coords_weight=1.0, recurrent=False, norm_diff=False, tanh=False, invariant=True,
+                 norm_vel=True, varDT=False, multiple_agg=None, bug_compat=False):
+        super().__init__()
+        unsupported = []
+        if hidden_nf != 64:
+            unsupported.append(f"hidden_nf={hidden_nf}")
+        if tanh:
+            unsupported.append("tanh=True")
+        if norm_diff:
+            unsupported.append("norm_diff=True")
+        if not isinstance(act_fn, nn.SiLU):
+            unsupported.append(f"act_fn={act_fn}")
+        if in_edge_nf > 4 or in_node_nf > 8:
+            unsupported.append(f"in_edge_nf={in_edge_nf}, in_node_nf={in_node_nf}")
+        if multiple_agg not in (None, "attn", "sum"):
+            raise ValueError("Invalid multiple aggregation method specified.")
+        if unsupported:
+            raise NotImplementedError("SEGNO (MI355X kernels) does not implement " + ", ".join(unsupported))
+        self.hidden_nf = hidden_nf
+        self.varDT = varDT
+        self.multiple_agg = multiple_agg
+        if multiple_agg == "attn":
+            # InvariantTemporalAttention parameters (model.py:126-139), created first as in the
+            # reference so the RNG stream matches; the multi-input path itself is not implemented
+            self.enc_attn_net = nn.Module()
+            self.enc_attn_net.attn_mlp = nn.Sequential(nn.Linear(hidden_nf + 1, hidden_nf), nn.Tanh(),
+                                                       nn.Linear(hidden_nf, 1))
+        self.device = device
+        self.n_layers = n_layers
+        self.embedding = nn.Linear(in_node_nf, hidden_nf)
+        self.invariant = invariant
+        self.norm_vel = norm_vel
+        self.sigmoid = nn.Sigmoid()
+        self.module = GCLParams(hidden_nf, hidden_nf, hidden_nf, edges_in_d=in_edge_nf, act_fn=act_fn)
+        self.coords_weight = coords_weight
+        self.recurrent = recurrent
+        self.in_node_nf = in_node_nf
+        self.in_edge_nf = in_edge_nf
+        self.bug_compat = bug_compat
+        self._blob = None
+        self._blob_key = None
+        self.to(device)
+
+    def _packed(self):
+        params = list(self.module.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._blob is not None and key == self._blob_key:
+            return self._blob
+        L = _lib.lib()
+        blob = torch.empty(L.nonode_layer_blob_floats(), dtype=torch.float32, device=self.embedding.weight.device)
+        w = self.module.weight_struct()
+        _lib.check(L.nonode_pack_layer(ctypes.byref(w), _lib.VARIANT_SEGNO, self.hidden_nf, self.in_edge_nf,
+                                       _lib.ptr(blob), _lib.stream_of(blob)))
+        self._blob, self._blob_key = blob, key
+        return blob
+
+    def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
+        """model.py:53-92 (single input). his [BN, in_node_nf], x, v [BN, 3], edges 2 x [E],
+        edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T."""
+        if x.dim() == 3:
+            raise NotImplementedError("SEGNO multi-input (num_inputs > 1) path is not implemented")
+        if self.bug_compat:
+            # the live reference forward returns its inputs (and the embedded h)
+            return x, self._embed(his), v
+        return self._run(his, None, x, edges, v, edge_attr, int(T))
+
+    def forward_step(self, h, x, edges, v, edge_attr, T=10):
+        """model.py:95-102: T substeps of the shared layer from an already-embedded h."""
+        self.module.n_layers = T
+        self.n_layers = T
+        out = self._run(None, h, x, edges, v, edge_attr, int(T))
+        return out
+
+    def _embed(self, his):
+        _lib.require_device(his, self.embedding.weight)
+        with torch.no_grad():
+            return torch.nn.functional.linear(his, self.embedding.weight, self.embedding.bias)
+
+    @torch.no_grad()
+    def _run(self, his, h_in, x, edges, v, edge_attr, T):
+        _lib.require_device(x, v, edge_attr, self.embedding.weight)
+        BN = x.shape[0]
+        B, N = check_full_graph(edges, BN)
+        if edge_attr.shape != (B * N * (N - 1), self.in_edge_nf):
+            raise ValueError(f"edge_attr must be [{B * N * (N - 1)}, {self.in_edge_nf}]")
+        f32 = lambda t: t.detach().to(torch.float32).contiguous() if t is not None else None  # noqa: E731
+        x, v, ea = f32(x), f32(v), f32(edge_attr)
+        his, h_in = f32(his), f32(h_in)
+        dev = x.device
+        blob = self._packed()
+        x_out = torch.empty(BN, 3, device=dev)
+        v_out = torch.empty(BN, 3, device=dev)
+        h_out = torch.empty(BN, self.hidden_nf, device=dev)
+        L = _lib.lib()
+        ws_bytes = L.nonode_segno_workspace_bytes(B, N)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+        ew, eb = f32(self.embedding.weight), f32(self.embedding.bias)
+        _lib.check(L.nonode_segno_forward_step(
+            B, N, T, self.in_node_nf, self.in_edge_nf, _lib.ptr(his), _lib.ptr(h_in), _lib.ptr(x), _lib.ptr(v),
+            _lib.ptr(ea), _lib.ptr(ew), _lib.ptr(eb), _lib.ptr(blob), float(self.coords_weight),
+            int(bool(self.recurrent)), _lib.ptr(x_out), _lib.ptr(v_out), _lib.ptr(h_out), _lib.ptr(ws),
+            ws_bytes, _lib.stream_of(x)))
+        return x_out, h_out, v_out

@@ -1,0 +1,344 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Test infrastructure only. This script imports simone7monaco/NO-NODE-comparison from
+/root/reference (available in the build container, never on the GPU box) and records
+inputs, weights and outputs as small .npz files. The fixtures are data; no reference
+source is copied. Re-run with:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What each fixture pins (reference file:line):
+  egno_fwd.npz        EGNO.forward (EGNO/model/egno.py:37-111) at B=4,N=20,T=10, plus the
+                      per-layer states after TimeConv / TimeConv_x / EGNN_Layer
+                      (layer_no.py:112-178, basic.py:167-186) and the timestep embedding
+                      (layer_no.py:8-17). Inputs come from the reference ChargedParticlesSim
+                      (synthetic_sim.py:220-296, np seed 43) through prepare_inputs
+                      (main_simulation_simple_no.py:311-339).
+  egno_rollout.npz    rollout_fn (main_simulation_simple_no.py:342-384), 2 segments, with the
+                      per-frame conserved energy (utils.py:126-144,197-219).
+  egno_grad.npz       one training step's loss + parameter gradients
+                      (main_simulation_simple_no.py:267-280).
+  segno_fwd.npz       SEGNO_GCL.forward (gcl.py:111-119), SEGNO.forward_step T=10
+                      (model.py:95-102) and the live SEGNO.forward (model.py:53-92).
+  segno_rollout.npz   train_nbody.rollout_fn (train_nbody.py:200-236), 2 segments, driven
+                      through forward_step (the integrator the shadowed forward intends).
+  segno_gravity.npz   forward_step at N=100, B=2, T=5 on GravitySim-style inputs
+                      (synthetic_sim.py:360-404).
+  init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
+                      torch.manual_seed(0) (RNG-consumption order of the constructors).
+"""
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+import numpy as np
+import torch
+
+torch.set_num_threads(8)
+
+
+# ---------------------------------------------------------------------------------
+# Stubs for the reference's non-arithmetic dependencies that are not installed here.
+# torch_geometric is used only for equal-size to_dense_batch reshapes and the Data
+# container; wandb only for logging.
+# ---------------------------------------------------------------------------------
+def _to_dense_batch(x, batch):
+    B = int(batch.max().item()) + 1
+    n = x.shape[0] // B
+    out = x.reshape(B, n, *x.shape[1:])
+    return out, torch.ones(B, n, dtype=torch.bool)
+
+
+tg = types.ModuleType("torch_geometric")
+tg_utils = types.ModuleType("torch_geometric.utils")
+tg_utils.to_dense_batch = _to_dense_batch
+tg_data = types.ModuleType("torch_geometric.data")
+tg_data.Data = dict
+tg.utils, tg.data = tg_utils, tg_data
+sys.modules.update({"torch_geometric": tg, "torch_geometric.utils": tg_utils,
+                    "torch_geometric.data": tg_data})
+wb = types.ModuleType("wandb")
+wb.log = lambda *a, **k: None
+sys.modules["wandb"] = wb
+
+sys.path.insert(0, REF)
+import utils as ref_utils  # noqa: E402  (root utils.py)
+import EGNO.utils as egno_utils  # noqa: E402
+
+egno_utils.random_ascending_tensor = ref_utils.random_ascending_tensor
+from EGNO.model.egno import EGNO  # noqa: E402
+from EGNO.model.layer_no import get_timestep_embedding  # noqa: E402
+import EGNO.main_simulation_simple_no as egno_main  # noqa: E402
+from synthetic_sim import ChargedParticlesSim  # noqa: E402
+
+sys.path.insert(0, os.path.join(REF, "SEGNO"))
+from models.model import SEGNO  # noqa: E402
+import train_nbody as segno_train  # noqa: E402  (SEGNO/train_nbody.py)
+
+
+def _np(t):
+    return t.detach().cpu().numpy().copy()
+
+
+def _sd(model, prefix="w::"):
+    return {prefix + k: _np(v) for k, v in model.state_dict().items()}
+
+
+def full_edges(B, N):
+    """Same edge list as dataset_simple.py:64-71 + get_edges 101-111."""
+    rows, cols = [], []
+    for i in range(N):
+        for j in range(N):
+            if i != j:
+                rows.append(i)
+                cols.append(j)
+    r = torch.tensor(rows)
+    c = torch.tensor(cols)
+    return [torch.cat([r + N * b for b in range(B)]), torch.cat([c + N * b for b in range(B)])]
+
+
+def charged_trajectories(S, N, T=6000, freq=100, seed=43):
+    np.random.seed(seed)
+    sim = ChargedParticlesSim(n_balls=N, box_size=5.0, noise_var=0.0, vel_norm=0.5)
+    locs, vels, charges = [], [], []
+    for _ in range(S):
+        loc, vel, edges, q = sim.sample_trajectory(T=T, sample_freq=freq)
+        locs.append(loc)
+        vels.append(vel)
+        charges.append(q)
+    # on-disk layout [S, frames, 3, N] -> loader transposes to [S, frames, N, 3]
+    loc = np.ascontiguousarray(np.transpose(np.stack(locs), (0, 1, 3, 2)).astype(np.float32))
+    vel = np.ascontiguousarray(np.transpose(np.stack(vels), (0, 1, 3, 2)).astype(np.float32))
+    q = np.stack(charges).astype(np.float32)  # [S, N, 1]
+    return loc, vel, q
+
+
+def edge_attr_o(q):
+    """q_i q_j per edge in (i, j != i) order, as dataset_simple.py:46-48,64-72."""
+    S, N, _ = q.shape
+    out = []
+    for s in range(S):
+        qq = q[s, :, 0]
+        out.append([qq[i] * qq[j] for i in range(N) for j in range(N) if i != j])
+    return torch.tensor(np.array(out, dtype=np.float32)).unsqueeze(-1)  # [S, N(N-1), 1]
+
+
+def make_egno(B=4, N=20, T=10, traj_len=2):
+    loc_all, vel_all, q = charged_trajectories(B, N)
+    start = 30
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start]))
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start]))
+    charges = torch.tensor(q)
+    eao = edge_attr_o(q).reshape(-1, 1)
+    edges = full_edges(B, N)
+    loc_p, vel_p, edge_attr, nodes, loc_mean = egno_main.prepare_inputs(
+        loc, vel, eao, edges, N, 1, charges)
+    t_out = torch.arange(1, T + 1).repeat(B, 1)  # out_indices - in_indices.max()
+    t_in = torch.zeros(B, dtype=torch.long)
+
+    torch.manual_seed(0)
+    model = EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True,
+                 num_modes=2, num_timesteps=T, time_emb_dim=32)
+    model.eval()
+
+    # per-layer capture via forward hooks (EGNO/model/egno.py:99-110)
+    cap = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            if isinstance(out, tuple):
+                for k, o in enumerate(out):
+                    cap[f"{name}.out{k}"] = _np(o)
+            else:
+                cap[f"{name}.out"] = _np(out)
+            cap[f"{name}.in0"] = _np(inp[0])
+        return f
+
+    for i in range(4):
+        model.time_conv_modules[i].register_forward_hook(hook(f"tconv{i}"))
+        model.time_conv_x_modules[i].register_forward_hook(hook(f"tconvx{i}"))
+        model.layers[i].register_forward_hook(hook(f"layer{i}"))
+    model.embedding.register_forward_hook(hook("embedding"))
+
+    with torch.no_grad():
+        x_out, v_out, h_out = model(loc_p, nodes, edges, edge_attr, v=vel_p, loc_mean=loc_mean,
+                                    timesteps_in=t_in, timesteps_out=t_out)
+    temb = get_timestep_embedding(t_out, embedding_dim=32, max_positions=10000)
+
+    fx = dict(_sd(model))
+    fx.update({f"cap::{k}": v for k, v in cap.items()})
+    fx.update({
+        "cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T),
+        "raw::loc": loc_all[:, start], "raw::vel": vel_all[:, start], "raw::charges": q,
+        "raw::edge_attr_o": _np(eao),
+        "in::x": _np(loc_p), "in::h": _np(nodes), "in::v": _np(vel_p),
+        "in::loc_mean": _np(loc_mean), "in::edge_attr": _np(edge_attr),
+        "in::row": _np(edges[0]), "in::col": _np(edges[1]),
+        "in::t_out": _np(t_out), "in::t_in": _np(t_in),
+        "out::x": _np(x_out), "out::v": _np(v_out), "out::h": _np(h_out),
+        "out::temb": _np(temb),
+        "truth::locs_out": loc_all[:, start + 1:start + 1 + T * traj_len],  # [B, T*traj, N, 3]
+        "truth::vels_out": vel_all[:, start + 1:start + 1 + T * traj_len],
+    })
+    np.savez_compressed(os.path.join(HERE, "egno_fwd.npz"), **fx)
+
+    # ---- rollout (main_simulation_simple_no.py:342-384) with conserved energy ----
+    class _DS:  # energy_fun as dataset_simple.py:33-34
+        dataset = "charged"
+
+        def energy_fun(self, loc, vel, edges, batch=None):
+            return ref_utils.conserved_energy_fun("charged", loc, vel, edges, batch=batch)
+
+    t_out_full = torch.arange(1, T * traj_len + 1).repeat(B, 1)
+    with torch.no_grad():
+        preds, energies, energies_all = egno_main.rollout_fn(
+            model, nodes, loc_p, edges, vel_p, eao, edge_attr, loc_mean, N, traj_len, B,
+            charges=charges, num_steps=T, timesteps_in=t_in.clone(),
+            timesteps_out=t_out_full.clone(), energy_fun=_DS().energy_fun)
+    np.savez_compressed(os.path.join(HERE, "egno_rollout.npz"), **{
+        "cfg::traj_len": np.array(traj_len),
+        "out::loc_preds": _np(preds), "out::energies": _np(energies),
+        "out::energies_allsteps": _np(energies_all),
+    })
+
+    # ---- one training step gradient (main_simulation_simple_no.py:267-280) ----
+    model.train()
+    model.zero_grad()
+    loc_true = torch.tensor(loc_all[:, start + 1:start + 1 + T]).transpose(1, 2)  # [B,N,T,3]
+    crit = torch.nn.MSELoss(reduction="none")
+    loc_pred, _, _ = model(loc_p, nodes, edges, edge_attr, v=vel_p, loc_mean=loc_mean,
+                           timesteps_in=t_in, timesteps_out=t_out)
+    loc_pred = loc_pred.reshape(T, -1, 3).transpose(0, 1)
+    loc_pred = _to_dense_batch(loc_pred, torch.arange(B).repeat_interleave(N))[0]
+    losses = crit(loc_pred, loc_true[:, :, :loc_pred.size(2)]).mean((0, 1, 3))
+    loss = losses.mean()
+    loss.backward()
+    # parameters that do not reach the loss (layers.3.node_net: the last h is unused) get
+    # grad None in torch; they are recorded as zeros.
+    g = {"grad::" + k: (_np(p.grad) if p.grad is not None else np.zeros(tuple(p.shape), np.float32))
+         for k, p in model.named_parameters()}
+    g["nograd"] = np.array([k for k, p in model.named_parameters() if p.grad is None])
+    g["out::loss"] = _np(loss)
+    g["out::losses"] = _np(losses)
+    g["in::loc_true"] = _np(loc_true)
+    np.savez_compressed(os.path.join(HERE, "egno_grad.npz"), **g)
+    return model
+
+
+def make_segno(B=4, N=20, T=10):
+    loc_all, vel_all, q = charged_trajectories(B, N, seed=44)
+    start = 30
+    edges = full_edges(B, N)
+    rows, cols = edges
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start])).reshape(-1, 3)
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start])).reshape(-1, 3)
+    charges = torch.tensor(q).reshape(-1, 1)
+    prod = charges[rows] * charges[cols]
+    h = torch.sqrt(torch.sum(vel ** 2, dim=1)).unsqueeze(-1)  # train_nbody.py:121
+    loc_dist = torch.sum((loc[rows] - loc[cols]) ** 2, 1).unsqueeze(1)
+    edge_attr = torch.cat([prod, loc_dist], 1)  # train_nbody.py:123
+
+    torch.manual_seed(0)
+    model = SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True,
+                  norm_diff=False, tanh=False, device="cpu", varDT=False, multiple_agg=None)
+    model.eval()
+    edge_index = torch.stack(edges)
+    with torch.no_grad():
+        h_emb = model.embedding(h)
+        model.module.n_layers = T
+        gcl_h, gcl_x, gcl_v, _ = model.module(h_emb, edge_index, loc, vel, vel, edge_attr=edge_attr)
+        fs_x, fs_h, fs_v = model.forward_step(h_emb, loc, edge_index, vel, edge_attr, T=T)
+        fw_x, fw_h, fw_v = model(h, loc, edges, vel, edge_attr, T=T)
+    fx = dict(_sd(model))
+    fx.update({
+        "cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T),
+        "raw::charges": q,
+        "in::x": _np(loc), "in::v": _np(vel), "in::his": _np(h), "in::edge_attr": _np(edge_attr),
+        "in::row": _np(rows), "in::col": _np(cols), "in::h_emb": _np(h_emb),
+        "gcl::h": _np(gcl_h), "gcl::x": _np(gcl_x), "gcl::v": _np(gcl_v),
+        "step::x": _np(fs_x), "step::h": _np(fs_h), "step::v": _np(fs_v),
+        "fwd::x": _np(fw_x), "fwd::h": _np(fw_h), "fwd::v": _np(fw_v),
+    })
+    np.savez_compressed(os.path.join(HERE, "segno_fwd.npz"), **fx)
+
+    # ---- rollout through the integrator (train_nbody.py:200-236) ----
+    class _Integrator(torch.nn.Module):
+        """Routes the reference rollout_fn through SEGNO.forward_step (model.py:95-102)."""
+
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
+            hh = self.m.embedding(his)
+            xo, ho, vo = self.m.forward_step(hh, x, edges, v, edge_attr, T=T)
+            return xo, ho, vo
+
+    batch = torch.arange(B).repeat_interleave(N)
+    with torch.no_grad():
+        preds, energies = segno_train.rollout_fn(
+            _Integrator(model), h, loc, edge_index, vel, edge_attr, batch, 2,
+            num_steps=[T, T // 2], num_prev=1, charges=charges,
+            energy_fun=lambda l, v, e, batch=None: ref_utils.conserved_energy_fun(
+                "charged", l, v, e, batch=batch))
+    np.savez_compressed(os.path.join(HERE, "segno_rollout.npz"), **{
+        "cfg::num_steps": np.array([T, T // 2]),
+        "out::loc_preds": _np(preds), "out::energies": _np(energies)})
+
+
+def make_segno_gravity(B=2, N=100, T=5):
+    rng = np.random.RandomState(7)
+    # GravitySim init (synthetic_sim.py:370-378): masses, positions, velocities, COM removed
+    mass = (1.0 + 0.1 * rng.randn(B, N, 1)).astype(np.float32)
+    pos = rng.randn(B, N, 3).astype(np.float32)
+    vel = rng.randn(B, N, 3).astype(np.float32)
+    vel -= (mass * vel).sum(1, keepdims=True) / mass.sum(1, keepdims=True)
+    edges = full_edges(B, N)
+    rows, cols = edges
+    loc = torch.tensor(pos).reshape(-1, 3)
+    v = torch.tensor(vel).reshape(-1, 3)
+    m = torch.tensor(mass).reshape(-1, 1)
+    prod = m[rows] * m[cols]
+    h = torch.sqrt(torch.sum(v ** 2, dim=1)).unsqueeze(-1)
+    loc_dist = torch.sum((loc[rows] - loc[cols]) ** 2, 1).unsqueeze(1)
+    edge_attr = torch.cat([prod, loc_dist], 1)
+    torch.manual_seed(1)
+    model = SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True,
+                  norm_diff=False, tanh=False, device="cpu")
+    with torch.no_grad():
+        hh = model.embedding(h)
+        xo, ho, vo = model.forward_step(hh, loc, torch.stack(edges), v, edge_attr, T=T)
+    fx = dict(_sd(model))
+    fx.update({"cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T),
+               "in::x": _np(loc), "in::v": _np(v), "in::his": _np(h),
+               "in::edge_attr": _np(edge_attr), "in::mass": mass,
+               "step::x": _np(xo), "step::h": _np(ho), "step::v": _np(vo)})
+    np.savez_compressed(os.path.join(HERE, "segno_gravity.npz"), **fx)
+
+
+def make_init():
+    torch.manual_seed(0)
+    e = EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+             num_timesteps=10, time_emb_dim=32)
+    torch.manual_seed(0)
+    s = SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True,
+              norm_diff=False, tanh=False)
+    fx = _sd(e, "egno::")
+    fx.update(_sd(s, "segno::"))
+    np.savez_compressed(os.path.join(HERE, "init_seed0.npz"), **fx)
+
+
+if __name__ == "__main__":
+    make_egno()
+    make_segno()
+    make_segno_gravity()
+    make_init()
+    with open(os.path.join(HERE, "PROVENANCE.txt"), "w") as f:
+        f.write(f"generated by tests/golden/make_golden.py\n"
+                f"reference snapshot: /root/reference (simone7monaco/NO-NODE-comparison 2025-07-04)\n"
+                f"torch {torch.__version__}, numpy {np.__version__}, CPU fp32, 8 threads\n")
+    print("golden fixtures written to", HERE)

@@ -1,0 +1,151 @@
+"""Pin the numpy oracle to fixtures recorded from the reference itself (CPU only)."""
+import numpy as np
+import pytest
+
+from oracle import egno as oe
+from oracle import harness as oh
+from oracle import segno as osg
+from tests.conftest import load_golden, maxnorm_rel, params_of
+
+TOL32 = 1e-5   # SURVEY §8d parity bound (max-norm relative, fp32)
+
+
+@pytest.fixture(scope="module")
+def egno_fx():
+    return load_golden("egno_fwd")
+
+
+@pytest.fixture(scope="module")
+def segno_fx():
+    return load_golden("segno_fwd")
+
+
+def _egno_inputs(fx, dtype=np.float32):
+    c = lambda k: fx[k].astype(dtype)  # noqa: E731
+    return dict(x=c("in::x"), h=c("in::h"), row=fx["in::row"], col=fx["in::col"],
+                edge_fea=c("in::edge_attr"), v=c("in::v"), loc_mean=c("in::loc_mean"),
+                t_out=fx["in::t_out"])
+
+
+def test_timestep_embedding(egno_fx):
+    got = oe.timestep_embedding(egno_fx["in::t_out"], 32)
+    assert maxnorm_rel(got, egno_fx["out::temb"]) < 1e-6
+
+
+def test_prepare_inputs(egno_fx):
+    fx = egno_fx
+    B, N = int(fx["cfg::B"]), int(fx["cfg::N"])
+    row, col = oh.full_edges(B, N)
+    assert np.array_equal(row, fx["in::row"]) and np.array_equal(col, fx["in::col"])
+    loc, vel, ea, nodes, lm = oh.prepare_inputs(fx["raw::loc"], fx["raw::vel"], fx["raw::edge_attr_o"],
+                                                row, col, N, fx["raw::charges"])
+    for got, key in [(loc, "in::x"), (vel, "in::v"), (ea, "in::edge_attr"), (nodes, "in::h"),
+                     (lm, "in::loc_mean")]:
+        assert maxnorm_rel(got, fx[key]) < 1e-6, key
+
+
+def test_spectral_layers_match(egno_fx):
+    fx = egno_fx
+    p = params_of(fx)
+    for i in range(4):
+        h_in = fx[f"cap::tconv{i}.in0"]
+        got = oe.time_conv(h_in, p[f"time_conv_modules.{i}.t_conv.weights1"])
+        assert maxnorm_rel(got, fx[f"cap::tconv{i}.out"]) < 1e-6
+        X = fx[f"cap::tconvx{i}.in0"]
+        got = oe.time_conv_x(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
+        assert maxnorm_rel(got, fx[f"cap::tconvx{i}.out"]) < 1e-6
+
+
+@pytest.mark.parametrize("dtype,tol", [(np.float32, TOL32), (np.float64, TOL32)])
+def test_egno_forward(egno_fx, dtype, tol):
+    fx = egno_fx
+    p = {k: v.astype(dtype) for k, v in params_of(fx).items()}
+    cap = {}
+    x, v, h = oe.egno_forward(p, **_egno_inputs(fx, dtype), capture=cap)
+    assert maxnorm_rel(x, fx["out::x"]) < tol
+    assert maxnorm_rel(v, fx["out::v"]) < tol
+    assert maxnorm_rel(h, fx["out::h"]) < tol
+    for i in range(4):
+        for k, got in enumerate(cap[f"layer{i}"]):
+            assert maxnorm_rel(got, fx[f"cap::layer{i}.out{k}"]) < tol
+
+
+def test_egno_rollout_two_segments(egno_fx):
+    fx = egno_fx
+    ro = load_golden("egno_rollout")
+    p = params_of(fx)
+    B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
+    L = int(ro["cfg::traj_len"])
+    t_full = np.tile(np.arange(1, T * L + 1), (B, 1))
+    preds, en, en_all = oh.egno_rollout(
+        p, fx["in::h"], fx["in::x"], fx["in::row"], fx["in::col"], fx["in::v"],
+        fx["raw::edge_attr_o"], fx["in::edge_attr"], fx["in::loc_mean"], N, L, B,
+        fx["raw::charges"], T=T, t_out=t_full)
+    # segment 0 is a plain forward; segment 1 starts from a chaotic state
+    assert maxnorm_rel(preds[:T], ro["out::loc_preds"][:T]) < TOL32
+    assert maxnorm_rel(preds, ro["out::loc_preds"]) < 1e-4
+    assert maxnorm_rel(en_all[:T], ro["out::energies_allsteps"][:T]) < 1e-4
+
+
+def test_egno_loss_matches(egno_fx):
+    fx = egno_fx
+    g = load_golden("egno_grad")
+    p = params_of(fx)
+    B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
+    x, _, _ = oe.egno_forward(p, **_egno_inputs(fx))
+    pred = x.reshape(T, B * N, 3).transpose(1, 0, 2).reshape(B, N, T, 3)
+    losses = ((pred - g["in::loc_true"]) ** 2).mean(axis=(0, 1, 3))
+    assert maxnorm_rel(losses, g["out::losses"]) < TOL32
+    assert abs(losses.mean() - float(g["out::loss"])) / float(g["out::loss"]) < TOL32
+
+
+def test_segno_gcl_and_forward_step(segno_fx):
+    fx = segno_fx
+    p = params_of(fx)
+    T = int(fx["cfg::T"])
+    row, col = fx["in::row"], fx["in::col"]
+    h, x, v = osg.gcl_forward(p, fx["in::h_emb"], row, col, fx["in::x"], fx["in::v"],
+                              fx["in::edge_attr"], n_layers=T, dense_mean=True)
+    assert maxnorm_rel(h, fx["gcl::h"]) < TOL32
+    assert maxnorm_rel(x, fx["gcl::x"]) < TOL32
+    assert maxnorm_rel(v, fx["gcl::v"]) < TOL32
+    for dense in (True, False):
+        x, h, v = osg.forward_step(p, fx["in::h_emb"], fx["in::x"], row, col, fx["in::v"],
+                                   fx["in::edge_attr"], T=T, dense_mean=dense)
+        assert maxnorm_rel(x, fx["step::x"]) < TOL32
+        assert maxnorm_rel(v, fx["step::v"]) < TOL32
+        assert maxnorm_rel(h, fx["step::h"]) < TOL32
+
+
+def test_segno_forward_bug_compat(segno_fx):
+    fx = segno_fx
+    p = params_of(fx)
+    x, h, v = osg.forward(p, fx["in::his"], fx["in::x"], fx["in::row"], fx["in::col"], fx["in::v"],
+                          fx["in::edge_attr"], T=int(fx["cfg::T"]), bug_compat=True)
+    assert np.array_equal(x, fx["fwd::x"]) and np.array_equal(v, fx["fwd::v"])
+    assert maxnorm_rel(h, fx["fwd::h"]) < 1e-6
+
+
+def test_segno_rollout(segno_fx):
+    fx = segno_fx
+    ro = load_golden("segno_rollout")
+    p = params_of(fx)
+    B = int(fx["cfg::B"])
+    preds, en = oh.segno_rollout(p, fx["in::his"], fx["in::x"], fx["in::row"], fx["in::col"],
+                                 fx["in::v"], fx["in::edge_attr"], 2, list(ro["cfg::num_steps"]),
+                                 fx["raw::charges"], B)
+    assert maxnorm_rel(preds, ro["out::loc_preds"]) < TOL32
+    assert maxnorm_rel(en, ro["out::energies"]) < 1e-4
+
+
+def test_segno_gravity_n100():
+    fx = load_golden("segno_gravity")
+    p = params_of(fx)
+    B, N = int(fx["cfg::B"]), int(fx["cfg::N"])
+    row, col = oh.full_edges(B, N)
+    hh = oe.linear(fx["in::his"], p, "embedding")
+    x, h, v = osg.forward_step(p, hh, fx["in::x"], row, col, fx["in::v"], fx["in::edge_attr"],
+                               T=int(fx["cfg::T"]))
+    assert maxnorm_rel(x, fx["step::x"]) < TOL32
+    assert maxnorm_rel(v, fx["step::v"]) < TOL32
+    assert maxnorm_rel(h, fx["step::h"]) < TOL32
