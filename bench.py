@@ -157,7 +157,7 @@ def run_egno(args, world, rank, dev):
         achieved = flop / (avg_ms * 1e-3) / 1e12
         res["roofline"] = {"kernel": "egnn_layer_kernel<EGNO>", "bound": "mfma", "achieved": achieved,
                            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-                           "traffic": pmc_traffic("egnn_layer_kernel"), "avg_launch_ms": avg_ms,
+                           "traffic": pmc_traffic("egnn_layer_kernel<EGNO>"), "avg_launch_ms": avg_ms,
                            "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(durs),
                            "tconv_avg_launch_ms": float(np.mean(tconv_ms)) if tconv_ms else None}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
