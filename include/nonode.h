@@ -84,7 +84,7 @@ size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt);
  *   t_out [Bt][T] (float; row b' feeds node rows r with r % Bt == b', egno.py:66);
  *   emb_w [64][in_node+time_emb_dim], emb_b [64];
  *   blobs[l]   (host array of device ptrs) packed layers from nonode_pack_layer(EGNO);
- *   tconv_w[l] (host array) time_conv_modules.l.t_conv.weights1   [64][64][modes][2];
+ *   tconv_blobs[l] (host array) time_conv_modules.l.t_conv.weights1 packed by nonode_pack_tconv;
  *   tconvx_w[l](host array) time_conv_x_modules.l.t_conv.weights1 [2][2][modes][2];
  *   outputs x_out, v_out [T*B*N][3], h_out [T*B*N][64] (time-major, egno.py:89-96).
  * Limits: N >= 2, T <= 16, modes <= 4, time_emb_dim even <= 64, in_node <= 8.
@@ -94,7 +94,7 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
                         const float* x, const float* h, const float* v, const float* loc_mean,
                         const float* edge_fea, const float* t_out,
                         const float* emb_w, const float* emb_b,
-                        const float* const* blobs, const float* const* tconv_w,
+                        const float* const* blobs, const float* const* tconv_blobs,
                         const float* const* tconvx_w,
                         float* x_out, float* v_out, float* h_out,
                         void* workspace, size_t workspace_bytes, void* stream);
@@ -122,10 +122,18 @@ int nonode_segno_forward_step(int B, int N, int T, int in_node, int n_edge_feat,
 /*
  * Building blocks (the forwards above are sequences of these).
  */
+/* Floats of one packed TimeConv weight blob; 0 if modes is unsupported. */
+size_t nonode_tconv_blob_floats(int modes);
+
+/* Pack time_conv_modules.l.t_conv.weights1 [64][64][modes][2] (layer_no.py:203-205) for trajectory
+ * length T: the irfft scale (c_m / T) is folded in. Call again after every optimizer step. */
+int nonode_pack_tconv(const float* tconv_w, int modes, int T, float* blob, void* stream);
+
 /* TimeConv + TimeConv_x of one EGNO layer (layer_no.py:96-126,152-178, egno.py:100-108) on
- * time-major [T][BN] arrays; h_out/x_out/v_out may alias h/x/v (in place per column). */
+ * time-major [T][BN] arrays; x_out/v_out may alias x/v (in place per column), h_out may not
+ * alias h. tconv_blob from nonode_pack_tconv, tconvx_w raw [2][2][modes][2]. */
 int nonode_egno_tconv(int BN, int T, int modes, const float* h, const float* x, const float* v,
-                      const float* loc_mean, const float* tconv_w, const float* tconvx_w,
+                      const float* loc_mean, const float* tconv_blob, const float* tconvx_w,
                       float* h_out, float* x_out, float* v_out, void* stream);
 
 /* One fused E(n)-equivariant layer over n_graphs fully connected graphs of N nodes:

@@ -16,7 +16,7 @@ SYMBOLS = (
     "nonode_version", "nonode_last_error", "nonode_layer_blob_floats", "nonode_pack_layer",
     "nonode_egno_workspace_bytes", "nonode_egno_forward", "nonode_segno_workspace_bytes",
     "nonode_segno_forward_step", "nonode_egno_tconv", "nonode_egnn_layer", "nonode_profile_begin",
-    "nonode_profile_end",
+    "nonode_profile_end", "nonode_tconv_blob_floats", "nonode_pack_tconv",
 )
 
 VARIANT_EGNO = 0
@@ -64,6 +64,9 @@ def lib():
     L.nonode_segno_forward_step.argtypes = ([_i] * 5 + [_vp] * 8 + [_f, _i] + [_vp] * 4 + [_sz, _vp])
     L.nonode_egno_tconv.argtypes = [_i, _i, _i] + [_vp] * 10
     L.nonode_egnn_layer.argtypes = [_i] * 5 + [_vp] * 5 + [_f, _f, _i] + [_vp] * 4
+    L.nonode_tconv_blob_floats.argtypes = [_i]
+    L.nonode_tconv_blob_floats.restype = _sz
+    L.nonode_pack_tconv.argtypes = [_vp, _i, _i, _vp, _vp]
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

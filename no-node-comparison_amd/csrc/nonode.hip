@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -26,6 +27,8 @@
 namespace {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f8 __attribute__((ext_vector_type(8)));
 
 constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
 constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
@@ -46,14 +49,19 @@ enum : int {
   OFF_WV1 = 16384,   // node_v W1            [64x64] (EGNO)
   OFF_WN1 = 20480,   // node W1              [64x128]
   OFF_WN2 = 28672,   // node W2              [64x64]
-  OFF_VEC = 32768,   // vectors, 64 floats each, in "vp" order vp[16*g + 4*mt + q] = v[16*mt + 4*g + q]
+  OFF_FEAT = 32768,  // edge W1 columns of the scalar edge inputs [|r|^2, e_0 .. e_{ne-1}] as up to
+                     // two extra k-steps: feat[kf][lane][mo] = W1[16*mo + (l&15)][feature 4*kf + (l>>4)]
+  OFF_VEC = 33280,   // vectors, 64 floats each, in "vp" order vp[16*g + 4*mt + q] = v[16*mt + 4*g + q]
+  OFF_H16 = 33856,   // W2 | Wc1 as fp16 hi/lo fragments of v_mfma_f32_16x16x32_f16 (2 x 4096 floats):
+                     // [mat][s][mo][hi|lo][lane][8 halves], half j of lane l = W[16*mo + (l&15)][chan(s, l>>4, j)],
+                     // chan(s, g, j) = 16*(2*s + (j>>2)) + 4*g + (j&3)  (the ECL order, see h16_b)
 };
-enum : int { V_B1 = 0, V_WS, V_WE0, V_WE1, V_WE2, V_WE3, V_B2, V_BC1, V_WC2, V_BV1, V_WV2, V_BN1, V_BN2,
-             V_COUNT };
+enum : int { V_B2 = 0, V_BC1, V_WC2, V_B1, V_BV1, V_WV2, V_BN1, V_BN2, V_COUNT };
 constexpr int OFF_SCAL = OFF_VEC + V_COUNT * 64;  // [0] = coord b2, [1] = node_v b2
-constexpr int BLOB_FLOATS = OFF_SCAL + 64;
-constexpr int EDGE_VEC_FIRST = V_WS;              // ws, we0..3, b2, bc1, wc2 staged to LDS
-constexpr int EDGE_VEC_COUNT = 8;
+static_assert(OFF_SCAL + 64 == OFF_H16, "blob layout");
+constexpr int BLOB_FLOATS = OFF_H16 + 8192;
+constexpr float H16_LIMIT = 16384.f;   // |activation| above this takes the exact f32 MFMA path
+constexpr int EDGE_STAGE_FLOATS = 512 + 3 * 64;   // FEAT | b2 | bc1 | wc2 (contiguous) staged to LDS
 
 thread_local std::string g_err;
 
@@ -122,21 +130,106 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
 }
 
 // acc[mo] += sum over the KT*16 input channels of W frag(mo, .) * in (ECL); wf = blob section.
-// UNR bounds how many fragment groups the compiler may keep in flight (register pressure):
-// LDS-resident weights use the full unroll, L2-streamed weights a shallow one.
-template <int KT, int UNR = KT>
+// acc[mo] += sum over the KT*16 input channels of W frag(mo, .) * in (ECL); wf = blob section.
+// Fully unrolled (static register indexing); fragments of step mt+1 are loaded while the 16 MFMAs
+// of step mt issue, and a scheduling barrier per step keeps at most two steps of fragments live.
+template <int KT>
 __device__ __forceinline__ void mfma_dense(f4 (&acc)[4], const float* __restrict__ wf, const f4* in,
                                            int lane) {
-#pragma unroll UNR
-  for (int mt = 0; mt < KT; ++mt) {
-    f4 a[4];
+  f4 a[2][4];
 #pragma unroll
-    for (int mo = 0; mo < 4; ++mo) a[mo] = *reinterpret_cast<const f4*>(wf + ((mo * KT + mt) * 64 + lane) * 4);
+  for (int mo = 0; mo < 4; ++mo) a[0][mo] = *reinterpret_cast<const f4*>(wf + ((mo * KT + 0) * 64 + lane) * 4);
+#pragma unroll
+  for (int mt = 0; mt < KT; ++mt) {
+    if (mt + 1 < KT) {
+#pragma unroll
+      for (int mo = 0; mo < 4; ++mo)
+        a[(mt + 1) & 1][mo] = *reinterpret_cast<const f4*>(wf + ((mo * KT + mt + 1) * 64 + lane) * 4);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
-      for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma(a[mo][q], in[mt][q], acc[mo]);
+      for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma(a[mt & 1][mo][q], in[mt][q], acc[mo]);
     }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Two independent column sets (two edge units) through the same weights: each fragment read
+// feeds two MFMAs, and the 8 accumulator chains hide the MFMA dependency latency.
+template <int KT>
+__device__ __forceinline__ void mfma_dense2(f4 (&acc0)[4], f4 (&acc1)[4], const float* __restrict__ wf,
+                                            const f4* in0, const f4* in1, int lane) {
+  f4 a[2][4];
+#pragma unroll
+  for (int mo = 0; mo < 4; ++mo) a[0][mo] = *reinterpret_cast<const f4*>(wf + ((mo * KT + 0) * 64 + lane) * 4);
+#pragma unroll
+  for (int mt = 0; mt < KT; ++mt) {
+    if (mt + 1 < KT) {
+#pragma unroll
+      for (int mo = 0; mo < 4; ++mo)
+        a[(mt + 1) & 1][mo] = *reinterpret_cast<const f4*>(wf + ((mo * KT + mt + 1) * 64 + lane) * 4);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int mo = 0; mo < 4; ++mo) {
+        acc0[mo] = mfma(a[mt & 1][mo][q], in0[mt][q], acc0[mo]);
+        acc1[mo] = mfma(a[mt & 1][mo][q], in1[mt][q], acc1[mo]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+__device__ __forceinline__ void load_frags(f4 (&a)[4], const float* wf, int mt, int lane) {
+#pragma unroll
+  for (int mo = 0; mo < 4; ++mo) a[mo] = *reinterpret_cast<const f4*>(wf + ((mo * 4 + mt) * 64 + lane) * 4);
+}
+
+// ---- fp16x3 split MFMA (fp32-level accuracy at fp16 matrix-core rate) ------------------------
+// x = hi + lo with hi = fp16(x), lo = fp16(x - hi): |x - hi - lo| <= 2^-22 |x|. W x is accumulated in
+// fp32 as W_lo x_hi + W_hi x_lo + W_hi x_hi (the dropped W_lo x_lo term is ~2^-22 relative).
+// The ECL accumulator of one layer is the B operand of v_mfma_f32_16x16x32_f16 for the next:
+// k-step s, half j of lane (g, e) = channel 16*(2s + (j>>2)) + 4g + (j&3) of column e.
+__device__ __forceinline__ void h16_split(const f4 (&x)[4], h8 (&hi)[2], h8 (&lo)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const f8 v = {x[2 * s][0], x[2 * s][1], x[2 * s][2], x[2 * s][3],
+                  x[2 * s + 1][0], x[2 * s + 1][1], x[2 * s + 1][2], x[2 * s + 1][3]};
+    hi[s] = __builtin_convertvector(v, h8);                       // v_cvt_pk_f16_f32 (RNE)
+    lo[s] = __builtin_convertvector(v - __builtin_convertvector(hi[s], f8), h8);
+  }
+}
+__device__ __forceinline__ float amax_ecl(const f4 (&x)[4]) {
+  float m = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m = fmaxf(m, fabsf(x[mt][q]));
+  return m;
+}
+__device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// two edge units through one 64x64 layer: acc0 += W x0, acc1 += W x1 (48 MFMAs, 8 chains)
+__device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
+                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2],
+                                           int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    h8 ah[4], al[4];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
+      al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(al[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(al[mo], x1h[s], acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1l[s], acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1h[s], acc1[mo]); }
   }
 }
 
@@ -197,11 +290,23 @@ __device__ __forceinline__ float vp_src(const float* src, int stride, int d) {
   return src ? src[(16 * mt + 4 * g + q) * stride] : 0.f;
 }
 
+__device__ __forceinline__ void pack_h16(_Float16* dst, const float* W, int d) {
+  // d indexes halves of one matrix: [s][mo][hl][lane][j], 2*4*2*64*8 = 8192
+  const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s = d >> 12;
+  const int row = 16 * mo + (lane & 15);
+  const int col = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
+  const float w = W[row * 64 + col];
+  const _Float16 h = (_Float16)w;
+  dst[d] = hl == 0 ? h : (_Float16)(w - (float)h);
+}
+
 __global__ void pack_kernel(PackArgs a) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
   const int sec = blockIdx.y;
   float* B = a.blob;
   switch (sec) {
+    case 8: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16), a.w2, d); break;
+    case 9: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16 + 4096), a.cw1, d); break;
     case 0: if (d < 4096) pack_frag(B + OFF_WA, a.w1, a.ld1, a.colA, 4, d); break;
     case 1: if (d < 4096) pack_frag(B + OFF_WB, a.w1, a.ld1, a.colB, 4, d); break;
     case 2: if (d < 4096) pack_frag(B + OFF_W2, a.w2, 64, 0, 4, d); break;
@@ -210,17 +315,18 @@ __global__ void pack_kernel(PackArgs a) {
     case 5: pack_frag(B + OFF_WN1, a.nw1, 128, 0, 8, d); break;
     case 6: if (d < 4096) pack_frag(B + OFF_WN2, a.nw2, 64, 0, 4, d); break;
     case 7:
-      if (d < V_COUNT * 64) {
-        const int v = d >> 6, i = d & 63;
+      if (d < 512) {   // feature k-steps
+        const int kf = d >> 8, l = (d >> 2) & 63, mo = d & 3;
+        const int row = 16 * mo + (l & 15), fi = 4 * kf + (l >> 4);
+        float val = 0.f;
+        if (fi == 0) val = a.w1[row * a.ld1 + a.colS];
+        else if (fi - 1 < a.ne) val = a.w1[row * a.ld1 + 2 * HID + 1 + (fi - 1)];
+        B[OFF_FEAT + d] = val;
+      } else if (d < 512 + V_COUNT * 64) {
+        const int dd = d - 512, v = dd >> 6, i = dd & 63;
         float val = 0.f;
         switch (v) {
           case V_B1: val = vp_src(a.b1, 1, i); break;
-          case V_WS: val = vp_src(a.w1 + a.colS, a.ld1, i); break;
-          case V_WE0: case V_WE1: case V_WE2: case V_WE3: {
-            const int f = v - V_WE0;
-            val = f < a.ne ? vp_src(a.w1 + 129 + f, a.ld1, i) : 0.f;
-            break;
-          }
           case V_B2: val = vp_src(a.b2, 1, i); break;
           case V_BC1: val = vp_src(a.cb1, 1, i); break;
           case V_WC2: val = vp_src(a.cw2, 1, i); break;
@@ -229,9 +335,9 @@ __global__ void pack_kernel(PackArgs a) {
           case V_BN1: val = vp_src(a.nb1, 1, i); break;
           case V_BN2: val = vp_src(a.nb2, 1, i); break;
         }
-        B[OFF_VEC + d] = val;
-      } else if (d < V_COUNT * 64 + 64) {
-        const int i = d - V_COUNT * 64;
+        B[OFF_VEC + dd] = val;
+      } else if (d < 512 + V_COUNT * 64 + 64) {
+        const int i = d - 512 - V_COUNT * 64;
         B[OFF_SCAL + i] = (i == 0) ? a.cb2[0] : (i == 1 && a.vb2) ? a.vb2[0] : 0.f;
       }
       break;
@@ -246,13 +352,14 @@ struct LayerArgs {
   const float* __restrict__ ef; const float* __restrict__ blob;
   float* h_out; float* x_out; float* v_out;
   int n_total, N, ne, ef_mod, n_tiles, ct, s_max, recurrent;
+  int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections
   float inv_deg, dt, cw;
 };
 
 size_t layer_lds_floats(int ct, int N, int* s_max_out) {
   const int s_max = ((16 * ct - 1) / N + 2) * N;
   if (s_max_out) *s_max_out = s_max;
-  return 8192 + EDGE_VEC_COUNT * 64 + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * (ROWP + 4) +
+  return 8192 + EDGE_STAGE_FLOATS + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * (ROWP + 4) +
          (size_t)ct * 16 * 4;
 }
 
@@ -263,36 +370,46 @@ size_t layer_lds_floats(int ct, int N, int* s_max_out) {
 //                sender (n + k) mod N of its graph; edge MLP + coord MLP on MFMA; partial
 //                message / force sums flushed into LDS accumulators;
 //             C) node update per tile: x (and v) update, node MLP, stores.
-template <int VARIANT>
+// KF: feature k-steps (1 + ne scalar edge inputs, 4 per step).
+template <int VARIANT, int KF>
 __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
-  float* sW = smem;                              // W2 | Wc1 fragments (8192)
-  float* sV = sW + 8192;                         // ws, we0..3, b2, bc1, wc2 (vp order)
-  float* sP = sV + EDGE_VEC_COUNT * 64;          // [ct*16][ROWP]
+  float* sW = smem;                              // W2 | Wc1 fp16 hi/lo fragments (8192 floats)
+  float* sV = sW + 8192;                         // feat k-steps (512) | b2 | bc1 | wc2 (vp order)
+  float* sP = sV + EDGE_STAGE_FLOATS;            // [ct*16][ROWP]
   float* sQ = sP + p.ct * 16 * ROWP;             // [s_max][ROWP]
   float* sX = sQ + p.s_max * ROWP;               // [s_max][4]
   float* sM = sX + p.s_max * 4;                  // [ct*16][ROWP] message sums
   float* sF = sM + p.ct * 16 * ROWP;             // [ct*16][4]   force sums
 
-  for (int i = tid; i < 2048; i += 512) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_W2)[i];
-  if (tid < EDGE_VEC_COUNT * 16)
-    reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_VEC + EDGE_VEC_FIRST * 64)[tid];
+  for (int i = tid; i < 2048; i += 512) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_H16)[i];
+  if (tid < EDGE_STAGE_FLOATS / 4)
+    reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_FEAT)[tid];
   const float bc2 = p.blob[OFF_SCAL + 0];
   const float bv2 = p.blob[OFF_SCAL + 1];
-  const float* vWS = sV + (V_WS - EDGE_VEC_FIRST) * 64;
-  const float* vB2 = sV + (V_B2 - EDGE_VEC_FIRST) * 64;
-  const float* vBC1 = sV + (V_BC1 - EDGE_VEC_FIRST) * 64;
-  const float* vWC2 = sV + (V_WC2 - EDGE_VEC_FIRST) * 64;
+  const float* vFEAT_ = sV;
+  const float* vB2_ = sV + 512 + V_B2 * 64;
+  const float* vBC1_ = sV + 512 + V_BC1 * 64;
+  const float* vWC2_ = sV + 512 + V_WC2 * 64;
 
   const int G = gridDim.x;
   const int t_begin = (int)(((long long)blockIdx.x * p.n_tiles) / G);
   const int t_end = (int)(((long long)(blockIdx.x + 1) * p.n_tiles) / G);
   __syncthreads();
 
-  for (int c0 = t_begin; c0 < t_end; c0 += p.ct) {
-    const int ctc = min(p.ct, t_end - c0);
+  const int ntw = t_end - t_begin;
+  const int nch = (ntw + p.ct - 1) / p.ct;
+  #pragma unroll 1
+  for (int ci = 0; ci < nch; ++ci) {
+    const int c0 = t_begin + (ci * ntw) / nch;
+    const int ctc = t_begin + ((ci + 1) * ntw) / nch - c0;
+    // keep per-chunk loads of weights/vectors inside the loop (LICM would pin them in VGPRs
+    // across all phases)
+    int boff = 0;
+    asm volatile("" : "+s"(boff));
+    const float* blob = p.blob + boff;
     const int rbase = c0 * 16;
     const int r_last = min(rbase + ctc * 16, p.n_total) - 1;
     const int g_lo = rbase / N, g_hi = r_last / N;
@@ -307,7 +424,8 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
       const int s = i / 3, d = i - 3 * s;
       sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
     }
-    for (int job = wave; job < ctc + nsT; job += NW) {
+    #pragma unroll 1
+    for (int job = wave; job < ((p.debug & 4) ? 0 : ctc + nsT); job += NW) {
       const bool isP = job < ctc;                       // wave-uniform
       const int local = (isP ? job : job - ctc) * 16 + e;
       int node = isP ? rbase + local : s0 + local;
@@ -317,97 +435,87 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
       load_ecl(hin, p.h + (size_t)node * HID, g);
       f4 acc[4];
       if (isP) {
-        load_vp(acc, p.blob + OFF_VEC + V_B1 * 64, g);
+        load_vp(acc, blob + OFF_VEC + V_B1 * 64, g);
       } else {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
       }
-      mfma_dense<4, 1>(acc, p.blob + (isP ? OFF_WA : OFF_WB), hin, lane);
+      mfma_dense<4>(acc, blob + (isP ? OFF_WA : OFF_WB), hin, lane);
       if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
     }
     __syncthreads();
 
     // ---------------- phase B: edges ----------------
+    // Units (tile, k) are split evenly over the waves; a wave walks its range tile segment by
+    // tile segment and processes the units of a segment two at a time, so that the VALU work of
+    // one unit (SiLU, gathers) can issue under the MFMA chains of the other.
     {
-      const int U = ctc * Nm1;
+      const int U = (p.debug & 1) ? 0 : ctc * Nm1;
       const int u0 = (wave * U) / NW, u1 = ((wave + 1) * U) / NW;
-      if (u0 < u1) {
-        int tau = u0 / Nm1;
-        int k = u0 - tau * Nm1 + 1;
-        int rl = 0, n = 0, sb = 0;
-        size_t ebase = 0;
-        bool rvalid = false;
-        float xr0 = 0.f, xr1 = 0.f, xr2 = 0.f, fs0 = 0.f, fs1 = 0.f, fs2 = 0.f;
-        f4 P[4], msum[4];
-        auto setup = [&](int t) {
-          rl = 16 * t + e;
-          const int r = rbase + rl;
-          rvalid = r < p.n_total;
-          const int rc = rvalid ? r : p.n_total - 1;
-          const int gr = rc / N;
-          n = rc - gr * N;
-          sb = gr * N - s0;
-          ebase = ((size_t)(gr % p.ef_mod) * N + n) * Nm1;
-          load_ecl(P, sP + rl * ROWP, g);
-          const float* xs = sX + (sb + n) * 4;
-          xr0 = xs[0]; xr1 = xs[1]; xr2 = xs[2];
+      int u = u0;
+      #pragma unroll 1
+      while (u < u1) {
+        const int tau = u / Nm1;
+        const int k_lo = u - tau * Nm1 + 1;
+        const int k_hi = min(Nm1, k_lo + (u1 - u) - 1);
+        u += k_hi - k_lo + 1;
+        // ---- tile state ----
+        const int rl = 16 * tau + e;
+        const int r = rbase + rl;
+        const bool rvalid = r < p.n_total;
+        const int rc = rvalid ? r : p.n_total - 1;
+        const int gr = rc / N;
+        const int n = rc - gr * N;
+        const int sb = gr * N - s0;
+        const size_t ebase = ((size_t)(gr % p.ef_mod) * N + n) * Nm1;
+        int voff = 0;
+        asm volatile("" : "+v"(voff));   // keeps the vector reads per segment (not hoisted), LDS space kept
+        const float* vB2 = vB2_ + voff;
+        const float* vBC1 = vBC1_ + voff;
+        const float* vWC2 = vWC2_ + voff;
+        const float* vFEAT = vFEAT_ + voff;
+        f4 P[4];
+        load_ecl(P, sP + rl * ROWP, g);
+        const float xr0 = sX[(sb + n) * 4 + 0], xr1 = sX[(sb + n) * 4 + 1], xr2 = sX[(sb + n) * 4 + 2];
+        f4 msum[4];
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) msum[mt] = f4{0.f, 0.f, 0.f, 0.f};
-          fs0 = fs1 = fs2 = 0.f;
+        for (int mt = 0; mt < 4; ++mt) msum[mt] = f4{0.f, 0.f, 0.f, 0.f};
+        float fs0 = 0.f, fs1 = 0.f, fs2 = 0.f;
+
+        // pre-activation of edge (r, k): P_r + Q_s + W1[:, scalars] [|r|^2, e_rs] on MFMA
+        // this lane's scalar edge inputs of unit k (feature 4*kf + g; feature 0 = |r|^2 is computed):
+        // one unconditional, clamped global load per k-step, issued a pair ahead of its use
+        auto fetch_ef = [&](int k, float (&ev)[KF]) __attribute__((always_inline)) {
+          int j = n + k;
+          j = (j >= N) ? j - N : j;
+          const int jj = (j < n) ? j : j - 1;             // reference edge order (i, j != i)
+          const float* efp = p.ef + (ebase + jj) * p.ne;
+#pragma unroll
+          for (int kf = 0; kf < KF; ++kf) ev[kf] = efp[min(max(4 * kf + g - 1, 0), p.ne - 1)];
         };
-        auto flush = [&]() {
-          if (rvalid) {
-            float* mrow = sM + rl * ROWP + 4 * g;
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-              for (int q = 0; q < 4; ++q) atomicAdd(mrow + 16 * mt + q, msum[mt][q]);
-            if (g == 0) {
-              atomicAdd(sF + rl * 4 + 0, fs0);
-              atomicAdd(sF + rl * 4 + 1, fs1);
-              atomicAdd(sF + rl * 4 + 2, fs2);
-            }
-          }
-        };
-        setup(tau);
-        for (int u = u0; u < u1; ++u) {
+        // pre-activation of edge (r, k): P_r + Q_s + W1[:, scalars] [|r|^2, e_rs] on MFMA
+        auto head = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
+            __attribute__((always_inline)) {
           int j = n + k;
           j = (j >= N) ? j - N : j;
           const int sl = sb + j;
-          const int jj = (j < n) ? j : j - 1;               // reference edge order (i, j != i)
           const float* xs = sX + sl * 4;
-          const float r0 = xr0 - xs[0], r1 = xr1 - xs[1], r2 = xr2 - xs[2];
+          r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
           const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
-          const float* efp = p.ef + (ebase + jj) * p.ne;
-          float ev[4];
-#pragma unroll
-          for (int f = 0; f < 4; ++f) ev[f] = (f < p.ne) ? efp[f] : 0.f;
-          // layer 1 (decomposed): P_i + Q_j + w_s*|r|^2 + W_e e_ij
-          f4 a[4], q4[4], w4[4];
+          f4 q4[4];
           load_ecl(q4, sQ + sl * ROWP, g);
-          load_vp(w4, vWS, g);
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) a[mt] = P[mt] + q4[mt] + w4[mt] * d2;
+          for (int mt = 0; mt < 4; ++mt) a[mt] = P[mt] + q4[mt];
 #pragma unroll
-          for (int f = 0; f < 4; ++f) {
-            if (f < p.ne) {
-              load_vp(w4, vWS + (1 + f) * 64, g);
+          for (int kf = 0; kf < KF; ++kf) {
+            const int fi = 4 * kf + g;
+            const float bv = (fi == 0) ? d2 : ((fi - 1 < p.ne) ? ev[kf] : 0.f);
+            const f4 wf = *reinterpret_cast<const f4*>(vFEAT + kf * 256 + lane * 4);
 #pragma unroll
-              for (int mt = 0; mt < 4; ++mt) a[mt] += w4[mt] * ev[f];
-            }
+            for (int mo = 0; mo < 4; ++mo) a[mo] = mfma(wf[mo], bv, a[mo]);
           }
-          silu_ecl(a);
-          // layer 2: m = SiLU(W2 a + b2)
-          f4 m[4];
-          load_vp(m, vB2, g);
-          mfma_dense<4>(m, sW, a, lane);
-          silu_ecl(m);
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
-          // coord MLP: c = w_c2 . SiLU(Wc1 m + bc1) + bc2
-          f4 c1[4];
-          load_vp(c1, vBC1, g);
-          mfma_dense<4>(c1, sW + 4096, m, lane);
+        };
+        auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
           silu_ecl(c1);
           const float c = dot_vp(c1, vWC2, g) + bc2;
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
@@ -417,20 +525,80 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
             f2 = fminf(fmaxf(f2, -100.f), 100.f);
           }
           fs0 += f0; fs1 += f1; fs2 += f2;
-          if (++k == N) {
-            flush();
-            k = 1;
-            ++tau;
-            if (u + 1 < u1) setup(tau);
+        };
+
+        const h8* w2h = reinterpret_cast<const h8*>(sW);
+        const h8* wc1h = reinterpret_cast<const h8*>(sW + 4096);
+        const float* w2f = p.blob + OFF_W2;     // exact fp32 fragments (global) for the guard path
+        const float* wc1f = p.blob + OFF_WC1;
+        // Units two at a time (k, k2). A lone last unit runs as a pair with itself (k2 = k) and its
+        // second copy is not accumulated.
+        float e0[KF], e1[KF];
+        fetch_ef(k_lo, e0);
+        fetch_ef(min(k_lo + 1, k_hi), e1);
+#pragma unroll 1
+        for (int k = k_lo; k <= k_hi; k += 2) {
+          const bool two = k + 1 <= k_hi;
+          const int k2 = two ? k + 1 : k;
+          float n0[KF], n1[KF];
+          fetch_ef(min(k + 2, k_hi), n0);              // next pair's edge inputs, in flight meanwhile
+          fetch_ef(min(k + 3, k_hi), n1);
+          f4 a0[4], a1[4], m0[4], m1[4];
+          float ra0, ra1, ra2, rb0, rb1, rb2;
+          head(k, e0, a0, ra0, ra1, ra2);
+          head(k2, e1, a1, rb0, rb1, rb2);
+#pragma unroll
+          for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
+          silu_ecl(a0);
+          silu_ecl(a1);
+          load_vp(m0, vB2, g);
+          load_vp(m1, vB2, g);
+          if (__builtin_expect(__any(fmaxf(amax_ecl(a0), amax_ecl(a1)) > H16_LIMIT), 0)) {
+            mfma_dense2<4>(m0, m1, w2f, a0, a1, lane);
+          } else {
+            h8 a0h[2], a0l[2], a1h[2], a1l[2];
+            h16_split(a0, a0h, a0l);
+            h16_split(a1, a1h, a1l);
+            mfma_h16x2(m0, m1, w2h, a0h, a0l, a1h, a1l, lane);     // m = SiLU(W2 a + b2)
+          }
+          silu_ecl(m0);
+          silu_ecl(m1);
+          const float w2nd = two ? 1.f : 0.f;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) msum[mt] += m0[mt] + m1[mt] * w2nd;
+          load_vp(a0, vBC1, g);
+          load_vp(a1, vBC1, g);
+          if (__builtin_expect(__any(fmaxf(amax_ecl(m0), amax_ecl(m1)) > H16_LIMIT), 0)) {
+            mfma_dense2<4>(a0, a1, wc1f, m0, m1, lane);
+          } else {
+            h8 m0h[2], m0l[2], m1h[2], m1l[2];
+            h16_split(m0, m0h, m0l);
+            h16_split(m1, m1h, m1l);
+            mfma_h16x2(a0, a1, wc1h, m0h, m0l, m1h, m1l, lane);   // coord hidden: SiLU(Wc1 m + bc1)
+          }
+          tail(a0, ra0, ra1, ra2);
+          tail(a1, rb0 * w2nd, rb1 * w2nd, rb2 * w2nd);
+        }
+        // ---- flush the segment's partial sums ----
+        if (rvalid) {
+          float* mrow = sM + rl * ROWP + 4 * g;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) atomicAdd(mrow + 16 * mt + q, msum[mt][q]);
+          if (g == 0) {
+            atomicAdd(sF + rl * 4 + 0, fs0);
+            atomicAdd(sF + rl * 4 + 1, fs1);
+            atomicAdd(sF + rl * 4 + 2, fs2);
           }
         }
-        if (k != 1) flush();
       }
     }
     __syncthreads();
 
     // ---------------- phase C: node update ----------------
-    for (int tau = wave; tau < ctc; tau += NW) {
+    #pragma unroll 1
+    for (int tau = wave; tau < ((p.debug & 2) ? 0 : ctc); tau += NW) {
       const int rl = 16 * tau + e;
       const int r = rbase + rl;
       const bool rvalid = r < p.n_total;
@@ -450,10 +618,10 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
       if (VARIANT == EGNO) {
         // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
         f4 t[4];
-        load_vp(t, p.blob + OFF_VEC + V_BV1 * 64, g);
-        mfma_dense<4, 1>(t, p.blob + OFF_WV1, hr, lane);
+        load_vp(t, blob + OFF_VEC + V_BV1 * 64, g);
+        mfma_dense<4>(t, blob + OFF_WV1, hr, lane);
         silu_ecl(t);
-        const float phi = dot_vp(t, p.blob + OFF_VEC + V_WV2 * 64, g) + bv2;
+        const float phi = dot_vp(t, blob + OFF_VEC + V_WV2 * 64, g) + bv2;
         nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
         nx1 = x1 + phi * v1 + fminf(fmaxf(F1 * p.inv_deg, -100.f), 100.f);
         nx2 = x2 + phi * v2 + fminf(fmaxf(F2 * p.inv_deg, -100.f), 100.f);
@@ -468,12 +636,12 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
       }
       // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
       f4 z[4];
-      load_vp(z, p.blob + OFF_VEC + V_BN1 * 64, g);
-      mfma_dense<8, 1>(z, p.blob + OFF_WN1, in8, lane);
+      load_vp(z, blob + OFF_VEC + V_BN1 * 64, g);
+      mfma_dense<8>(z, blob + OFF_WN1, in8, lane);
       silu_ecl(z);
       f4 hn[4];
-      load_vp(hn, p.blob + OFF_VEC + V_BN2 * 64, g);
-      mfma_dense<4, 1>(hn, p.blob + OFF_WN2, z, lane);
+      load_vp(hn, blob + OFF_VEC + V_BN2 * 64, g);
+      mfma_dense<4>(hn, blob + OFF_WN2, z, lane);
       if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
@@ -498,164 +666,199 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
 struct TconvArgs {
   int BN, T, M, Mfull;
   const float* h; const float* x; const float* v; const float* lm;
-  const float* w; const float* wx;
+  const float* wp;   // packed mixing fragments (nonode_pack_tconv)
+  const float* wx;   // TimeConv_x weights [2][2][Mfull][2] (raw)
   float* h_out; float* x_out; float* v_out;
   // FIRST layer only: h0 = embedding([h_in, temb]) built on the fly (egno.py:63-76)
   const float* hin; int din; const float* emb_w; int emb_ld; const float* etab; int Bt;
 };
 
-// Closed form of irfft(pad(Y[:M]), n=T) used here (pocketfft c2r semantics):
-//   y[t] = (1/T) * sum_{m<M} c_m * (Re Y_m cos(2 pi m t/T) - Im Y_m sin(2 pi m t/T)),
-//   c_0 = 1, c_{T/2} = 1 (T even), else 2 — the imaginary parts at DC / Nyquist drop out since
-//   their sine vanishes.
+// Packed mixing weights of one TimeConv (layer_no.py:80-126), as W^T fragments (f32 MFMA A operand)
+// with the irfft scale folded in: mode 0 -> A_0 = Wr_0 / T; mode m >= 1 -> A_m = c_m Wr_m / T,
+// B_m = c_m Wi_m / T, -A_m. With Xr_m = sum_t h cos, Xs_m = sum_t h sin (so X_m = Xr_m - i Xs_m):
+//   Yr_m = A_m^T Xr_m + B_m^T Xs_m,  Yi_m = B_m^T Xr_m - A_m^T Xs_m,
+//   y[t] = sum_m (Yr_m cos(2 pi m t/T) - Yi_m sin(2 pi m t/T))   (= irfft(pad(Y), n=T)).
+size_t tconv_blob_floats(int modes) { return (size_t)(1 + 3 * (modes - 1)) * 4096; }
+
+__global__ void tconv_pack_kernel(const float* w, int Mfull, int M, int T, float* out) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nmat = 1 + 3 * (M - 1);
+  if (d >= nmat * 4096) return;
+  const int mat = d >> 12, r = d & 4095;
+  const int q = r & 3, l = (r >> 2) & 63, rest = r >> 8, mt = rest & 3, mo = rest >> 2;
+  const int o = 16 * mo + (l & 15), i = 16 * mt + 4 * (l >> 4) + q;     // W^T[o][i] = W[i][o]
+  int m, c;
+  float sgn = 1.f;
+  if (mat == 0) { m = 0; c = 0; }
+  else { m = 1 + (mat - 1) / 3; const int kind = (mat - 1) % 3; c = (kind == 1) ? 1 : 0; sgn = (kind == 2) ? -1.f : 1.f; }
+  const float cm = (m == 0 || 2 * m == T) ? 1.f : 2.f;
+  out[d] = sgn * cm / (float)T * w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
+}
+
+// One workgroup (4 waves) per tile of 16 columns (b, n). Wave w: DFT of input channels 16w..16w+15,
+// then the mixing MFMAs for output channels 16w..16w+15, then LeakyReLU + residual for those
+// channels over all T. Lanes hold (column e = lane & 15, channels 16w + 4g + q).
 template <bool FIRST>
 __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) float sX[2 * MMAX - 1][16][ROWP];
+  __shared__ float sCos[MMAX * TMAX], sSin[MMAX * TMAX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int T = p.T, M = p.M, BN = p.BN;
-  float* sWh = smem;                          // [(i*64 + o) * 2M + 2m + c]
-  float* sCos = sWh + 64 * 64 * 2 * M;        // [m][TMAX]
-  float* sSin = sCos + MMAX * TMAX;
-  float* sXf = sSin + MMAX * TMAX;            // per wave [2M][64]
-  for (int i = tid; i < 64 * 64 * M; i += 256) {
-    const int io = i / M, m = i - io * M;
-    sWh[io * 2 * M + 2 * m + 0] = p.w[((size_t)io * p.Mfull + m) * 2 + 0];
-    sWh[io * 2 * M + 2 * m + 1] = p.w[((size_t)io * p.Mfull + m) * 2 + 1];
-  }
   if (tid < M * T) {
     const int m = tid / T, t = tid - (tid / T) * T;
     const double ang = 2.0 * (double)m * (double)t / (double)T;
     sCos[m * TMAX + t] = (float)cospi(ang);
     sSin[m * TMAX + t] = (float)sinpi(ang);
   }
+  const int col = blockIdx.x * 16 + e;
+  const bool cvalid = col < BN;
+  const int c = cvalid ? col : BN - 1;
+  const int ch = 16 * wave + 4 * g;      // this lane's 4 channels: ch .. ch+3
+  f4 base = {0.f, 0.f, 0.f, 0.f};
+  const float* et = nullptr;
+  if (FIRST) {
+    for (int k = 0; k < p.din; ++k) {
+      const float hv = p.hin[(size_t)c * p.din + k];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) base[q] = fmaf(p.emb_w[(ch + q) * p.emb_ld + k], hv, base[q]);
+    }
+    et = p.etab + ((size_t)(c % p.Bt) * T) * 64 + ch;
+  }
+  auto hval = [&](int t) -> f4 {
+    if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + base;
+    return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + c) * 64 + ch);
+  };
   __syncthreads();
-  const float invT = 1.0f / (float)T;
-  float cm[MMAX];
+  // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
+  if (wave == 3 && g < 3 && cvalid) {
+    const int d = g;
+    const float lmv = p.lm[(size_t)c * 3 + d];
+    float xs[TMAX], vs[TMAX];
 #pragma unroll
-  for (int m = 0; m < MMAX; ++m) cm[m] = (m == 0 || 2 * m == T) ? 1.f : 2.f;
-  float* sX = sXf + wave * 2 * M * 64;
-
-  for (int cc = 0; cc < 4; ++cc) {
-    const int col = blockIdx.x * 16 + wave * 4 + cc;
-    const bool cvalid = col < BN;
-    const int c = cvalid ? col : BN - 1;
-    // ---- x / v channels (TimeConv_x): lanes 0..2 own spatial dim d ----
-    if (lane < 3 && cvalid) {
-      const int d = lane;
-      const float lmv = p.lm[(size_t)c * 3 + d];
-      float xs[TMAX], vs[TMAX];
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          const size_t row = FIRST ? (size_t)c : ((size_t)t * BN + c);
-          xs[t] = p.x[row * 3 + d] - lmv;
-          vs[t] = p.v[row * 3 + d];
-        }
-      }
-      float yr[MMAX][2], yi[MMAX][2];
-#pragma unroll
-      for (int m = 0; m < MMAX; ++m) {
-        if (m < M) {
-          float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f};
-#pragma unroll
-          for (int t = 0; t < TMAX; ++t) {
-            if (t < T) {
-              const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
-              Xr[0] = fmaf(xs[t], cs, Xr[0]); Xi[0] = fmaf(-xs[t], sn, Xi[0]);
-              Xr[1] = fmaf(vs[t], cs, Xr[1]); Xi[1] = fmaf(-vs[t], sn, Xi[1]);
-            }
-          }
-#pragma unroll
-          for (int o = 0; o < 2; ++o) {
-            float ar = 0.f, ai = 0.f;
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              const float wr = p.wx[(((size_t)i * 2 + o) * p.Mfull + m) * 2 + 0];
-              const float wi = p.wx[(((size_t)i * 2 + o) * p.Mfull + m) * 2 + 1];
-              ar += Xr[i] * wr - Xi[i] * wi;
-              ai += Xr[i] * wi + Xi[i] * wr;
-            }
-            yr[m][o] = ar; yi[m][o] = ai;
-          }
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          float y0 = 0.f, y1 = 0.f;
-#pragma unroll
-          for (int m = 0; m < MMAX; ++m) {
-            if (m < M) {
-              const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
-              y0 += cm[m] * (yr[m][0] * cs - yi[m][0] * sn);
-              y1 += cm[m] * (yr[m][1] * cs - yi[m][1] * sn);
-            }
-          }
-          const size_t row = (size_t)t * BN + c;
-          p.x_out[row * 3 + d] = xs[t] + y0 * invT + lmv;
-          p.v_out[row * 3 + d] = vs[t] + y1 * invT;
-        }
+    for (int t = 0; t < TMAX; ++t) {
+      if (t < T) {
+        const size_t row = FIRST ? (size_t)c : ((size_t)t * BN + c);
+        xs[t] = p.x[row * 3 + d] - lmv;
+        vs[t] = p.v[row * 3 + d];
       }
     }
-    // ---- hidden channels (TimeConv): lane = channel ----
-    float hc[TMAX];
-    if (FIRST) {
-      float base = 0.f;
-      for (int k = 0; k < p.din; ++k) base = fmaf(p.emb_w[lane * p.emb_ld + k], p.hin[(size_t)c * p.din + k], base);
-      const float* et = p.etab + ((size_t)(c % p.Bt) * T) * 64 + lane;
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t)
-        if (t < T) hc[t] = et[t * 64] + base;
-    } else {
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t)
-        if (t < T) hc[t] = p.h[((size_t)t * BN + c) * 64 + lane];
-    }
+    float yr[MMAX][2], yi[MMAX][2];
 #pragma unroll
     for (int m = 0; m < MMAX; ++m) {
       if (m < M) {
-        float Xr = 0.f, Xi = 0.f;
+        float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < TMAX; ++t) {
           if (t < T) {
-            Xr = fmaf(hc[t], sCos[m * TMAX + t], Xr);
-            Xi = fmaf(-hc[t], sSin[m * TMAX + t], Xi);
+            const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
+            Xr[0] = fmaf(xs[t], cs, Xr[0]); Xi[0] = fmaf(-xs[t], sn, Xi[0]);
+            Xr[1] = fmaf(vs[t], cs, Xr[1]); Xi[1] = fmaf(-vs[t], sn, Xi[1]);
           }
         }
-        sX[(2 * m) * 64 + lane] = Xr;
-        sX[(2 * m + 1) * 64 + lane] = Xi;
-      }
-    }
-    __syncthreads();
-    float yr[MMAX], yi[MMAX];
+        const float cm = (m == 0 || 2 * m == T) ? 1.f : 2.f;
 #pragma unroll
-    for (int m = 0; m < MMAX; ++m) { yr[m] = 0.f; yi[m] = 0.f; }
-    for (int i = 0; i < 64; ++i) {
-      const float* wrow = sWh + (i * 64 + lane) * 2 * M;
+        for (int o = 0; o < 2; ++o) {
+          float ar = 0.f, ai = 0.f;
 #pragma unroll
-      for (int m = 0; m < MMAX; ++m) {
-        if (m < M) {
-          const float Xr = sX[(2 * m) * 64 + i], Xi = sX[(2 * m + 1) * 64 + i];
-          const float wr = wrow[2 * m], wi = wrow[2 * m + 1];
-          yr[m] += Xr * wr - Xi * wi;
-          yi[m] += Xr * wi + Xi * wr;
+          for (int i = 0; i < 2; ++i) {
+            const float wr = p.wx[(((size_t)i * 2 + o) * p.Mfull + m) * 2 + 0];
+            const float wi = p.wx[(((size_t)i * 2 + o) * p.Mfull + m) * 2 + 1];
+            ar += Xr[i] * wr - Xi[i] * wi;
+            ai += Xr[i] * wi + Xi[i] * wr;
+          }
+          yr[m][o] = ar * cm; yi[m][o] = ai * cm;
         }
       }
     }
-    if (cvalid) {
+    const float invT = 1.0f / (float)T;
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          float y = 0.f;
+    for (int t = 0; t < TMAX; ++t) {
+      if (t < T) {
+        float y0 = 0.f, y1 = 0.f;
 #pragma unroll
-          for (int m = 0; m < MMAX; ++m)
-            if (m < M) y += cm[m] * (yr[m] * sCos[m * TMAX + t] - yi[m] * sSin[m * TMAX + t]);
-          y *= invT;
-          p.h_out[((size_t)t * BN + c) * 64 + lane] = hc[t] + (y >= 0.f ? y : 0.01f * y);
+        for (int m = 0; m < MMAX; ++m) {
+          if (m < M) {
+            const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
+            y0 += yr[m][0] * cs - yi[m][0] * sn;
+            y1 += yr[m][1] * cs - yi[m][1] * sn;
+          }
+        }
+        const size_t row = (size_t)t * BN + c;
+        p.x_out[row * 3 + d] = xs[t] + y0 * invT + lmv;
+        p.v_out[row * 3 + d] = vs[t] + y1 * invT;
+      }
+    }
+  }
+  // ---- step 1: truncated DFT of this wave's input channels ----
+  {
+    f4 Xr[MMAX], Xs[MMAX];
+#pragma unroll
+    for (int m = 0; m < MMAX; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) {
+      if (t < T) {
+        const f4 hv = hval(t);
+#pragma unroll
+        for (int m = 0; m < MMAX; ++m) {
+          if (m < M) {
+            Xr[m] += hv * sCos[m * TMAX + t];
+            if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
+          }
         }
       }
     }
-    __syncthreads();
+    *reinterpret_cast<f4*>(&sX[0][e][ch]) = Xr[0];
+#pragma unroll
+    for (int m = 1; m < MMAX; ++m) {
+      if (m < M) {
+        *reinterpret_cast<f4*>(&sX[2 * m - 1][e][ch]) = Xr[m];
+        *reinterpret_cast<f4*>(&sX[2 * m][e][ch]) = Xs[m];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- step 2: channel mixing on MFMA (output tile mo = wave) ----
+  f4 Yr[MMAX], Yi[MMAX];
+  auto mix = [&](f4& acc, int mat, int vec) {
+    f4 in[4];
+    load_ecl(in, &sX[vec][e][0], g);
+    const float* wf = p.wp + (size_t)mat * 4096;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const f4 a = *reinterpret_cast<const f4*>(wf + ((wave * 4 + mt) * 64 + lane) * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
+    }
+  };
+  Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
+  mix(Yr[0], 0, 0);
+#pragma unroll
+  for (int m = 1; m < MMAX; ++m) {
+    if (m < M) {
+      const int mat = 1 + 3 * (m - 1);
+      Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
+      Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
+      mix(Yr[m], mat + 0, 2 * m - 1);   // A^T Xr
+      mix(Yr[m], mat + 1, 2 * m);       // B^T Xs
+      mix(Yi[m], mat + 1, 2 * m - 1);   // B^T Xr
+      mix(Yi[m], mat + 2, 2 * m);       // -A^T Xs
+    }
+  }
+  // ---- step 3: y[t] (output channels ch..ch+3 of column e), LeakyReLU(0.01), residual ----
+  if (cvalid) {
+#pragma unroll
+    for (int t = 0; t < TMAX; ++t) {
+      if (t < T) {
+        f4 y = Yr[0];
+#pragma unroll
+        for (int m = 1; m < MMAX; ++m)
+          if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
+        f4 o = hval(t);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
+        *reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + c) * 64 + 16 * wave + 4 * g) = o;
+      }
+    }
   }
 }
 
@@ -706,36 +909,34 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "N=%d too large for the LDS sender table", N);
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
   });
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
   a.n_total = n_total; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.n_tiles = n_tiles; a.ct = ct;
+  static const int dbg = getenv("NONODE_DEBUG") ? atoi(getenv("NONODE_DEBUG")) : 0;
+  a.debug = dbg;
   a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
   ProfScope prof(VARIANT, stream);
-  hipLaunchKernelGGL(egnn_layer_kernel<VARIANT>, dim3(G), dim3(512), lds, stream, a);
+  if (ne == 0) { a.ef = blob; a.ne = 1; a.ef_mod = 1; }   // dummy gather target; feature weights are 0
+  if (a.ne <= 3)
+    hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1>), dim3(G), dim3(512), lds, stream, a);
+  else
+    hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2>), dim3(G), dim3(512), lds, stream, a);
   return check_launch("egnn_layer_kernel");
 }
 
 int launch_tconv(bool first, const TconvArgs& a, hipStream_t stream) {
-  const size_t lds = (size_t)(64 * 64 * 2 * a.M + 2 * MMAX * TMAX + 4 * 2 * a.M * 64) * 4;
   const int grid = (a.BN + 15) / 16;
   ProfScope prof(first ? 3 : 2, stream);
-  if (first) {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      hipFuncSetAttribute((const void*)tconv_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
-    hipLaunchKernelGGL(tconv_kernel<true>, dim3(grid), dim3(256), lds, stream, a);
-  } else {
-    static std::once_flag once;
-    std::call_once(once, [] {
-      hipFuncSetAttribute((const void*)tconv_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    });
-    hipLaunchKernelGGL(tconv_kernel<false>, dim3(grid), dim3(256), lds, stream, a);
-  }
+  if (first)
+    hipLaunchKernelGGL(tconv_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(tconv_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
   return check_launch("tconv_kernel");
 }
 
@@ -776,20 +977,34 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
   a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
   a.ne = n_edge_feat;
   a.blob = blob;
-  hipLaunchKernelGGL(pack_kernel, dim3(32, 8), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_kernel, dim3(32, 10), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_kernel");
 }
 
+size_t nonode_tconv_blob_floats(int modes) { return (modes >= 1 && modes <= MMAX) ? tconv_blob_floats(modes) : 0; }
+
+int nonode_pack_tconv(const float* tconv_w, int modes, int T, float* blob, void* stream) {
+  if (!tconv_w || !blob) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
+  if (modes < 1 || modes > MMAX || T < 1 || T > TMAX)
+    return fail(NONODE_EUNSUPPORTED, "pack_tconv: modes=%d T=%d", modes, T);
+  const int M = effective_modes(T, modes);
+  const int n = (int)tconv_blob_floats(M);
+  hipLaunchKernelGGL(tconv_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, tconv_w, modes,
+                     M, T, blob);
+  return check_launch("tconv_pack_kernel");
+}
+
 int nonode_egno_tconv(int BN, int T, int modes, const float* h, const float* x, const float* v,
-                      const float* loc_mean, const float* tconv_w, const float* tconvx_w,
+                      const float* loc_mean, const float* tconv_blob, const float* tconvx_w,
                       float* h_out, float* x_out, float* v_out, void* stream) {
   if (BN <= 0 || T <= 0 || T > TMAX || modes <= 0 || modes > MMAX)
     return fail(NONODE_EUNSUPPORTED, "tconv: BN=%d T=%d modes=%d (T<=%d, modes<=%d)", BN, T, modes, TMAX, MMAX);
-  if (!h || !x || !v || !loc_mean || !tconv_w || !tconvx_w || !h_out || !x_out || !v_out)
+  if (!h || !x || !v || !loc_mean || !tconv_blob || !tconvx_w || !h_out || !x_out || !v_out)
     return fail(NONODE_EINVAL, "tconv: null pointer");
+  if (h_out == h) return fail(NONODE_EINVAL, "tconv: h_out may not alias h");
   TconvArgs a{};
   a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
-  a.h = h; a.x = x; a.v = v; a.lm = loc_mean; a.w = tconv_w; a.wx = tconvx_w;
+  a.h = h; a.x = x; a.v = v; a.lm = loc_mean; a.wp = tconv_blob; a.wx = tconvx_w;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
   return launch_tconv(false, a, (hipStream_t)stream);
 }
@@ -824,7 +1039,7 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
                         const float* x, const float* h, const float* v, const float* loc_mean,
                         const float* edge_fea, const float* t_out,
                         const float* emb_w, const float* emb_b,
-                        const float* const* blobs, const float* const* tconv_w,
+                        const float* const* blobs, const float* const* tconv_blobs,
                         const float* const* tconvx_w,
                         float* x_out, float* v_out, float* h_out,
                         void* workspace, size_t workspace_bytes, void* stream) {
@@ -834,7 +1049,7 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
     return fail(NONODE_EUNSUPPORTED,
                 "egno_forward: B=%d N=%d T=%d layers=%d in_node=%d modes=%d temb=%d Bt=%d", B, N, T,
                 n_layers, in_node, modes, time_emb_dim, Bt);
-  if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_w || !tconvx_w ||
+  if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_blobs || !tconvx_w ||
       !x_out || !v_out || !h_out || !workspace)
     return fail(NONODE_EINVAL, "egno_forward: null pointer");
   if (workspace_bytes < nonode_egno_workspace_bytes(B, N, T, Bt))
@@ -856,7 +1071,7 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
   for (int l = 0; l < n_layers; ++l) {
     TconvArgs a{};
     a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
-    a.w = tconv_w[l]; a.wx = tconvx_w[l];
+    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l];
     a.h_out = hB; a.x_out = xB; a.v_out = v_out;
     if (l == 0) {
       a.h = nullptr; a.x = x; a.v = v; a.lm = loc_mean;

@@ -134,7 +134,10 @@ class EGNO(nn.Module):
 
     # ---- packed weights (re-packed whenever a parameter changed in place) ----
     def _packed(self):
-        params = [p for l in self.layers for p in l.parameters()]
+        """Packed kernel weights (layer blobs, TimeConv blobs), rebuilt whenever a parameter
+        changed in place (optimizer step) or moved."""
+        params = [p for l in self.layers for p in l.parameters()] + \
+            [m.t_conv.weights1 for m in self.time_conv_modules]
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._blobs is not None and key == self._blob_key:
             return self._blobs
@@ -142,13 +145,18 @@ class EGNO(nn.Module):
         n = L.nonode_layer_blob_floats()
         dev = self.embedding.weight.device
         blobs = torch.empty(self.n_layers, n, dtype=torch.float32, device=dev)
+        tblobs = torch.empty(self.n_layers, L.nonode_tconv_blob_floats(self.num_modes), dtype=torch.float32,
+                             device=dev)
         stream = _lib.stream_of(blobs)
         for i, layer in enumerate(self.layers):
             w = layer.weight_struct()
             _lib.check(L.nonode_pack_layer(ctypes.byref(w), _lib.VARIANT_EGNO, self.hidden_nf,
                                            self.in_edge_nf, _lib.ptr(blobs[i]), stream))
-        self._blobs, self._blob_key = blobs, key
-        return blobs
+            tw = self.time_conv_modules[i].t_conv.weights1.detach().float().contiguous()
+            _lib.check(L.nonode_pack_tconv(_lib.ptr(tw), self.num_modes, self.num_timesteps, _lib.ptr(tblobs[i]),
+                                           stream))
+        self._blobs, self._blob_key = (blobs, tblobs), key
+        return self._blobs
 
     def forward(self, x, h, edge_index, edge_fea, v=None, loc_mean=None, timesteps_in=None, timesteps_out=None):
         """egno.py:37-111. x, v, loc_mean: [BN, 3]; h: [BN, in_node_nf]; edge_index: 2 x [E]
@@ -181,7 +189,7 @@ class EGNO(nn.Module):
         f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
         x, h, v, lm, ef = f32(x), f32(h), f32(v), f32(loc_mean), f32(edge_fea)
         tt = f32(t_out)
-        blobs = self._packed()
+        blobs, tblobs = self._packed()
         dev = x.device
         n = T * B * N
         x_out = torch.empty(n, 3, device=dev)
@@ -192,9 +200,8 @@ class EGNO(nn.Module):
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
         P = ctypes.c_void_p * self.n_layers
         blob_p = P(*[blobs[i].data_ptr() for i in range(self.n_layers)])
-        tcw = [f32(m.t_conv.weights1) for m in self.time_conv_modules]
         tcx = [f32(m.t_conv.weights1) for m in self.time_conv_x_modules]
-        tcw_p = P(*[t.data_ptr() for t in tcw])
+        tcw_p = P(*[tblobs[i].data_ptr() for i in range(self.n_layers)])
         tcx_p = P(*[t.data_ptr() for t in tcx])
         ew, eb = f32(self.embedding.weight), f32(self.embedding.bias)
         _lib.check(L.nonode_egno_forward(

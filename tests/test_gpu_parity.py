@@ -69,7 +69,7 @@ def test_egno_building_blocks_match_reference_layers():
     L = pkg.lib()
     B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
     BN = B * N
-    blobs = m._packed()
+    blobs, tblobs = m._packed()
     lm = _dev(fx["in::loc_mean"])
     ef = _dev(fx["in::edge_attr"])
     s = pkg._lib.stream_of(lm)
@@ -81,10 +81,9 @@ def test_egno_building_blocks_match_reference_layers():
         x_in = _dev(X[..., 0].reshape(T * BN, 3) + np.tile(fx["in::loc_mean"], (T, 1)))
         v_in = _dev(X[..., 1].reshape(T * BN, 3))
         ho, xo, vo = torch.empty_like(h_in), torch.empty_like(x_in), torch.empty_like(v_in)
-        w = m.time_conv_modules[i].t_conv.weights1.detach().contiguous()
         wx = m.time_conv_x_modules[i].t_conv.weights1.detach().contiguous()
-        pkg._lib.check(L.nonode_egno_tconv(BN, T, 2, P(h_in), P(x_in), P(v_in), P(lm), P(w), P(wx), P(ho), P(xo),
-                                           P(vo), s))
+        pkg._lib.check(L.nonode_egno_tconv(BN, T, 2, P(h_in), P(x_in), P(v_in), P(lm), P(tblobs[i]), P(wx), P(ho),
+                                           P(xo), P(vo), s))
         Y = fx[f"cap::tconvx{i}.out"]
         assert maxnorm_rel(ho.cpu().reshape(T, BN, 64), fx[f"cap::tconv{i}.out"]) < TOL
         assert maxnorm_rel(xo.cpu(), Y[..., 0].reshape(T * BN, 3) + np.tile(fx["in::loc_mean"], (T, 1))) < TOL
