@@ -32,7 +32,6 @@ typedef float f8 __attribute__((ext_vector_type(8)));
 
 constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
 constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
-constexpr int NW = 8;      // waves per workgroup of the layer kernel
 constexpr int TMAX = 16;   // max trajectory length handled by tconv_kernel
 constexpr int MMAX = 4;    // max Fourier modes
 
@@ -212,6 +211,26 @@ __device__ __forceinline__ float amax_ecl(const f4 (&x)[4]) {
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
+// one edge unit through one 64x64 layer: acc += W x (24 MFMAs, 4 chains)
+__device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&xh)[2], const h8 (&xl)[2],
+                                         int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    h8 ah[4], al[4];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
+      al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(al[mo], xh[s], acc[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(ah[mo], xl[s], acc[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(ah[mo], xh[s], acc[mo]);
+  }
+}
+
 // two edge units through one 64x64 layer: acc0 += W x0, acc1 += W x1 (48 MFMAs, 8 chains)
 __device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
                                            const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2],
@@ -370,9 +389,9 @@ size_t layer_lds_floats(int ct, int N, int* s_max_out) {
 //                sender (n + k) mod N of its graph; edge MLP + coord MLP on MFMA; partial
 //                message / force sums flushed into LDS accumulators;
 //             C) node update per tile: x (and v) update, node MLP, stores.
-// KF: feature k-steps (1 + ne scalar edge inputs, 4 per step).
-template <int VARIANT, int KF>
-__global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
+// KF: feature k-steps (1 + ne scalar edge inputs, 4 per step); NW: waves per workgroup.
+template <int VARIANT, int KF, int NW>
+__global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
@@ -384,7 +403,7 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
   float* sM = sX + p.s_max * 4;                  // [ct*16][ROWP] message sums
   float* sF = sM + p.ct * 16 * ROWP;             // [ct*16][4]   force sums
 
-  for (int i = tid; i < 2048; i += 512) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_H16)[i];
+  for (int i = tid; i < 2048; i += NW * 64) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_H16)[i];
   if (tid < EDGE_STAGE_FLOATS / 4)
     reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_FEAT)[tid];
   const float bc2 = p.blob[OFF_SCAL + 0];
@@ -418,9 +437,13 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
     const int nsT = (S + 15) >> 4;
 
     // ---------------- phase A: node projections into LDS ----------------
-    for (int i = tid; i < ctc * 16 * ROWP; i += 512) sM[i] = 0.f;
-    for (int i = tid; i < ctc * 16 * 4; i += 512) sF[i] = 0.f;
-    for (int i = tid; i < S * 3; i += 512) {
+    for (int i = tid; i < ctc * 16 * ROWP; i += NW * 64) sM[i] = 0.f;
+    for (int i = tid; i < ctc * 16 * 4; i += NW * 64) sF[i] = 0.f;
+    if (p.debug & 4) {   // ablation: projections skipped, tables zeroed so later phases stay finite
+      for (int i = tid; i < ctc * 16 * ROWP; i += NW * 64) sP[i] = 0.f;
+      for (int i = tid; i < S * ROWP; i += NW * 64) sQ[i] = 0.f;
+    }
+    for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
       sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
     }
@@ -531,53 +554,39 @@ __global__ __launch_bounds__(512) void egnn_layer_kernel(LayerArgs p) {
         const h8* wc1h = reinterpret_cast<const h8*>(sW + 4096);
         const float* w2f = p.blob + OFF_W2;     // exact fp32 fragments (global) for the guard path
         const float* wc1f = p.blob + OFF_WC1;
-        // Units two at a time (k, k2). A lone last unit runs as a pair with itself (k2 = k) and its
-        // second copy is not accumulated.
-        float e0[KF], e1[KF];
+        // One unit (16 edges) per iteration; the next unit's edge inputs are in flight meanwhile.
+        float e0[KF];
         fetch_ef(k_lo, e0);
-        fetch_ef(min(k_lo + 1, k_hi), e1);
 #pragma unroll 1
-        for (int k = k_lo; k <= k_hi; k += 2) {
-          const bool two = k + 1 <= k_hi;
-          const int k2 = two ? k + 1 : k;
-          float n0[KF], n1[KF];
-          fetch_ef(min(k + 2, k_hi), n0);              // next pair's edge inputs, in flight meanwhile
-          fetch_ef(min(k + 3, k_hi), n1);
-          f4 a0[4], a1[4], m0[4], m1[4];
-          float ra0, ra1, ra2, rb0, rb1, rb2;
-          head(k, e0, a0, ra0, ra1, ra2);
-          head(k2, e1, a1, rb0, rb1, rb2);
+        for (int k = k_lo; k <= k_hi; ++k) {
+          float en[KF];
+          fetch_ef(min(k + 1, k_hi), en);
+          f4 a[4], m[4];
+          float r0, r1, r2;
+          head(k, e0, a, r0, r1, r2);
 #pragma unroll
-          for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
-          silu_ecl(a0);
-          silu_ecl(a1);
-          load_vp(m0, vB2, g);
-          load_vp(m1, vB2, g);
-          if (__builtin_expect(__any(fmaxf(amax_ecl(a0), amax_ecl(a1)) > H16_LIMIT), 0)) {
-            mfma_dense2<4>(m0, m1, w2f, a0, a1, lane);
+          for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
+          silu_ecl(a);
+          load_vp(m, vB2, g);
+          if (__builtin_expect(__any(amax_ecl(a) > H16_LIMIT), 0)) {
+            mfma_dense<4>(m, w2f, a, lane);
           } else {
-            h8 a0h[2], a0l[2], a1h[2], a1l[2];
-            h16_split(a0, a0h, a0l);
-            h16_split(a1, a1h, a1l);
-            mfma_h16x2(m0, m1, w2h, a0h, a0l, a1h, a1l, lane);     // m = SiLU(W2 a + b2)
+            h8 ah[2], al[2];
+            h16_split(a, ah, al);
+            mfma_h16(m, w2h, ah, al, lane);                      // m = SiLU(W2 a + b2)
           }
-          silu_ecl(m0);
-          silu_ecl(m1);
-          const float w2nd = two ? 1.f : 0.f;
+          silu_ecl(m);
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) msum[mt] += m0[mt] + m1[mt] * w2nd;
-          load_vp(a0, vBC1, g);
-          load_vp(a1, vBC1, g);
-          if (__builtin_expect(__any(fmaxf(amax_ecl(m0), amax_ecl(m1)) > H16_LIMIT), 0)) {
-            mfma_dense2<4>(a0, a1, wc1f, m0, m1, lane);
+          for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
+          load_vp(a, vBC1, g);
+          if (__builtin_expect(__any(amax_ecl(m) > H16_LIMIT), 0)) {
+            mfma_dense<4>(a, wc1f, m, lane);
           } else {
-            h8 m0h[2], m0l[2], m1h[2], m1l[2];
-            h16_split(m0, m0h, m0l);
-            h16_split(m1, m1h, m1l);
-            mfma_h16x2(a0, a1, wc1h, m0h, m0l, m1h, m1l, lane);   // coord hidden: SiLU(Wc1 m + bc1)
+            h8 mh[2], ml[2];
+            h16_split(m, mh, ml);
+            mfma_h16(a, wc1h, mh, ml, lane);                     // coord hidden: SiLU(Wc1 m + bc1)
           }
-          tail(a0, ra0, ra1, ra2);
-          tail(a1, rb0 * w2nd, rb1 * w2nd, rb2 * w2nd);
+          tail(a, r0, r1, r2);
         }
         // ---- flush the segment's partial sums ----
         if (rvalid) {
@@ -909,24 +918,29 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "N=%d too large for the LDS sender table", N);
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, 12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, 12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
   a.n_total = n_total; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.n_tiles = n_tiles; a.ct = ct;
   static const int dbg = getenv("NONODE_DEBUG") ? atoi(getenv("NONODE_DEBUG")) : 0;
+  static const int nw = getenv("NONODE_NW") ? atoi(getenv("NONODE_NW")) : 8;
   a.debug = dbg;
   a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
   ProfScope prof(VARIANT, stream);
   if (ne == 0) { a.ef = blob; a.ne = 1; a.ef_mod = 1; }   // dummy gather target; feature weights are 0
-  if (a.ne <= 3)
-    hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1>), dim3(G), dim3(512), lds, stream, a);
-  else
-    hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2>), dim3(G), dim3(512), lds, stream, a);
+  const int kf = a.ne <= 3 ? 1 : 2;
+  if (nw == 8) {
+    if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, 8>), dim3(G), dim3(512), lds, stream, a);
+    else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, 8>), dim3(G), dim3(512), lds, stream, a);
+  } else {
+    if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, 12>), dim3(G), dim3(768), lds, stream, a);
+    else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, 12>), dim3(G), dim3(768), lds, stream, a);
+  }
   return check_launch("egnn_layer_kernel");
 }
 

@@ -33,7 +33,10 @@ for k, dd in res.items():
         for c in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU"):
             if c in out:
                 line += f" | {c} {out[c] / out['SQ_WAVE_CYCLES']:.1%}"
-    for c in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA"):
+    for c in ("SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_MISC", "SQ_ACTIVE_INST_SCA"):
+        if c in out and "SQ_WAVE_CYCLES" in out:
+            line += f" | {c} {out[c] / out['SQ_WAVE_CYCLES']:.1%}"
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_BUSY_CYCLES"):
         if c in out:
             line += f" | {c} {out[c]:.3g}"
     print(line)
