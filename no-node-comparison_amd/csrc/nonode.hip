@@ -30,6 +30,9 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f8 __attribute__((ext_vector_type(8)));
 
+#ifndef NONODE_REG_FRAGS
+#define NONODE_REG_FRAGS 1
+#endif
 constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
 constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
 constexpr int TMAX = 16;   // max trajectory length handled by tconv_kernel
@@ -120,9 +123,17 @@ struct ProfScope {
 };
 
 // ---- device helpers ---------------------------------------------------------------------------
-__device__ __forceinline__ float silu(float x) {  // nn.SiLU
-  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+// SiLU in the log2 domain. Every SiLU input z is produced by a packed linear layer whose weights
+// and bias were pre-multiplied by -log2(e) (pack_kernel), so the kernel sees z' = -log2(e) z and
+//   silu2(z') = z' / (1 + 2^z') = -log2(e) * SiLU(z)
+// (v_exp_f32 + v_add + v_rcp + v_mul: the multiply of __expf is gone). The -ln 2 that undoes the
+// factor is folded into whatever consumes the output: the next layer's weights (where it cancels
+// against the next -log2(e)), the coord / node_v output vectors, and node W2.
+__device__ __forceinline__ float silu(float z) {
+  return z * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z));
 }
+constexpr float NEG_LOG2E = -1.4426950408889634f;   // scale of every SiLU input
+constexpr float NEG_LN2 = -0.6931471805599453f;     // 1 / NEG_LOG2E, scale of every SiLU consumer
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -231,6 +242,45 @@ __device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&
   }
 }
 
+// Fragments of one 64x64 matrix held in registers: [s][mo] hi and lo (64 VGPRs).
+struct H16Frags {
+  h8 hi[2][4], lo[2][4];
+};
+__device__ __forceinline__ void load_h16frags(H16Frags& f, const h8* wf, int lane) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      f.hi[s][mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
+      f.lo[s][mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
+    }
+}
+__device__ __forceinline__ void mfma_h16r(f4 (&acc)[4], const H16Frags& f, const h8 (&xh)[2], const h8 (&xl)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.lo[s][mo], xh[s], acc[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xl[s], acc[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xh[s], acc[mo]);
+  }
+}
+
+// two edge units through register-resident fragments, the two chains interleaved
+__device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H16Frags& f, const h8 (&x0h)[2],
+                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2]) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.lo[s][mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(f.lo[s][mo], x1h[s], acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.hi[s][mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(f.hi[s][mo], x1l[s], acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.hi[s][mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(f.hi[s][mo], x1h[s], acc1[mo]); }
+  }
+}
+
 // two edge units through one 64x64 layer: acc0 += W x0, acc1 += W x1 (48 MFMAs, 8 chains)
 __device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
                                            const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2],
@@ -271,11 +321,34 @@ __device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) a[mt][q] = silu(a[mt][q]);
 }
+#ifndef NONODE_ABLATE
+#define NONODE_ABLATE 0   // 1: compile the phase-B internal ablation bits (8/16/32) into the kernel
+#endif
+__device__ __forceinline__ void silu_ecl_dbg(f4 (&a)[4], int debug) {
+  if (NONODE_ABLATE && (debug & 16)) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[mt][q] = fminf(fmaxf(a[mt][q], -1.f), 1.f);
+  } else {
+    silu_ecl(a);
+  }
+}
 // sum over the 4 lane groups (lanes e, e+16, e+32, e+48): the full 64-channel dot product
+// (gfx950 permlane swaps: v + v^32 and then v + v^16 without an LDS round trip)
 __device__ __forceinline__ float group_sum(float v) {
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+__device__ __forceinline__ float dot_r(const f4 (&a)[4], const f4 (&w)[4]) {
+  float s = 0.f;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s = fmaf(a[mt][q], w[mt][q], s);
+  return group_sum(s);
 }
 __device__ __forceinline__ float dot_vp(const f4 (&a)[4], const float* vp, int g) {
   f4 w[4];
@@ -299,10 +372,13 @@ struct PackArgs {
   float* blob;
 };
 
-__device__ __forceinline__ void pack_frag(float* dst, const float* src, int ld, int col0, int KT, int d) {
+// scale(col): multiplier of input column col (the SiLU-domain factors, see silu()).
+__device__ __forceinline__ void pack_frag(float* dst, const float* src, int ld, int col0, int KT, int d,
+                                          float scale_lo, float scale_hi = 0.f, int col_split = 1 << 30) {
   const int q = d & 3, l = (d >> 2) & 63, rest = d >> 8;
   const int mt = rest % KT, mo = rest / KT;
-  dst[d] = src[(16 * mo + (l & 15)) * ld + col0 + 16 * mt + 4 * (l >> 4) + q];
+  const int col = 16 * mt + 4 * (l >> 4) + q;
+  dst[d] = src[(16 * mo + (l & 15)) * ld + col0 + col] * (col < col_split ? scale_lo : scale_hi);
 }
 __device__ __forceinline__ float vp_src(const float* src, int stride, int d) {
   const int g = d >> 4, mt = (d >> 2) & 3, q = d & 3;
@@ -326,13 +402,16 @@ __global__ void pack_kernel(PackArgs a) {
   switch (sec) {
     case 8: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16), a.w2, d); break;
     case 9: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16 + 4096), a.cw1, d); break;
-    case 0: if (d < 4096) pack_frag(B + OFF_WA, a.w1, a.ld1, a.colA, 4, d); break;
-    case 1: if (d < 4096) pack_frag(B + OFF_WB, a.w1, a.ld1, a.colB, 4, d); break;
-    case 2: if (d < 4096) pack_frag(B + OFF_W2, a.w2, 64, 0, 4, d); break;
-    case 3: if (d < 4096) pack_frag(B + OFF_WC1, a.cw1, 64, 0, 4, d); break;
-    case 4: if (d < 4096) { if (a.vw1) pack_frag(B + OFF_WV1, a.vw1, 64, 0, 4, d); else B[OFF_WV1 + d] = 0.f; } break;
-    case 5: pack_frag(B + OFF_WN1, a.nw1, 128, 0, 8, d); break;
-    case 6: if (d < 4096) pack_frag(B + OFF_WN2, a.nw2, 64, 0, 4, d); break;
+    // edge W1 (h parts) produce SiLU inputs: x -log2e.  W2 / Wc1 map SiLU outputs (x -log2e) to
+    // SiLU inputs (x -log2e): unscaled.  node W1: h columns x -log2e, message-sum columns (sums of
+    // SiLU outputs) unscaled.  node W2 maps a SiLU output to h: x -ln2.  node_v W1: x -log2e.
+    case 0: if (d < 4096) pack_frag(B + OFF_WA, a.w1, a.ld1, a.colA, 4, d, NEG_LOG2E); break;
+    case 1: if (d < 4096) pack_frag(B + OFF_WB, a.w1, a.ld1, a.colB, 4, d, NEG_LOG2E); break;
+    case 2: if (d < 4096) pack_frag(B + OFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
+    case 3: if (d < 4096) pack_frag(B + OFF_WC1, a.cw1, 64, 0, 4, d, 1.f); break;
+    case 4: if (d < 4096) { if (a.vw1) pack_frag(B + OFF_WV1, a.vw1, 64, 0, 4, d, NEG_LOG2E); else B[OFF_WV1 + d] = 0.f; } break;
+    case 5: pack_frag(B + OFF_WN1, a.nw1, 128, 0, 8, d, NEG_LOG2E, 1.f, HID); break;
+    case 6: if (d < 4096) pack_frag(B + OFF_WN2, a.nw2, 64, 0, 4, d, NEG_LN2); break;
     case 7:
       if (d < 512) {   // feature k-steps
         const int kf = d >> 8, l = (d >> 2) & 63, mo = d & 3;
@@ -340,18 +419,18 @@ __global__ void pack_kernel(PackArgs a) {
         float val = 0.f;
         if (fi == 0) val = a.w1[row * a.ld1 + a.colS];
         else if (fi - 1 < a.ne) val = a.w1[row * a.ld1 + 2 * HID + 1 + (fi - 1)];
-        B[OFF_FEAT + d] = val;
+        B[OFF_FEAT + d] = val * NEG_LOG2E;
       } else if (d < 512 + V_COUNT * 64) {
         const int dd = d - 512, v = dd >> 6, i = dd & 63;
         float val = 0.f;
-        switch (v) {
-          case V_B1: val = vp_src(a.b1, 1, i); break;
-          case V_B2: val = vp_src(a.b2, 1, i); break;
-          case V_BC1: val = vp_src(a.cb1, 1, i); break;
-          case V_WC2: val = vp_src(a.cw2, 1, i); break;
-          case V_BV1: val = vp_src(a.vb1, 1, i); break;
-          case V_WV2: val = vp_src(a.vw2, 1, i); break;
-          case V_BN1: val = vp_src(a.nb1, 1, i); break;
+        switch (v) {   // biases of SiLU inputs x -log2e; vectors that read SiLU outputs x -ln2
+          case V_B1: val = vp_src(a.b1, 1, i) * NEG_LOG2E; break;
+          case V_B2: val = vp_src(a.b2, 1, i) * NEG_LOG2E; break;
+          case V_BC1: val = vp_src(a.cb1, 1, i) * NEG_LOG2E; break;
+          case V_WC2: val = vp_src(a.cw2, 1, i) * NEG_LN2; break;
+          case V_BV1: val = vp_src(a.vb1, 1, i) * NEG_LOG2E; break;
+          case V_WV2: val = vp_src(a.vw2, 1, i) * NEG_LN2; break;
+          case V_BN1: val = vp_src(a.nb1, 1, i) * NEG_LOG2E; break;
           case V_BN2: val = vp_src(a.nb2, 1, i); break;
         }
         B[OFF_VEC + dd] = val;
@@ -371,7 +450,8 @@ struct LayerArgs {
   const float* __restrict__ ef; const float* __restrict__ blob;
   float* h_out; float* x_out; float* v_out;
   int n_total, N, ne, ef_mod, n_tiles, ct, s_max, recurrent;
-  int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections
+  int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections,
+               // 8 no edge-feature loads, 16 SiLU -> clamp, 32 skip the per-edge fp16 MFMAs
   float inv_deg, dt, cw;
 };
 
@@ -390,7 +470,7 @@ size_t layer_lds_floats(int ct, int N, int* s_max_out) {
 //                message / force sums flushed into LDS accumulators;
 //             C) node update per tile: x (and v) update, node MLP, stores.
 // KF: feature k-steps (1 + ne scalar edge inputs, 4 per step); NW: waves per workgroup.
-template <int VARIANT, int KF, int NW>
+template <int VARIANT, int KF, int NW, bool PAIR>
 __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
@@ -476,6 +556,19 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
       const int U = (p.debug & 1) ? 0 : ctc * Nm1;
       const int u0 = (wave * U) / NW, u1 = ((wave + 1) * U) / NW;
       int u = u0;
+#if NONODE_REG_FRAGS
+      // W2 / Wc1 fp16 fragments stay in registers for the whole edge phase (loop invariant)
+      H16Frags fw2, fwc1;
+      load_h16frags(fw2, reinterpret_cast<const h8*>(sW), lane);
+      load_h16frags(fwc1, reinterpret_cast<const h8*>(sW + 4096), lane);
+#endif
+      // PAIR (one wave per SIMD): b2 / bc1 / wc2 also stay in registers for the edge phase
+      f4 rB2[4], rBC1[4], rWC2[4];
+      if (PAIR) {
+        load_vp(rB2, vB2_, g);
+        load_vp(rBC1, vBC1_, g);
+        load_vp(rWC2, vWC2_, g);
+      }
       #pragma unroll 1
       while (u < u1) {
         const int tau = u / Nm1;
@@ -497,8 +590,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         const float* vBC1 = vBC1_ + voff;
         const float* vWC2 = vWC2_ + voff;
         const float* vFEAT = vFEAT_ + voff;
-        f4 P[4];
-        load_ecl(P, sP + rl * ROWP, g);
+        const float* Prow = sP + rl * ROWP;            // re-read per unit (saves 16 live VGPRs)
         const float xr0 = sX[(sb + n) * 4 + 0], xr1 = sX[(sb + n) * 4 + 1], xr2 = sX[(sb + n) * 4 + 2];
         f4 msum[4];
 #pragma unroll
@@ -514,7 +606,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           const int jj = (j < n) ? j : j - 1;             // reference edge order (i, j != i)
           const float* efp = p.ef + (ebase + jj) * p.ne;
 #pragma unroll
-          for (int kf = 0; kf < KF; ++kf) ev[kf] = efp[min(max(4 * kf + g - 1, 0), p.ne - 1)];
+          for (int kf = 0; kf < KF; ++kf) ev[kf] = (NONODE_ABLATE && (p.debug & 8)) ? 0.5f : efp[min(max(4 * kf + g - 1, 0), p.ne - 1)];
         };
         // pre-activation of edge (r, k): P_r + Q_s + W1[:, scalars] [|r|^2, e_rs] on MFMA
         auto head = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
@@ -527,8 +619,9 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
           f4 q4[4];
           load_ecl(q4, sQ + sl * ROWP, g);
+          load_ecl(a, Prow, g);
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) a[mt] = P[mt] + q4[mt];
+          for (int mt = 0; mt < 4; ++mt) a[mt] += q4[mt];
 #pragma unroll
           for (int kf = 0; kf < KF; ++kf) {
             const int fi = 4 * kf + g;
@@ -539,8 +632,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           }
         };
         auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
-          silu_ecl(c1);
-          const float c = dot_vp(c1, vWC2, g) + bc2;
+          silu_ecl_dbg(c1, p.debug);
+          const float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2, g)) + bc2;
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
           if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
             f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -554,11 +647,61 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         const h8* wc1h = reinterpret_cast<const h8*>(sW + 4096);
         const float* w2f = p.blob + OFF_W2;     // exact fp32 fragments (global) for the guard path
         const float* wc1f = p.blob + OFF_WC1;
+        int k = k_lo;
+        if (PAIR) {
+          // Two units (32 edges, same receivers) per iteration: two independent dependency chains
+          // the scheduler interleaves, so one unit's MFMAs issue beside the other's SiLU work.
+          float e0[KF], e1[KF];
+          fetch_ef(k, e0);
+          fetch_ef(min(k + 1, k_hi), e1);
+#pragma unroll 1
+          for (; k + 1 <= k_hi; k += 2) {
+            float n0[KF], n1[KF];
+            fetch_ef(min(k + 2, k_hi), n0);
+            fetch_ef(min(k + 3, k_hi), n1);
+            f4 a0[4], a1[4], m0[4], m1[4];
+            float r00, r01, r02, r10, r11, r12;
+            head(k, e0, a0, r00, r01, r02);
+            head(k + 1, e1, a1, r10, r11, r12);
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
+            silu_ecl(a0);
+            silu_ecl(a1);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; }
+            if (__builtin_expect(__any(fmaxf(amax_ecl(a0), amax_ecl(a1)) > H16_LIMIT), 0)) {
+              mfma_dense<4>(m0, w2f, a0, lane);
+              mfma_dense<4>(m1, w2f, a1, lane);
+            } else {
+              h8 ah0[2], al0[2], ah1[2], al1[2];
+              h16_split(a0, ah0, al0);
+              h16_split(a1, ah1, al1);
+              mfma_h16r2(m0, m1, fw2, ah0, al0, ah1, al1);
+            }
+            silu_ecl(m0);
+            silu_ecl(m1);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) msum[mt] += m0[mt] + m1[mt];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) { a0[mt] = rBC1[mt]; a1[mt] = rBC1[mt]; }
+            if (__builtin_expect(__any(fmaxf(amax_ecl(m0), amax_ecl(m1)) > H16_LIMIT), 0)) {
+              mfma_dense<4>(a0, wc1f, m0, lane);
+              mfma_dense<4>(a1, wc1f, m1, lane);
+            } else {
+              h8 mh0[2], ml0[2], mh1[2], ml1[2];
+              h16_split(m0, mh0, ml0);
+              h16_split(m1, mh1, ml1);
+              mfma_h16r2(a0, a1, fwc1, mh0, ml0, mh1, ml1);
+            }
+            tail(a0, r00, r01, r02);
+            tail(a1, r10, r11, r12);
+          }
+        }
         // One unit (16 edges) per iteration; the next unit's edge inputs are in flight meanwhile.
         float e0[KF];
-        fetch_ef(k_lo, e0);
+        fetch_ef(min(k, k_hi), e0);
 #pragma unroll 1
-        for (int k = k_lo; k <= k_hi; ++k) {
+        for (; k <= k_hi; ++k) {
           float en[KF];
           fetch_ef(min(k + 1, k_hi), en);
           f4 a[4], m[4];
@@ -566,16 +709,20 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           head(k, e0, a, r0, r1, r2);
 #pragma unroll
           for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
-          silu_ecl(a);
+          silu_ecl_dbg(a, p.debug);
           load_vp(m, vB2, g);
           if (__builtin_expect(__any(amax_ecl(a) > H16_LIMIT), 0)) {
             mfma_dense<4>(m, w2f, a, lane);
           } else {
             h8 ah[2], al[2];
             h16_split(a, ah, al);
+#if NONODE_REG_FRAGS
+            if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(m, fw2, ah, al);      // m = SiLU(W2 a + b2)
+#else
             mfma_h16(m, w2h, ah, al, lane);                      // m = SiLU(W2 a + b2)
+#endif
           }
-          silu_ecl(m);
+          silu_ecl_dbg(m, p.debug);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
           load_vp(a, vBC1, g);
@@ -584,7 +731,11 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           } else {
             h8 mh[2], ml[2];
             h16_split(m, mh, ml);
+#if NONODE_REG_FRAGS
+            if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(a, fwc1, mh, ml);     // coord hidden: SiLU(Wc1 m + bc1)
+#else
             mfma_h16(a, wc1h, mh, ml, lane);                     // coord hidden: SiLU(Wc1 m + bc1)
+#endif
           }
           tail(a, r0, r1, r2);
         }
@@ -902,6 +1053,16 @@ __global__ void embed_kernel(int n_nodes, int din, const float* in, const float*
 }
 
 // ---- host-side launchers ----------------------------------------------------------------------
+template <int VARIANT, int NW, bool PAIR>
+void launch_cfg(int kf, int G, size_t lds, hipStream_t stream, const LayerArgs& a) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, NW, PAIR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, NW, PAIR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, NW, PAIR>), dim3(G), dim3(NW * 64), lds, stream, a);
+  else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, NW, PAIR>), dim3(G), dim3(NW * 64), lds, stream, a);
+}
 template <int VARIANT>
 int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const float* x,
                  const float* v, const float* ef, const float* blob, float dt, float cw, int recurrent,
@@ -916,31 +1077,22 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   while (ct > 1 && layer_lds_floats(ct, N, &s_max) * 4 > 160 * 1024) --ct;
   const size_t lds = layer_lds_floats(ct, N, &s_max) * 4;
   if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "N=%d too large for the LDS sender table", N);
-  static std::once_flag once;
-  std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, 12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, 12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  });
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
   a.n_total = n_total; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.n_tiles = n_tiles; a.ct = ct;
   static const int dbg = getenv("NONODE_DEBUG") ? atoi(getenv("NONODE_DEBUG")) : 0;
-  static const int nw = getenv("NONODE_NW") ? atoi(getenv("NONODE_NW")) : 8;
+  // wave configuration (NONODE_CFG): 0 = 8 waves, one unit per iteration; 1 = 4 waves (one per
+  // SIMD, 512-register budget), two units per iteration; 2 = 8 waves, two units per iteration
+  static const int cfg = getenv("NONODE_CFG") ? atoi(getenv("NONODE_CFG")) : 0;
   a.debug = dbg;
   a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
   ProfScope prof(VARIANT, stream);
   if (ne == 0) { a.ef = blob; a.ne = 1; a.ef_mod = 1; }   // dummy gather target; feature weights are 0
   const int kf = a.ne <= 3 ? 1 : 2;
-  if (nw == 8) {
-    if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, 8>), dim3(G), dim3(512), lds, stream, a);
-    else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, 8>), dim3(G), dim3(512), lds, stream, a);
-  } else {
-    if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, 12>), dim3(G), dim3(768), lds, stream, a);
-    else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, 12>), dim3(G), dim3(768), lds, stream, a);
-  }
+  if (cfg == 1) launch_cfg<VARIANT, 4, true>(kf, G, lds, stream, a);
+  else if (cfg == 2) launch_cfg<VARIANT, 8, true>(kf, G, lds, stream, a);
+  else launch_cfg<VARIANT, 8, false>(kf, G, lds, stream, a);
   return check_launch("egnn_layer_kernel");
 }
 
