@@ -45,6 +45,15 @@ def synthetic_charged(B, N, seed):
     return loc, vel, q
 
 
+def rank_batch(B_per, world, rank, N, seed):
+    """This rank's shard of the global synthetic batch of B_per * world samples (weak scaling: the
+    per-GPU batch is fixed). Concatenating every rank's shard gives the global batch."""
+    from no_node_comparison_amd.sharding import shard_range
+    loc, vel, q = synthetic_charged(B_per * world, N, seed)
+    lo, hi = shard_range(B_per * world, world, rank)
+    return loc[lo:hi], vel[lo:hi], q[lo:hi]
+
+
 def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -65,17 +74,9 @@ def barrier_sync(world, dev):
         torch.cuda.synchronize(dev)
 
 
-def max_over_ranks(world, v, dev):
-    if world == 1:
-        return v
-    t = torch.tensor([v], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def build_egno_case(B, N, T, seed, dev):
+def build_egno_case(B, N, T, seed, dev, world=1, rank=0):
     import no_node_comparison_amd as pkg
-    loc, vel, q = synthetic_charged(B, N, seed)
+    loc, vel, q = rank_batch(B, world, rank, N, seed)
     edges = pkg.harness.get_edges(B, N, dev)
     loc, vel, q = loc.to(dev), vel.to(dev), q.to(dev)
     qq = q.reshape(-1, 1)
@@ -119,7 +120,7 @@ def run_egno(args, world, rank, dev):
     torch.manual_seed(0)
     model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
                      num_timesteps=T, time_emb_dim=32, device=dev).eval()
-    case = build_egno_case(B, N, T, seed=1234 + rank, dev=dev)
+    case = build_egno_case(B, N, T, seed=1234, dev=dev, world=world, rank=rank)
     from no_node_comparison_amd import _lib
     call = lambda: model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],  # noqa: E731
                          loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
@@ -137,7 +138,8 @@ def run_egno(args, world, rank, dev):
         records = _lib.profile_end() if args.kernel_events else []
     layer_events = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
     tconv_ms = [ms for kind, ms in records if kind in (2, 3)]
-    el = max_over_ranks(world, el, dev)
+    from no_node_comparison_amd.sharding import max_over_ranks
+    el = max_over_ranks(el, dev)
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,

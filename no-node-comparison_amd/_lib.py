@@ -9,7 +9,8 @@ import os
 import torch  # load torch's HIP runtime first so libnonode.so binds to the same libamdhip64
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnonode.so")
+# NONODE_LIB selects an in-tree diagnostic build of the same sources (tools/stamp_build.sh)
+LIB_PATH = os.environ.get("NONODE_LIB") or os.path.join(_HERE, "libnonode.so")
 
 # every symbol include/nonode.h declares (tests check the .so exports exactly these)
 SYMBOLS = (

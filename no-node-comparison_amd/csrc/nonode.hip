@@ -57,11 +57,13 @@ enum : int {
   OFF_H16 = 33856,   // W2 | Wc1 as fp16 hi/lo fragments of v_mfma_f32_16x16x32_f16 (2 x 4096 floats):
                      // [mat][s][mo][hi|lo][lane][8 halves], half j of lane l = W[16*mo + (l&15)][chan(s, l>>4, j)],
                      // chan(s, g, j) = 16*(2*s + (j>>2)) + 4*g + (j&3)  (the ECL order, see h16_b)
+  OFF_H16N = 33856 + 8192,   // node-side matrices in the same fp16 hi/lo layout, 4096 floats each (H_*)
 };
+enum : int { H_WA = 0, H_WB, H_WV1, H_WN1A, H_WN1B, H_WN2, H_COUNT };   // WN1A/B: h / message-sum columns
 enum : int { V_B2 = 0, V_BC1, V_WC2, V_B1, V_BV1, V_WV2, V_BN1, V_BN2, V_COUNT };
 constexpr int OFF_SCAL = OFF_VEC + V_COUNT * 64;  // [0] = coord b2, [1] = node_v b2
 static_assert(OFF_SCAL + 64 == OFF_H16, "blob layout");
-constexpr int BLOB_FLOATS = OFF_H16 + 8192;
+constexpr int BLOB_FLOATS = OFF_H16N + H_COUNT * 4096;
 constexpr float H16_LIMIT = 16384.f;   // |activation| above this takes the exact f32 MFMA path
 constexpr int EDGE_STAGE_FLOATS = 512 + 3 * 64;   // FEAT | b2 | bc1 | wc2 (contiguous) staged to LDS
 
@@ -242,6 +244,18 @@ __device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&
   }
 }
 
+// acc += W x for one 16-column tile: fp16x3 on the matrix cores, or the exact f32 MFMA path (wf)
+// when any |x| is beyond the fp16 hi range (wave-uniform guard)
+__device__ __forceinline__ void mm64(f4 (&acc)[4], const h8* wh, const float* wf, const f4 (&x)[4], int lane) {
+  if (__builtin_expect(__any(amax_ecl(x) > H16_LIMIT), 0)) {
+    mfma_dense<4>(acc, wf, x, lane);
+  } else {
+    h8 xh[2], xl[2];
+    h16_split(x, xh, xl);
+    mfma_h16(acc, wh, xh, xl, lane);
+  }
+}
+
 // Fragments of one 64x64 matrix held in registers: [s][mo] hi and lo (64 VGPRs).
 struct H16Frags {
   h8 hi[2][4], lo[2][4];
@@ -385,12 +399,14 @@ __device__ __forceinline__ float vp_src(const float* src, int stride, int d) {
   return src ? src[(16 * mt + 4 * g + q) * stride] : 0.f;
 }
 
-__device__ __forceinline__ void pack_h16(_Float16* dst, const float* W, int d) {
-  // d indexes halves of one matrix: [s][mo][hl][lane][j], 2*4*2*64*8 = 8192
+__device__ __forceinline__ void pack_h16(_Float16* dst, const float* W, int d, int ld = 64, int col0 = 0,
+                                         float scale = 1.f) {
+  // d indexes halves of one 64x64 block: [s][mo][hl][lane][j], 2*4*2*64*8 = 8192; the block is
+  // columns col0 .. col0+63 of W (row stride ld), scaled (SiLU-domain factor) before the split
   const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s = d >> 12;
   const int row = 16 * mo + (lane & 15);
   const int col = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
-  const float w = W[row * 64 + col];
+  const float w = W ? W[row * ld + col0 + col] * scale : 0.f;
   const _Float16 h = (_Float16)w;
   dst[d] = hl == 0 ? h : (_Float16)(w - (float)h);
 }
@@ -402,6 +418,12 @@ __global__ void pack_kernel(PackArgs a) {
   switch (sec) {
     case 8: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16), a.w2, d); break;
     case 9: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16 + 4096), a.cw1, d); break;
+    case 10: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WA * 4096), a.w1, d, a.ld1, a.colA, NEG_LOG2E); break;
+    case 11: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WB * 4096), a.w1, d, a.ld1, a.colB, NEG_LOG2E); break;
+    case 12: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WV1 * 4096), a.vw1, d, 64, 0, NEG_LOG2E); break;
+    case 13: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WN1A * 4096), a.nw1, d, 128, 0, NEG_LOG2E); break;
+    case 14: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WN1B * 4096), a.nw1, d, 128, HID, 1.f); break;
+    case 15: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WN2 * 4096), a.nw2, d, 64, 0, NEG_LN2); break;
     // edge W1 (h parts) produce SiLU inputs: x -log2e.  W2 / Wc1 map SiLU outputs (x -log2e) to
     // SiLU inputs (x -log2e): unscaled.  node W1: h columns x -log2e, message-sum columns (sums of
     // SiLU outputs) unscaled.  node W2 maps a SiLU output to h: x -ln2.  node_v W1: x -log2e.
@@ -441,6 +463,30 @@ __global__ void pack_kernel(PackArgs a) {
       break;
   }
 }
+
+// ---- diagnostic cycle stamps (NONODE_STAMP builds only; tools/stamp_build.sh) ----------------
+#ifndef NONODE_STAMP
+#define NONODE_STAMP 0
+#endif
+#if NONODE_STAMP
+__device__ unsigned long long g_stamp[16];
+#define STAMP_DECL unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                   \
+  do {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                             \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();    \
+    st_acc[i] += _t - st_last;                                     \
+    st_last = _t;                                                  \
+    __builtin_amdgcn_sched_barrier(0);                             \
+  } while (0)
+#define STAMP_FLUSH                                                \
+  if (lane == 0)                                                   \
+    for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_stamp[_i], st_acc[_i]);
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH
+#endif
 
 // ---- fused E(n)-equivariant layer ------------------------------------------------------------
 enum { EGNO = 0, SEGNO = 1 };
@@ -500,6 +546,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
 
   const int ntw = t_end - t_begin;
   const int nch = (ntw + p.ct - 1) / p.ct;
+  STAMP_DECL
   #pragma unroll 1
   for (int ci = 0; ci < nch; ++ci) {
     const int c0 = t_begin + (ci * ntw) / nch;
@@ -543,10 +590,13 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
       }
-      mfma_dense<4>(acc, blob + (isP ? OFF_WA : OFF_WB), hin, lane);
+      mm64(acc, reinterpret_cast<const h8*>(blob + OFF_H16N + (isP ? H_WA : H_WB) * 4096),
+           blob + (isP ? OFF_WA : OFF_WB), hin, lane);
       if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
     }
+    STAMP(6);
     __syncthreads();
+    STAMP(7);
 
     // ---------------- phase B: edges ----------------
     // Units (tile, k) are split evenly over the waves; a wave walks its range tile segment by
@@ -665,6 +715,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             head(k + 1, e1, a1, r10, r11, r12);
 #pragma unroll
             for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
+            STAMP(0);
             silu_ecl(a0);
             silu_ecl(a1);
 #pragma unroll
@@ -678,6 +729,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               h16_split(a1, ah1, al1);
               mfma_h16r2(m0, m1, fw2, ah0, al0, ah1, al1);
             }
+            STAMP(1);
             silu_ecl(m0);
             silu_ecl(m1);
 #pragma unroll
@@ -693,13 +745,16 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               h16_split(m1, mh1, ml1);
               mfma_h16r2(a0, a1, fwc1, mh0, ml0, mh1, ml1);
             }
+            STAMP(2);
             tail(a0, r00, r01, r02);
             tail(a1, r10, r11, r12);
+            STAMP(3);
           }
         }
         // One unit (16 edges) per iteration; the next unit's edge inputs are in flight meanwhile.
         float e0[KF];
         fetch_ef(min(k, k_hi), e0);
+        STAMP(8);
 #pragma unroll 1
         for (; k <= k_hi; ++k) {
           float en[KF];
@@ -709,6 +764,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           head(k, e0, a, r0, r1, r2);
 #pragma unroll
           for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
+          STAMP(0);
           silu_ecl_dbg(a, p.debug);
           load_vp(m, vB2, g);
           if (__builtin_expect(__any(amax_ecl(a) > H16_LIMIT), 0)) {
@@ -722,6 +778,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             mfma_h16(m, w2h, ah, al, lane);                      // m = SiLU(W2 a + b2)
 #endif
           }
+          STAMP(1);
           silu_ecl_dbg(m, p.debug);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
@@ -737,7 +794,9 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             mfma_h16(a, wc1h, mh, ml, lane);                     // coord hidden: SiLU(Wc1 m + bc1)
 #endif
           }
+          STAMP(2);
           tail(a, r0, r1, r2);
+          STAMP(3);
         }
         // ---- flush the segment's partial sums ----
         if (rvalid) {
@@ -752,9 +811,12 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             atomicAdd(sF + rl * 4 + 2, fs2);
           }
         }
+        STAMP(9);
       }
     }
+    STAMP(10);
     __syncthreads();
+    STAMP(11);
 
     // ---------------- phase C: node update ----------------
     #pragma unroll 1
@@ -779,7 +841,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
         f4 t[4];
         load_vp(t, blob + OFF_VEC + V_BV1 * 64, g);
-        mfma_dense<4>(t, blob + OFF_WV1, hr, lane);
+        mm64(t, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WV1 * 4096), blob + OFF_WV1, hr, lane);
         silu_ecl(t);
         const float phi = dot_vp(t, blob + OFF_VEC + V_WV2 * 64, g) + bv2;
         nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
@@ -797,11 +859,19 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
       // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
       f4 z[4];
       load_vp(z, blob + OFF_VEC + V_BN1 * 64, g);
-      mfma_dense<8>(z, blob + OFF_WN1, in8, lane);
+      if (__builtin_expect(__any(fmaxf(amax_ecl(hr), amax_ecl(Mr)) > H16_LIMIT), 0)) {
+        mfma_dense<8>(z, blob + OFF_WN1, in8, lane);
+      } else {
+        h8 xh[2], xl[2];
+        h16_split(hr, xh, xl);
+        mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1A * 4096), xh, xl, lane);
+        h16_split(Mr, xh, xl);
+        mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1B * 4096), xh, xl, lane);
+      }
       silu_ecl(z);
       f4 hn[4];
       load_vp(hn, blob + OFF_VEC + V_BN2 * 64, g);
-      mfma_dense<4>(hn, blob + OFF_WN2, z, lane);
+      mm64(hn, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN2 * 4096), blob + OFF_WN2, z, lane);
       if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
@@ -818,8 +888,11 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         }
       }
     }
+    STAMP(12);
     __syncthreads();
+    STAMP(13);
   }
+  STAMP_FLUSH
 }
 
 // ---- temporal spectral layers -----------------------------------------------------------------
@@ -1084,7 +1157,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   static const int dbg = getenv("NONODE_DEBUG") ? atoi(getenv("NONODE_DEBUG")) : 0;
   // wave configuration (NONODE_CFG): 0 = 8 waves, one unit per iteration; 1 = 4 waves (one per
   // SIMD, 512-register budget), two units per iteration; 2 = 8 waves, two units per iteration
-  static const int cfg = getenv("NONODE_CFG") ? atoi(getenv("NONODE_CFG")) : 0;
+  static const int cfg = getenv("NONODE_CFG") ? atoi(getenv("NONODE_CFG")) : 1;
   a.debug = dbg;
   a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
   ProfScope prof(VARIANT, stream);
@@ -1143,7 +1216,7 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
   a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
   a.ne = n_edge_feat;
   a.blob = blob;
-  hipLaunchKernelGGL(pack_kernel, dim3(32, 10), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_kernel, dim3(32, 16), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_kernel");
 }
 
@@ -1337,6 +1410,18 @@ int nonode_profile_end(float* ms_out, int* kind_out, int max_out) {
   g_prof.n = 0;
   return n;
 }
+
+#if NONODE_STAMP
+// diagnostic builds only: read and clear the accumulated per-section wave cycles
+int nonode_debug_stamps(unsigned long long* out16) {
+  if (hipDeviceSynchronize() != hipSuccess) return fail(NONODE_ELAUNCH, "stamps: sync");
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamp), 16 * sizeof(unsigned long long)) != hipSuccess)
+    return fail(NONODE_ELAUNCH, "stamps: copy");
+  unsigned long long z[16] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return fail(NONODE_ELAUNCH, "stamps: clear");
+  return NONODE_OK;
+}
+#endif
 
 }  // extern "C"
 

@@ -1,0 +1,67 @@
+"""Batch sharding across ranks (one process per GPU).
+
+The rollout path partitions by trajectory sample: every sample's graph, edge features and
+trajectory are independent of every other sample (EGNO/model/egno.py:37-111 and
+SEGNO/models/model.py:95-102 never mix rows of different samples). A job over B_global samples
+on W ranks therefore gives rank r the contiguous sample range shard_range(B_global, W, r), runs
+the kernels on it with no collective in the data path, and only the timing (max over ranks) and
+optional result collection touch the process group.
+
+The reference runs single-process (main.py:27-31 picks one device); this module is the
+MI355X-side replacement for "one big batch on one device".
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total, world, rank):
+    """Contiguous, balanced [lo, hi) slice of `total` samples for `rank` of `world`
+    (sizes differ by at most one; the union over ranks is exactly range(total))."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    if total < 0:
+        raise ValueError(f"bad total {total}")
+    return (total * rank) // world, (total * (rank + 1)) // world
+
+
+def _initialized():
+    return dist.is_available() and dist.is_initialized()
+
+
+def _reduce_device(dev):
+    # RCCL reduces device tensors; gloo reduces host tensors
+    return dev if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def max_over_ranks(value, dev=torch.device("cpu")):
+    """Max of a host float over all ranks (the bench's step time): one scalar all-reduce."""
+    if not _initialized() or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(dev))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(value, dev=torch.device("cpu")):
+    """Sum of a host number over all ranks (e.g. samples processed)."""
+    if not _initialized() or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(dev))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def gather_samples(local, total):
+    """Concatenate every rank's per-sample rows (dim 0 = local samples of shard_range order) into
+    the full [total, ...] tensor on every rank. Result collection only — outside timed regions."""
+    if not _initialized() or dist.get_world_size() == 1:
+        return local
+    world = dist.get_world_size()
+    dev = _reduce_device(local.device)
+    sizes = [shard_range(total, world, r) for r in range(world)]
+    pad = max(hi - lo for lo, hi in sizes)
+    buf = torch.zeros((pad,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    buf[: local.shape[0]] = local.to(dev)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    return torch.cat([p[: hi - lo] for p, (lo, hi) in zip(parts, sizes)]).to(local.device)

@@ -1,0 +1,125 @@
+"""Multi-rank path on the CPU: world_size-2 gloo process groups.
+
+The rollout shards by sample with no collective in the data path (no_node_comparison_amd/sharding.py);
+these tests check the shard assignment, the bench's per-rank inputs, the timing reduction, and that
+per-rank results reassembled on rank 0 equal a single-process run of the whole batch. The per-rank
+compute here is the oracle (test infrastructure; the kernels themselves need the GPU and are
+covered by tests/test_gpu_parity.py, including batch independence).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.conftest import load_golden, params_of, maxnorm_rel
+from no_node_comparison_amd.sharding import shard_range, gather_samples, max_over_ranks, sum_over_ranks
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, fn, *args):
+    port = _free_port()
+    mp.start_processes(_entry, args=(world, port, fn, args), nprocs=world, join=True, start_method="spawn")
+
+
+def _entry(rank, world, port, fn, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world, *args)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("total,world", [(0, 2), (1, 2), (7, 2), (512, 8), (4096, 8), (13, 5)])
+def test_shard_range_partitions(total, world):
+    parts = [shard_range(total, world, r) for r in range(world)]
+    assert parts[0][0] == 0 and parts[-1][1] == total
+    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+    sizes = [hi - lo for lo, hi in parts]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_range_rejects():
+    with pytest.raises(ValueError):
+        shard_range(8, 2, 2)
+    with pytest.raises(ValueError):
+        shard_range(8, 0, 0)
+
+
+def _reductions(rank, world):
+    assert max_over_ranks(1.5 + rank) == 1.5 + world - 1
+    assert sum_over_ranks(rank + 1) == world * (world + 1) / 2
+    lo, hi = shard_range(7, world, rank)
+    local = torch.full((hi - lo, 2), float(rank))
+    full = gather_samples(local, 7)
+    assert full.shape == (7, 2)
+    for r in range(world):
+        a, b = shard_range(7, world, r)
+        assert torch.all(full[a:b] == r)
+
+
+def test_reductions_gloo_ws2():
+    _run(2, _reductions)
+
+
+def _bench_shards(rank, world, B_per, N):
+    import bench
+    loc, vel, q = bench.rank_batch(B_per, world, rank, N, seed=99)
+    gl, gv, gq = bench.synthetic_charged(B_per * world, N, 99)
+    lo, hi = shard_range(B_per * world, world, rank)
+    assert loc.shape == (B_per, N, 3)
+    assert torch.equal(loc, gl[lo:hi]) and torch.equal(vel, gv[lo:hi]) and torch.equal(q, gq[lo:hi])
+    full = gather_samples(loc, B_per * world)
+    assert torch.equal(full, gl)
+
+
+def test_bench_rank_inputs_gloo_ws2():
+    _run(2, _bench_shards, 3, 5)
+
+
+def _egno_sharded(rank, world, total):
+    """Each rank runs the EGNO forward (oracle) on its sample shard; rank-0 reassembly must equal
+    the whole-batch run (the path has no cross-sample coupling, egno.py:37-111)."""
+    from oracle import egno as oe
+    from oracle import harness as oh
+    fx = load_golden("egno_fwd")
+    p = params_of(fx)
+    N = 5
+    rng = np.random.default_rng(7)
+    loc = rng.standard_normal((total, N, 3)).astype(np.float32)
+    vel = rng.standard_normal((total, N, 3)).astype(np.float32)
+    q = rng.choice([-1.0, 1.0], size=(total, N, 1)).astype(np.float32)
+    T = 10
+
+    def run(lo, hi):
+        B = hi - lo
+        r, c = oh.full_edges(B, N)
+        qq = q[lo:hi].reshape(-1, 1)
+        x, v, ea, nodes, lm = oh.prepare_inputs(loc[lo:hi], vel[lo:hi], qq[r] * qq[c], r, c, N, q[lo:hi])
+        t_out = np.tile(np.arange(1, T + 1, dtype=np.float32), (B, 1))
+        xo, vo, ho = oe.egno_forward(p, x, nodes, r, c, ea, v, lm, t_out, T=T)
+        return xo.reshape(T, B, N, 3).transpose(1, 0, 2, 3)     # [B, T, N, 3] per sample
+
+    lo, hi = shard_range(total, world, rank)
+    mine = torch.from_numpy(np.ascontiguousarray(run(lo, hi)))
+    full = gather_samples(mine, total).numpy()
+    if rank == 0:
+        ref = run(0, total)
+        assert maxnorm_rel(full, ref) < 1e-6
+
+
+def test_egno_sharded_equals_whole_batch_gloo_ws2():
+    fx = load_golden("egno_fwd")
+    if "w::embedding.weight" not in fx:
+        pytest.skip("golden weights missing")
+    _run(2, _egno_sharded, 5)
