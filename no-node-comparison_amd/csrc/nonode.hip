@@ -29,6 +29,8 @@ namespace {
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f8 __attribute__((ext_vector_type(8)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 #ifndef NONODE_REG_FRAGS
 #define NONODE_REG_FRAGS 1
@@ -204,13 +206,32 @@ __device__ __forceinline__ void load_frags(f4 (&a)[4], const float* wf, int mt, 
 // fp32 as W_lo x_hi + W_hi x_lo + W_hi x_hi (the dropped W_lo x_lo term is ~2^-22 relative).
 // The ECL accumulator of one layer is the B operand of v_mfma_f32_16x16x32_f16 for the next:
 // k-step s, half j of lane (g, e) = channel 16*(2s + (j>>2)) + 4g + (j&3) of column e.
+// x - (float)half(hp): one v_fma_mix_f32 (f16 operand taken from the low / high half of hp). For
+// |x| in the fp16 range the difference is exactly representable, so the residual is exact.
+__device__ __forceinline__ float resid_lo(unsigned hp, float x) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(x));
+  return r;
+}
+__device__ __forceinline__ float resid_hi(unsigned hp, float x) {
+  float r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(x));
+  return r;
+}
 __device__ __forceinline__ void h16_split(const f4 (&x)[4], h8 (&hi)[2], h8 (&lo)[2]) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const f8 v = {x[2 * s][0], x[2 * s][1], x[2 * s][2], x[2 * s][3],
                   x[2 * s + 1][0], x[2 * s + 1][1], x[2 * s + 1][2], x[2 * s + 1][3]};
     hi[s] = __builtin_convertvector(v, h8);                       // v_cvt_pk_f16_f32 (RNE)
-    lo[s] = __builtin_convertvector(v - __builtin_convertvector(hi[s], f8), h8);
+    const auto hw = __builtin_bit_cast(u4, hi[s]);
+    f8 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      r[2 * i] = resid_lo(hw[i], v[2 * i]);
+      r[2 * i + 1] = resid_hi(hw[i], v[2 * i + 1]);
+    }
+    lo[s] = __builtin_convertvector(r, h8);
   }
 }
 __device__ __forceinline__ float amax_ecl(const f4 (&x)[4]) {
@@ -329,11 +350,19 @@ __device__ __forceinline__ void load_vp(f4 (&d)[4], const float* vp, int g) {
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) d[mt] = *reinterpret_cast<const f4*>(vp + 16 * g + 4 * mt);
 }
+// SiLU of the 16 ECL values, with the add / multiply as packed f32 ops (one wave per SIMD issues
+// a v_pk_* at the cost of a plain VALU op)
 __device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) a[mt][q] = silu(a[mt][q]);
+    for (int q = 0; q < 4; q += 2) {
+      const f2 z = {a[mt][q], a[mt][q + 1]};
+      const f2 d = f2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.0f;
+      const f2 y = z * f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+      a[mt][q] = y.x;
+      a[mt][q + 1] = y.y;
+    }
 }
 #ifndef NONODE_ABLATE
 #define NONODE_ABLATE 0   // 1: compile the phase-B internal ablation bits (8/16/32) into the kernel
@@ -606,12 +635,15 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
       const int U = (p.debug & 1) ? 0 : ctc * Nm1;
       const int u0 = (wave * U) / NW, u1 = ((wave + 1) * U) / NW;
       int u = u0;
-#if NONODE_REG_FRAGS
-      // W2 / Wc1 fp16 fragments stay in registers for the whole edge phase (loop invariant)
+      // 8-wave single-unit loop: W2 / Wc1 fp16 fragments stay in registers for the edge phase.
+      // PAIR reads them from LDS (each read feeds two units' MFMAs; the registers go to the
+      // second unit instead)
+      constexpr bool REGF = NONODE_REG_FRAGS && !PAIR;
       H16Frags fw2, fwc1;
-      load_h16frags(fw2, reinterpret_cast<const h8*>(sW), lane);
-      load_h16frags(fwc1, reinterpret_cast<const h8*>(sW + 4096), lane);
-#endif
+      if (REGF) {
+        load_h16frags(fw2, reinterpret_cast<const h8*>(sW), lane);
+        load_h16frags(fwc1, reinterpret_cast<const h8*>(sW + 4096), lane);
+      }
       // PAIR (one wave per SIMD): b2 / bc1 / wc2 also stay in registers for the edge phase
       f4 rB2[4], rBC1[4], rWC2[4];
       if (PAIR) {
@@ -699,8 +731,60 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         const float* wc1f = p.blob + OFF_WC1;
         int k = k_lo;
         if (PAIR) {
-          // Two units (32 edges, same receivers) per iteration: two independent dependency chains
-          // the scheduler interleaves, so one unit's MFMAs issue beside the other's SiLU work.
+          // Two units (32 edges, same receivers) per iteration. The hot body is ONE basic block:
+          // both units always take the fp16x3 path while the largest |activation| is tracked, and
+          // only if it exceeded the fp16 range (rare) is the pair recomputed on exact f32 MFMAs
+          // before its sums are committed. So the scheduler can put one unit's MFMAs beside the
+          // other unit's SiLU work.
+          f4 pr[4];
+          load_ecl(pr, Prow, g);                       // receiver projection, fixed for the segment
+          auto head2 = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
+              __attribute__((always_inline)) {
+            int j = n + k;
+            j = (j >= N) ? j - N : j;
+            const int sl = sb + j;
+            const float* xs = sX + sl * 4;
+            r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
+            const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+            load_ecl(a, sQ + sl * ROWP, g);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) {
+              const int fi = 4 * kf + g;
+              const float bv = (fi == 0) ? d2 : ((fi - 1 < p.ne) ? ev[kf] : 0.f);
+              const f4 wf = *reinterpret_cast<const f4*>(vFEAT + kf * 256 + lane * 4);
+#pragma unroll
+              for (int mo = 0; mo < 4; ++mo) a[mo] = mfma(wf[mo], bv, a[mo]);
+            }
+          };
+          auto edge_f = [&](f4 (&c1)[4], float r0, float r1, float r2, float& f0, float& f1, float& f2)
+              __attribute__((always_inline)) {
+            silu_ecl(c1);
+            const float c = dot_r(c1, rWC2) + bc2;
+            f0 = r0 * c; f1 = r1 * c; f2 = r2 * c;
+            if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
+              f0 = fminf(fmaxf(f0, -100.f), 100.f);
+              f1 = fminf(fmaxf(f1, -100.f), 100.f);
+              f2 = fminf(fmaxf(f2, -100.f), 100.f);
+            }
+          };
+          // exact f32 recomputation of one unit (the guard path)
+          auto exact_unit = [&](int k, const float (&ev)[KF], f4 (&m)[4], float& f0, float& f1, float& f2)
+              __attribute__((always_inline)) {
+            f4 a[4], c[4];
+            float r0, r1, r2;
+            head2(k, ev, a, r0, r1, r2);
+            silu_ecl(a);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
+            mfma_dense<4>(m, w2f, a, lane);
+            silu_ecl(m);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
+            mfma_dense<4>(c, wc1f, m, lane);
+            edge_f(c, r0, r1, r2, f0, f1, f2);
+          };
           float e0[KF], e1[KF];
           fetch_ef(k, e0);
           fetch_ef(min(k + 1, k_hi), e1);
@@ -709,45 +793,60 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             float n0[KF], n1[KF];
             fetch_ef(min(k + 2, k_hi), n0);
             fetch_ef(min(k + 3, k_hi), n1);
+            // fragment reads stay in the loop (LICM would pin 128 VGPRs of loop-invariant weights)
+            int foff = 0;
+            asm volatile("" : "+v"(foff));
+            const h8* w2l = w2h + foff;
+            const h8* wc1l = wc1h + foff;
             f4 a0[4], a1[4], m0[4], m1[4];
             float r00, r01, r02, r10, r11, r12;
-            head(k, e0, a0, r00, r01, r02);
-            head(k + 1, e1, a1, r10, r11, r12);
-#pragma unroll
-            for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
+            head2(k, e0, a0, r00, r01, r02);
+            head2(k + 1, e1, a1, r10, r11, r12);
             STAMP(0);
             silu_ecl(a0);
             silu_ecl(a1);
+            float gmax = fmaxf(amax_ecl(a0), amax_ecl(a1));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; }
-            if (__builtin_expect(__any(fmaxf(amax_ecl(a0), amax_ecl(a1)) > H16_LIMIT), 0)) {
-              mfma_dense<4>(m0, w2f, a0, lane);
-              mfma_dense<4>(m1, w2f, a1, lane);
-            } else {
+            {
               h8 ah0[2], al0[2], ah1[2], al1[2];
               h16_split(a0, ah0, al0);
               h16_split(a1, ah1, al1);
-              mfma_h16r2(m0, m1, fw2, ah0, al0, ah1, al1);
+              mfma_h16x2(m0, m1, w2l, ah0, al0, ah1, al1, lane);   // m = SiLU(W2 a + b2)
             }
             STAMP(1);
             silu_ecl(m0);
             silu_ecl(m1);
+            gmax = fmaxf(gmax, fmaxf(amax_ecl(m0), amax_ecl(m1)));
+            f4 pm[4];
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) msum[mt] += m0[mt] + m1[mt];
-#pragma unroll
-            for (int mt = 0; mt < 4; ++mt) { a0[mt] = rBC1[mt]; a1[mt] = rBC1[mt]; }
-            if (__builtin_expect(__any(fmaxf(amax_ecl(m0), amax_ecl(m1)) > H16_LIMIT), 0)) {
-              mfma_dense<4>(a0, wc1f, m0, lane);
-              mfma_dense<4>(a1, wc1f, m1, lane);
-            } else {
+            for (int mt = 0; mt < 4; ++mt) {
+              pm[mt] = m0[mt] + m1[mt];
+              a0[mt] = rBC1[mt];
+              a1[mt] = rBC1[mt];
+            }
+            {
               h8 mh0[2], ml0[2], mh1[2], ml1[2];
               h16_split(m0, mh0, ml0);
               h16_split(m1, mh1, ml1);
-              mfma_h16r2(a0, a1, fwc1, mh0, ml0, mh1, ml1);
+              mfma_h16x2(a0, a1, wc1l, mh0, ml0, mh1, ml1, lane);  // coord hidden: SiLU(Wc1 m + bc1)
             }
             STAMP(2);
-            tail(a0, r00, r01, r02);
-            tail(a1, r10, r11, r12);
+            float f00, f01, f02, f10, f11, f12;
+            edge_f(a0, r00, r01, r02, f00, f01, f02);
+            edge_f(a1, r10, r11, r12, f10, f11, f12);
+            if (__builtin_expect(__any(gmax > H16_LIMIT), 0)) {
+              f4 x0[4], x1[4];
+              exact_unit(k, e0, x0, f00, f01, f02);
+              exact_unit(k + 1, e1, x1, f10, f11, f12);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) pm[mt] = x0[mt] + x1[mt];
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) msum[mt] += pm[mt];
+            fs0 += f00 + f10; fs1 += f01 + f11; fs2 += f02 + f12;
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
             STAMP(3);
           }
         }
@@ -772,11 +871,11 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           } else {
             h8 ah[2], al[2];
             h16_split(a, ah, al);
-#if NONODE_REG_FRAGS
-            if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(m, fw2, ah, al);      // m = SiLU(W2 a + b2)
-#else
-            mfma_h16(m, w2h, ah, al, lane);                      // m = SiLU(W2 a + b2)
-#endif
+            if (REGF) {
+              if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(m, fw2, ah, al);    // m = SiLU(W2 a + b2)
+            } else {
+              mfma_h16(m, w2h, ah, al, lane);
+            }
           }
           STAMP(1);
           silu_ecl_dbg(m, p.debug);
@@ -788,11 +887,11 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           } else {
             h8 mh[2], ml[2];
             h16_split(m, mh, ml);
-#if NONODE_REG_FRAGS
-            if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(a, fwc1, mh, ml);     // coord hidden: SiLU(Wc1 m + bc1)
-#else
-            mfma_h16(a, wc1h, mh, ml, lane);                     // coord hidden: SiLU(Wc1 m + bc1)
-#endif
+            if (REGF) {
+              if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(a, fwc1, mh, ml);   // SiLU(Wc1 m + bc1)
+            } else {
+              mfma_h16(a, wc1h, mh, ml, lane);
+            }
           }
           STAMP(2);
           tail(a, r0, r1, r2);
