@@ -31,6 +31,9 @@ HBM_PEAK_GBS = 8000.0
 #   per node: 24640 MAC (P, Q projections 2x64x64, node_v 64x64+64, node MLP 128x64+64x64)
 MAC_PER_EDGE = 8448
 MAC_PER_NODE = 24640
+# SEGNO_GCL (gcl.py:71-119): per edge W2 + Wc1 + vectors as EGNO; per node P, Q + node MLP (no phi_v)
+MAC_PER_EDGE_SEGNO = 8448
+MAC_PER_NODE_SEGNO = 20480
 
 
 def synthetic_charged(B, N, seed):
@@ -173,6 +176,91 @@ def run_egno(args, world, rank, dev):
     return res
 
 
+def synthetic_gravity(B, N, seed):
+    """SURVEY §8d gravity generator: masses 1 + 0.1 N(0,1); positions, velocities ~ N(0,1) with the
+    centre-of-mass velocity removed (synthetic_sim.py:370-378)."""
+    g = torch.Generator().manual_seed(seed)
+    mass = 1.0 + 0.1 * torch.randn(B, N, 1, generator=g)
+    loc = torch.randn(B, N, 3, generator=g)
+    vel = torch.randn(B, N, 3, generator=g)
+    vel = vel - (mass * vel).sum(1, keepdim=True) / mass.sum(1, keepdim=True)
+    return loc, vel, mass
+
+
+def c5_substeps(total=50, seed=0):
+    """C5 multi-horizon substep list: draws in [5, 10) from default_rng(0) until they sum to 50
+    (the last one clipped), SURVEY §8d."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while sum(out) < total:
+        out.append(int(min(rng.integers(5, 10), total - sum(out))))
+    return out
+
+
+def run_segno(args, world, rank, dev, gravity=False):
+    """C3 (SEGNO charged N=20, B=512 per GPU, one forward of 10 substeps) or C5 (SEGNO gravity
+    N=100, B=256 per GPU, a 50-frame multi-horizon rollout: segments of c5_substeps() substeps)."""
+    import no_node_comparison_amd as pkg
+    from no_node_comparison_amd.sharding import max_over_ranks
+    N = 100 if gravity else 20
+    B = args.batch if args.batch != 512 or not gravity else 256
+    torch.manual_seed(0)
+    model = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=4, recurrent=True, device=dev).eval()
+    gen = synthetic_gravity if gravity else synthetic_charged
+    loc, vel, q = gen(B * world, N, 4321)
+    from no_node_comparison_amd.sharding import shard_range
+    lo, hi = shard_range(B * world, world, rank)
+    loc, vel, q = loc[lo:hi].to(dev), vel[lo:hi].to(dev), q[lo:hi].to(dev)
+    edges = pkg.harness.get_edges(B, N, dev)
+    x = loc.reshape(-1, 3)
+    v = vel.reshape(-1, 3)
+    qq = q.reshape(-1, 1)
+    ea = torch.cat([qq[edges[0]] * qq[edges[1]], ((x[edges[0]] - x[edges[1]]) ** 2).sum(-1, keepdim=True)], 1)
+    his = v.norm(dim=-1, keepdim=True)
+    steps = c5_substeps() if gravity else [10]
+
+    def call():
+        xx, vv = x, v
+        for T in steps:
+            xx, _, vv = model(his, xx, edges, vv, ea, T=T)
+        return xx
+
+    from no_node_comparison_amd import _lib
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            call()
+        barrier_sync(world, dev)
+        if args.kernel_events:
+            _lib.profile_begin(8 * args.steps * len(steps) + 64)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            call()
+        barrier_sync(world, dev)
+        el = time.perf_counter() - t0
+        records = _lib.profile_end() if args.kernel_events else []
+    el = max_over_ranks(el, dev)
+    value = B * world * args.steps / el
+    name = "C5: SEGNO gravity N=100, 50-frame multi-horizon rollout" if gravity else \
+        "C3: SEGNO charged N=20, 10 integrator substeps (one fused launch)"
+    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d, seeded)",
+           "config": {"workload": f"{name}, B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world,
+                      "n_balls": N, "substeps": steps, "parallelism": f"batch-sharded replicas x{world}"}}
+    layer = [ms for kind, ms in records if kind == _lib.VARIANT_SEGNO]
+    if layer:
+        E = B * N * (N - 1) * sum(steps) / len(steps)
+        n = B * N * sum(steps) / len(steps)
+        avg = float(np.mean(layer))
+        flop = 2.0 * (E * MAC_PER_EDGE_SEGNO + n * MAC_PER_NODE_SEGNO)
+        ach = flop / (avg * 1e-3) / 1e12
+        res["roofline"] = {"kernel": "egnn_layer_kernel<SEGNO> (fused substeps)", "bound": "mfma",
+                           "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP32_PEAK_TFLOPS,
+                           "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
+                           "launches_timed": len(layer)}
+    return res
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -189,14 +277,18 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=512, help="samples per GPU")
-    ap.add_argument("--workload", default="egno", choices=["egno"])
+    ap.add_argument("--workload", default="egno", choices=["egno", "segno", "segno_gravity"],
+                    help="egno = C2 (the headline line); segno = C3; segno_gravity = C5")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", dest="kernel_events", action="store_false")
     args = ap.parse_args()
     world, rank, dev = setup_dist()
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    res = run_egno(args, world, rank, dev)
+    if args.workload == "egno":
+        res = run_egno(args, world, rank, dev)
+    else:
+        res = run_segno(args, world, rank, dev, gravity=args.workload == "segno_gravity")
     if rank == 0:
         print(json.dumps(res))
     if world > 1:

@@ -524,7 +524,11 @@ struct LayerArgs {
   const float* __restrict__ h; const float* __restrict__ x; const float* __restrict__ v;
   const float* __restrict__ ef; const float* __restrict__ blob;
   float* h_out; float* x_out; float* v_out;
-  int n_total, N, ne, ef_mod, n_tiles, ct, s_max, recurrent;
+  // fused substeps (SEGNO forward_step): step s reads (h, x, v) for s = 0, else pp_*[(s-1)&1], and
+  // writes pp_*[s&1], the last step the *_out arrays
+  float* pp_h[2]; float* pp_x[2]; float* pp_v[2];
+  int steps;
+  int n_total, n_graphs, N, ne, ef_mod, ct, s_max, recurrent;
   int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections,
                // 8 no edge-feature loads, 16 SiLU -> clamp, 32 skip the per-edge fp16 MFMAs
   float inv_deg, dt, cw;
@@ -537,7 +541,8 @@ size_t layer_lds_floats(int ct, int N, int* s_max_out) {
          (size_t)ct * 16 * 4;
 }
 
-// One workgroup (8 waves) walks a contiguous range of 16-receiver tiles in chunks of `ct` tiles.
+// One workgroup owns a contiguous range of whole graphs (so every sender of its receivers is its
+// own: substeps need no grid-wide sync) and walks it as 16-receiver tiles, in chunks of `ct` tiles.
 // Per chunk:  A) P = W1[h_i] h + b1 for receivers, Q = W1[h_j] h for every sender of the touched
 //                graphs (LDS tables), sender positions;
 //             B) (tile, k) units split evenly over the waves: receiver r (lane column) meets
@@ -569,24 +574,32 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
   const float* vWC2_ = sV + 512 + V_WC2 * 64;
 
   const int G = gridDim.x;
-  const int t_begin = (int)(((long long)blockIdx.x * p.n_tiles) / G);
-  const int t_end = (int)(((long long)(blockIdx.x + 1) * p.n_tiles) / G);
+  const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;         // first receiver
+  const int nend = (int)(((long long)(blockIdx.x + 1) * p.n_graphs) / G) * N;  // one past the last
   __syncthreads();
 
-  const int ntw = t_end - t_begin;
+  const int ntw = (nend - nb + 15) >> 4;
   const int nch = (ntw + p.ct - 1) / p.ct;
   STAMP_DECL
   #pragma unroll 1
+  for (int step = 0; step < p.steps; ++step) {
+  const float* __restrict__ hI = step == 0 ? p.h : p.pp_h[(step - 1) & 1];
+  const float* __restrict__ xI = step == 0 ? p.x : p.pp_x[(step - 1) & 1];
+  const float* __restrict__ vI = step == 0 ? p.v : p.pp_v[(step - 1) & 1];
+  float* hO = step == p.steps - 1 ? p.h_out : p.pp_h[step & 1];
+  float* xO = step == p.steps - 1 ? p.x_out : p.pp_x[step & 1];
+  float* vO = step == p.steps - 1 ? p.v_out : p.pp_v[step & 1];
+  #pragma unroll 1
   for (int ci = 0; ci < nch; ++ci) {
-    const int c0 = t_begin + (ci * ntw) / nch;
-    const int ctc = t_begin + ((ci + 1) * ntw) / nch - c0;
+    const int c0 = (ci * ntw) / nch;
+    const int ctc = ((ci + 1) * ntw) / nch - c0;
     // keep per-chunk loads of weights/vectors inside the loop (LICM would pin them in VGPRs
     // across all phases)
     int boff = 0;
     asm volatile("" : "+s"(boff));
     const float* blob = p.blob + boff;
-    const int rbase = c0 * 16;
-    const int r_last = min(rbase + ctc * 16, p.n_total) - 1;
+    const int rbase = nb + c0 * 16;
+    const int r_last = min(rbase + ctc * 16, nend) - 1;
     const int g_lo = rbase / N, g_hi = r_last / N;
     const int s0 = g_lo * N;
     const int S = (g_hi - g_lo + 1) * N;
@@ -601,17 +614,17 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     }
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
-      sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
+      sX[s * 4 + d] = xI[(size_t)(s0 + s) * 3 + d];
     }
     #pragma unroll 1
     for (int job = wave; job < ((p.debug & 4) ? 0 : ctc + nsT); job += NW) {
       const bool isP = job < ctc;                       // wave-uniform
       const int local = (isP ? job : job - ctc) * 16 + e;
       int node = isP ? rbase + local : s0 + local;
-      const bool valid = isP ? (node < p.n_total) : (local < S);
-      node = valid ? node : (isP ? p.n_total - 1 : s0);
+      const bool valid = isP ? (node < nend) : (local < S);
+      node = valid ? node : (isP ? nend - 1 : s0);
       f4 hin[4];
-      load_ecl(hin, p.h + (size_t)node * HID, g);
+      load_ecl(hin, hI + (size_t)node * HID, g);
       f4 acc[4];
       if (isP) {
         load_vp(acc, blob + OFF_VEC + V_B1 * 64, g);
@@ -660,8 +673,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         // ---- tile state ----
         const int rl = 16 * tau + e;
         const int r = rbase + rl;
-        const bool rvalid = r < p.n_total;
-        const int rc = rvalid ? r : p.n_total - 1;
+        const bool rvalid = r < nend;
+        const int rc = rvalid ? r : nend - 1;
         const int gr = rc / N;
         const int n = rc - gr * N;
         const int sb = gr * N - s0;
@@ -922,17 +935,17 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     for (int tau = wave; tau < ((p.debug & 2) ? 0 : ctc); tau += NW) {
       const int rl = 16 * tau + e;
       const int r = rbase + rl;
-      const bool rvalid = r < p.n_total;
-      const int rc = rvalid ? r : p.n_total - 1;
+      const bool rvalid = r < nend;
+      const int rc = rvalid ? r : nend - 1;
       f4 in8[8];
       f4 hr[4], Mr[4];
-      load_ecl(hr, p.h + (size_t)rc * HID, g);
+      load_ecl(hr, hI + (size_t)rc * HID, g);
       load_ecl(Mr, sM + rl * ROWP, g);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
       const float F0 = sF[rl * 4 + 0], F1 = sF[rl * 4 + 1], F2 = sF[rl * 4 + 2];
-      const float* xp = p.x + (size_t)rc * 3;
-      const float* vpn = p.v + (size_t)rc * 3;
+      const float* xp = xI + (size_t)rc * 3;
+      const float* vpn = vI + (size_t)rc * 3;
       const float x0 = xp[0], x1 = xp[1], x2 = xp[2];
       const float v0 = vpn[0], v1 = vpn[1], v2 = vpn[2];
       float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
@@ -976,12 +989,12 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
       }
       if (rvalid) {
-        store_ecl(p.h_out + (size_t)r * HID, hn, g);
+        store_ecl(hO + (size_t)r * HID, hn, g);
         if (g == 0) {
-          float* xo = p.x_out + (size_t)r * 3;
+          float* xo = xO + (size_t)r * 3;
           xo[0] = nx0; xo[1] = nx1; xo[2] = nx2;
           if (VARIANT == SEGNO) {
-            float* vo = p.v_out + (size_t)r * 3;
+            float* vo = vO + (size_t)r * 3;
             vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
           }
         }
@@ -990,6 +1003,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     STAMP(12);
     __syncthreads();
     STAMP(13);
+  }
   }
   STAMP_FLUSH
 }
@@ -1235,15 +1249,17 @@ void launch_cfg(int kf, int G, size_t lds, hipStream_t stream, const LayerArgs& 
   if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, NW, PAIR>), dim3(G), dim3(NW * 64), lds, stream, a);
   else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, NW, PAIR>), dim3(G), dim3(NW * 64), lds, stream, a);
 }
+// steps > 1 runs that many substeps in one launch (SEGNO forward_step), ping-ponging through
+// pp = {h0, h1, x0, x1, v0, v1} (each n_graphs*N rows)
 template <int VARIANT>
 int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const float* x,
                  const float* v, const float* ef, const float* blob, float dt, float cw, int recurrent,
-                 float* h_out, float* x_out, float* v_out, hipStream_t stream) {
+                 float* h_out, float* x_out, float* v_out, hipStream_t stream, int steps = 1,
+                 float* const* pp = nullptr) {
   const int n_total = n_graphs * N;
-  const int n_tiles = (n_total + 15) / 16;
   const int cus = num_cus();
-  const int G = n_tiles < cus ? n_tiles : cus;
-  const int tiles_per = (n_tiles + G - 1) / G;
+  const int G = n_graphs < cus ? n_graphs : cus;
+  const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
   int ct = 8 < tiles_per ? 8 : tiles_per;
   int s_max = 0;
   while (ct > 1 && layer_lds_floats(ct, N, &s_max) * 4 > 160 * 1024) --ct;
@@ -1252,7 +1268,14 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
-  a.n_total = n_total; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.n_tiles = n_tiles; a.ct = ct;
+  a.n_total = n_total; a.n_graphs = n_graphs; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.ct = ct;
+  if (steps < 1 || (steps > 1 && !pp)) return fail(NONODE_EINVAL, "layer: steps=%d", steps);
+  a.steps = steps;
+  for (int i = 0; i < 2; ++i) {
+    a.pp_h[i] = pp ? pp[i] : nullptr;
+    a.pp_x[i] = pp ? pp[2 + i] : nullptr;
+    a.pp_v[i] = pp ? pp[4 + i] : nullptr;
+  }
   static const int dbg = getenv("NONODE_DEBUG") ? atoi(getenv("NONODE_DEBUG")) : 0;
   // wave configuration (NONODE_CFG): 0 = 8 waves, one unit per iteration; 1 = 4 waves (one per
   // SIMD, 512-register budget), two units per iteration; 2 = 8 waves, two units per iteration
@@ -1427,7 +1450,7 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
 
 size_t nonode_segno_workspace_bytes(int B, int N) {
   const size_t n = (size_t)B * N;
-  return (2 * n * 64 + 4 * n * 3 + 64) * sizeof(float);
+  return (3 * n * 64 + 4 * n * 3 + 64) * sizeof(float);   // embedding | h ping-pong | x, v ping-pong
 }
 
 int nonode_segno_forward_step(int B, int N, int T, int in_node, int n_edge_feat,
@@ -1445,15 +1468,15 @@ int nonode_segno_forward_step(int B, int N, int T, int in_node, int n_edge_feat,
     return fail(NONODE_EINVAL, "segno_forward_step: workspace too small");
   hipStream_t s = (hipStream_t)stream;
   const size_t n = (size_t)B * N;
-  float* hbuf[2] = {(float*)workspace, (float*)workspace + n * 64};
-  float* xbuf[2] = {hbuf[1] + n * 64, hbuf[1] + n * 64 + n * 3};
-  float* vbuf[2] = {xbuf[1] + n * 3, xbuf[1] + n * 6};
+  float* hemb = (float*)workspace;
+  float* pp[6] = {hemb + n * 64, hemb + 2 * n * 64, hemb + 3 * n * 64, hemb + 3 * n * 64 + n * 3,
+                  hemb + 3 * n * 64 + 2 * n * 3, hemb + 3 * n * 64 + 3 * n * 3};
   const float* hc = h_in;
   if (!hc) {
     hipLaunchKernelGGL(embed_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, (int)n, in_node,
-                       his, emb_w, emb_b, hbuf[0]);
+                       his, emb_w, emb_b, hemb);
     if (int rc = check_launch("embed_kernel")) return rc;
-    hc = hbuf[0];
+    hc = hemb;
   }
   if (T == 0) {
     hipMemcpyAsync(h_out, hc, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -1461,20 +1484,10 @@ int nonode_segno_forward_step(int B, int N, int T, int in_node, int n_edge_feat,
     hipMemcpyAsync(v_out, v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
     return check_launch("segno T=0 copy");
   }
-  const float* xc = x;
-  const float* vc = v;
-  const float dt = 1.0f / (float)T;
-  for (int it = 0; it < T; ++it) {
-    const bool last = it == T - 1;
-    float* ho = last ? h_out : (hc == hbuf[0] ? hbuf[1] : hbuf[0]);
-    float* xo = last ? x_out : (xc == xbuf[0] ? xbuf[1] : xbuf[0]);
-    float* vo = last ? v_out : (vc == vbuf[0] ? vbuf[1] : vbuf[0]);
-    if (int rc = launch_layer<SEGNO>(B, N, n_edge_feat, B, hc, xc, vc, edge_attr, blob, dt, coords_weight,
-                                     recurrent, ho, xo, vo, s))
-      return rc;
-    hc = ho; xc = xo; vc = vo;
-  }
-  return NONODE_OK;
+  // all T substeps in one launch: each workgroup owns whole samples, so substep t+1 only needs
+  // its own workgroup's substep-t results (model.py:95-102, gcl.py:111-119)
+  return launch_layer<SEGNO>(B, N, n_edge_feat, B, hc, x, v, edge_attr, blob, 1.0f / (float)T, coords_weight,
+                             recurrent, h_out, x_out, v_out, s, T, pp);
 }
 
 int nonode_profile_begin(int max_records) {
