@@ -44,7 +44,7 @@ def test_size_queries_need_no_gpu():
     B, N, T = 512, 20, 10
     ws = L.nonode_egno_workspace_bytes(B, N, T, B)
     assert ws == (B * N * T * 67 + B * T * 64 + 64) * 4
-    assert L.nonode_segno_workspace_bytes(B, N) == (2 * B * N * 64 + 12 * B * N + 64) * 4
+    assert L.nonode_segno_workspace_bytes(B, N) == (3 * B * N * 64 + 12 * B * N + 64) * 4
 
 
 def test_status_codes_and_last_error():
