@@ -155,6 +155,59 @@ int nonode_egnn_layer(int variant, int n_graphs, int N, int n_edge_feat, int ef_
 int nonode_profile_begin(int max_records);
 int nonode_profile_end(float* ms_out, int* kind_out, int max_out);
 
+/* ---- EGNO training (row a14: loss.backward() of main_simulation_simple_no.py:267-280) ---- */
+
+/* Gradient outputs of ONE layer, same tensors and shapes as nonode_layer_weights (written, not
+ * accumulated). */
+typedef struct {
+  float* edge_w1; float* edge_b1;
+  float* edge_w2; float* edge_b2;
+  float* coord_w1; float* coord_b1;
+  float* coord_w2; float* coord_b2;
+  float* vel_w1; float* vel_b1;
+  float* vel_w2; float* vel_b2;
+  float* node_w1; float* node_b1;
+  float* node_w2; float* node_b2;
+} nonode_layer_grads;
+
+/* Floats in one backward blob (unscaled forward + transposed fragments). */
+size_t nonode_bwd_blob_floats(void);
+/* Pack one EGNO layer for the backward pass (EGNO only). */
+int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
+                          float* bblob, void* stream);
+
+/* Bytes of the saved forward state (every layer's inputs, message / force sums, embedding rows). */
+size_t nonode_egno_train_state_bytes(int B, int N, int T, int n_layers, int in_node, int time_emb_dim);
+
+/* EGNO.forward (egno.py:37-111) that also saves the state the backward needs. Same arguments and
+ * outputs as nonode_egno_forward plus the state buffer. Outputs equal nonode_egno_forward's. */
+int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                              int time_emb_dim, int modes, int Bt,
+                              const float* x, const float* h, const float* v, const float* loc_mean,
+                              const float* edge_fea, const float* t_out,
+                              const float* emb_w, const float* emb_b,
+                              const float* const* blobs, const float* const* tconv_blobs,
+                              const float* const* tconvx_w,
+                              float* x_out, float* v_out, float* h_out,
+                              void* state, size_t state_bytes,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
+size_t nonode_egno_backward_workspace_bytes(int B, int N, int T, int modes);
+
+/* Reverse of nonode_egno_forward_train: given dL/dx_out (and optionally dL/dv_out, dL/dh_out;
+ * NULL = 0), writes the gradient of every EGNO parameter: per layer (layer_grads[l]), the raw
+ * TimeConv / TimeConv_x weights1 ([64][64][modes][2], [2][2][modes][2]) and the embedding Linear.
+ * bblobs from nonode_pack_layer_bwd; tconv_w / tconvx_w are the raw weights1 tensors. */
+int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                         int time_emb_dim, int modes, int Bt,
+                         const float* loc_mean, const float* edge_fea,
+                         const float* const* bblobs, const float* const* tconv_w,
+                         const float* const* tconvx_w, const void* state,
+                         const float* g_x, const float* g_v, const float* g_h,
+                         const nonode_layer_grads* layer_grads, float* const* g_tconv,
+                         float* const* g_tconvx, float* g_emb_w, float* g_emb_b,
+                         void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

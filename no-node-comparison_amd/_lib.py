@@ -18,6 +18,8 @@ SYMBOLS = (
     "nonode_egno_workspace_bytes", "nonode_egno_forward", "nonode_segno_workspace_bytes",
     "nonode_segno_forward_step", "nonode_egno_tconv", "nonode_egnn_layer", "nonode_profile_begin",
     "nonode_profile_end", "nonode_tconv_blob_floats", "nonode_pack_tconv",
+    "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
+    "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
 )
 
 VARIANT_EGNO = 0
@@ -38,6 +40,11 @@ class LayerWeights(ctypes.Structure):
     _fields_ = [(n, _vp) for n in (
         "edge_w1", "edge_b1", "edge_w2", "edge_b2", "coord_w1", "coord_b1", "coord_w2", "coord_b2",
         "vel_w1", "vel_b1", "vel_w2", "vel_b2", "node_w1", "node_b1", "node_w2", "node_b2")]
+
+
+class LayerGrads(ctypes.Structure):
+    """nonode_layer_grads (same fields as LayerWeights, written by nonode_egno_backward)."""
+    _fields_ = LayerWeights._fields_
 
 
 _lib = None
@@ -68,6 +75,17 @@ def lib():
     L.nonode_tconv_blob_floats.argtypes = [_i]
     L.nonode_tconv_blob_floats.restype = _sz
     L.nonode_pack_tconv.argtypes = [_vp, _i, _i, _vp, _vp]
+    L.nonode_bwd_blob_floats.restype = _sz
+    L.nonode_pack_layer_bwd.argtypes = [ctypes.POINTER(LayerWeights), _i, _i, _i, _vp, _vp]
+    L.nonode_egno_train_state_bytes.argtypes = [_i] * 6
+    L.nonode_egno_train_state_bytes.restype = _sz
+    L.nonode_egno_forward_train.argtypes = ([_i] * 9 + [_vp] * 8 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
+                                            + [_sz, _vp, _sz, _vp])
+    L.nonode_egno_backward_workspace_bytes.argtypes = [_i] * 4
+    L.nonode_egno_backward_workspace_bytes.restype = _sz
+    L.nonode_egno_backward.argtypes = ([_i] * 9 + [_vp] * 2 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
+                                       + [ctypes.POINTER(LayerGrads), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]
+                                       + [_vp] * 3 + [_sz, _vp])
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

@@ -1,10 +1,89 @@
-"""Training entry for EGNO (EGNO/main_simulation_simple_no.py:267-280).
+"""Training entry for EGNO: loss.backward() of run_epoch (main_simulation_simple_no.py:267-280).
 
-The backward kernels are not built yet: a forward that must produce gradients raises instead of
-silently falling back to a non-HIP implementation.
+EGNOTrain is a torch.autograd.Function around the C ABI: its forward runs
+nonode_egno_forward_train (same kernels and outputs as the inference forward, plus the saved
+state), its backward runs nonode_egno_backward and returns the gradient of every parameter. The
+reference's training loop (criterion, loss.backward(), optimizer.step()) runs unchanged on top.
 """
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _f32(t):
+    return t.detach().to(torch.float32).contiguous()
+
+
+class EGNOTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, x, h, edge_fea, v, loc_mean, t_out, B, N, *params):
+        L = _lib.lib()
+        T = model.num_timesteps
+        dev = x.device
+        x, h, v, lm, ef, tt = _f32(x), _f32(h), _f32(v), _f32(loc_mean), _f32(edge_fea), _f32(t_out)
+        Bt = tt.shape[0]
+        blobs, tblobs = model._packed()
+        n = T * B * N
+        x_out = torch.empty(n, 3, device=dev)
+        v_out = torch.empty(n, 3, device=dev)
+        h_out = torch.empty(n, model.hidden_nf, device=dev)
+        ws_bytes = L.nonode_egno_workspace_bytes(B, N, T, Bt)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+        st_bytes = L.nonode_egno_train_state_bytes(B, N, T, model.n_layers, model.in_node_nf, model.time_emb_dim)
+        state = torch.empty((st_bytes + 3) // 4, dtype=torch.float32, device=dev)
+        P = ctypes.c_void_p * model.n_layers
+        tcx = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
+        ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
+        _lib.check(L.nonode_egno_forward_train(
+            B, N, T, model.n_layers, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
+            _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef), _lib.ptr(tt), _lib.ptr(ew),
+            _lib.ptr(eb), P(*[blobs[i].data_ptr() for i in range(model.n_layers)]),
+            P(*[tblobs[i].data_ptr() for i in range(model.n_layers)]), P(*[t.data_ptr() for t in tcx]),
+            _lib.ptr(x_out), _lib.ptr(v_out), _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.ptr(ws), ws_bytes,
+            _lib.stream_of(x)))
+        ctx.model, ctx.B, ctx.N, ctx.Bt = model, B, N, Bt
+        ctx.state, ctx.lm, ctx.ef = state, lm, ef
+        ctx.n_params = len(params)
+        return x_out, v_out, h_out
+
+    @staticmethod
+    def backward(ctx, gx, gv, gh):
+        model, B, N, Bt = ctx.model, ctx.B, ctx.N, ctx.Bt
+        L = _lib.lib()
+        T = model.num_timesteps
+        dev = ctx.state.device
+        nl = model.n_layers
+        bblobs = model._packed_bwd()
+        grads = {name: torch.empty_like(p) for name, p in model.named_parameters()}
+        lg = (_lib.LayerGrads * nl)()
+        for i in range(nl):
+            names = model.layer_param_names(i)
+            lg[i] = _lib.LayerGrads(*[grads[nm].data_ptr() for nm in names])
+        P = ctypes.c_void_p * nl
+        tw = [_f32(m.t_conv.weights1) for m in model.time_conv_modules]
+        txw = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
+        g_tc = P(*[grads[f"time_conv_modules.{i}.t_conv.weights1"].data_ptr() for i in range(nl)])
+        g_tcx = P(*[grads[f"time_conv_x_modules.{i}.t_conv.weights1"].data_ptr() for i in range(nl)])
+        ws_bytes = L.nonode_egno_backward_workspace_bytes(B, N, T, model.num_modes)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+        gx = _f32(gx) if gx is not None else torch.zeros(T * B * N, 3, device=dev)
+        gv = _f32(gv) if gv is not None else None
+        gh = _f32(gh) if gh is not None else None
+        _lib.check(L.nonode_egno_backward(
+            B, N, T, nl, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
+            _lib.ptr(ctx.lm), _lib.ptr(ctx.ef), P(*[bblobs[i].data_ptr() for i in range(nl)]),
+            P(*[t.data_ptr() for t in tw]), P(*[t.data_ptr() for t in txw]), _lib.ptr(ctx.state),
+            _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh), lg, g_tc, g_tcx,
+            _lib.ptr(grads["embedding.weight"]), _lib.ptr(grads["embedding.bias"]), _lib.ptr(ws), ws_bytes,
+            _lib.stream_of(gx)))
+        ctx.state = None
+        out = [grads[name] for name, _ in model.named_parameters()]
+        return (None,) * 9 + tuple(out)
 
 
 def egno_forward_train(model, x, h, edge_fea, v, loc_mean, t_out, B, N):
-    raise NotImplementedError("EGNO backward (training) kernels are not built yet; run the forward "
-                              "under torch.no_grad() or model.eval()")
+    """EGNO forward that records the kernels' backward on the autograd tape."""
+    params = [p for _, p in model.named_parameters()]
+    return EGNOTrain.apply(model, x, h, edge_fea, v, loc_mean, t_out, B, N, *params)

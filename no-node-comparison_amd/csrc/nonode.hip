@@ -528,6 +528,9 @@ struct LayerArgs {
   // writes pp_*[s&1], the last step the *_out arrays
   float* pp_h[2]; float* pp_x[2]; float* pp_v[2];
   int steps;
+  // training forward only (else null): per-receiver message sums (true scale) [n][64] and force
+  // sums [n][4] (f summed over the N-1 senders, before the mean and clamp)
+  float* m_out; float* f_out;
   int n_total, n_graphs, N, ne, ef_mod, ct, s_max, recurrent;
   int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections,
                // 8 no edge-feature loads, 16 SiLU -> clamp, 32 skip the per-edge fp16 MFMAs
@@ -988,6 +991,13 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
       }
+      if (rvalid && p.m_out) {
+        f4 mt4[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[mt] * NEG_LN2;    // sM holds -log2e * sum m
+        store_ecl(p.m_out + (size_t)r * HID, mt4, g);
+        if (g == 0) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
+      }
       if (rvalid) {
         store_ecl(hO + (size_t)r * HID, hn, g);
         if (g == 0) {
@@ -1255,7 +1265,7 @@ template <int VARIANT>
 int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const float* x,
                  const float* v, const float* ef, const float* blob, float dt, float cw, int recurrent,
                  float* h_out, float* x_out, float* v_out, hipStream_t stream, int steps = 1,
-                 float* const* pp = nullptr) {
+                 float* const* pp = nullptr, float* m_out = nullptr, float* f_out = nullptr) {
   const int n_total = n_graphs * N;
   const int cus = num_cus();
   const int G = n_graphs < cus ? n_graphs : cus;
@@ -1271,6 +1281,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   a.n_total = n_total; a.n_graphs = n_graphs; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.ct = ct;
   if (steps < 1 || (steps > 1 && !pp)) return fail(NONODE_EINVAL, "layer: steps=%d", steps);
   a.steps = steps;
+  a.m_out = m_out; a.f_out = f_out;
   for (int i = 0; i < 2; ++i) {
     a.pp_h[i] = pp ? pp[i] : nullptr;
     a.pp_x[i] = pp ? pp[2 + i] : nullptr;
@@ -1537,3 +1548,5 @@ int nonode_debug_stamps(unsigned long long* out16) {
 
 }  // extern "C"
 
+// training path (forward with saved state + backward), same translation unit
+#include "nonode_train.hip"

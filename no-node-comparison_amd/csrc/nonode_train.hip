@@ -1,0 +1,967 @@
+// EGNO training path on gfx950: forward with saved states + hand-written backward.
+//
+// Replaces loss.backward() of run_epoch (main_simulation_simple_no.py:267-280) through
+// EGNO.forward (egno.py:37-111). The reverse pass follows oracle/egno_grad.py op by op, which is
+// pinned to the reference's own autograd gradients (tests/golden/egno_grad.npz).
+//
+// Included at the end of nonode.hip (same translation unit: shares the ECL helpers, the MFMA
+// fragment layout and the launch utilities).
+//
+// Per layer l (reverse order), given the gradients of that layer's outputs (gx, gv, gh):
+//   node_bwd_kernel   x/v update + node MLP reverse (basic.py:174-185): gF, gM, gv, part of gh
+//   edge_bwd_kernel   per-edge recompute + reverse of the coordinate and edge MLPs (basic.py:
+//                     170-173, 107-144): per-receiver / per-sender sums GA, GB and gx terms
+//   node_post_kernel  gh = part + W_A^T GA + W_B^T GB,  gx = gx + edge terms
+//   tconvx_bwd / tconv_bwd  TimeConv_x / TimeConv reverse (layer_no.py:80-178)
+// Weight gradients are GEMMs over edges or nodes, C = sum_k G[k] (x) A[k]: the kernels above write
+// the per-row operands, gemm_tn_partial sums K-slices per workgroup and gemm_reduce adds the
+// partials in a fixed order (deterministic).
+//
+// Stage 1 of the training path: exact f32 MFMAs (16x16x4) for every matrix product.
+
+namespace {
+
+// ---- backward weight blob (unscaled f32 fragments, forward and transposed) --------------------
+enum : int {
+  BOFF_WA = 0,          // edge W1 h_i columns                 (frag layout, KT=4)
+  BOFF_WB = 4096,       // edge W1 h_j columns
+  BOFF_W2 = 8192,       // edge W2
+  BOFF_WC1 = 12288,     // coord W1
+  BOFF_WV1 = 16384,     // node_v W1
+  BOFF_WN1 = 20480,     // node W1 [64][128]                   (KT=8)
+  BOFF_WN2 = 28672,     // node W2
+  BOFF_W2T = 32768,     // W2^T
+  BOFF_WC1T = 36864,    // Wc1^T
+  BOFF_WV1T = 40960,    // WV1^T
+  BOFF_WN2T = 45056,    // WN2^T
+  BOFF_WN1TH = 49152,   // (WN1[:, 0:64])^T    (h columns)
+  BOFF_WN1TM = 53248,   // (WN1[:, 64:128])^T  (message-sum columns)
+  BOFF_WAT = 57344,     // W_A^T
+  BOFF_WBT = 61440,     // W_B^T
+  BOFF_FEAT = 65536,    // scalar-input columns [s, e...] as k-steps (as OFF_FEAT, unscaled)
+  BOFF_VEC = 66048,     // vectors (vp order), BV_* below
+};
+enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
+constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2
+constexpr int BBLOB_FLOATS = BOFF_SCAL + 64;
+
+// frag of W^T: value W^T[row][col] = W[col][row0 + row] (W row stride ld)
+__device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, int row0, int d) {
+  const int q = d & 3, l = (d >> 2) & 63, rest = d >> 8;
+  const int mt = rest & 3, mo = rest >> 2;
+  const int row = 16 * mo + (l & 15), col = 16 * mt + 4 * (l >> 4) + q;
+  dst[d] = W[col * ld + row0 + row];
+}
+
+__global__ void pack_bwd_kernel(PackArgs a) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
+  float* B = a.blob;
+  switch (blockIdx.y) {
+    case 0: if (d < 4096) pack_frag(B + BOFF_WA, a.w1, a.ld1, a.colA, 4, d, 1.f); break;
+    case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
+    case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
+    case 3: if (d < 4096) pack_frag(B + BOFF_WC1, a.cw1, 64, 0, 4, d, 1.f); break;
+    case 4: if (d < 4096) pack_frag(B + BOFF_WV1, a.vw1, 64, 0, 4, d, 1.f); break;
+    case 5: pack_frag(B + BOFF_WN1, a.nw1, 128, 0, 8, d, 1.f); break;
+    case 6: if (d < 4096) pack_frag(B + BOFF_WN2, a.nw2, 64, 0, 4, d, 1.f); break;
+    case 7: if (d < 4096) pack_frag_t(B + BOFF_W2T, a.w2, 64, 0, d); break;
+    case 8: if (d < 4096) pack_frag_t(B + BOFF_WC1T, a.cw1, 64, 0, d); break;
+    case 9: if (d < 4096) pack_frag_t(B + BOFF_WV1T, a.vw1, 64, 0, d); break;
+    case 10: if (d < 4096) pack_frag_t(B + BOFF_WN2T, a.nw2, 64, 0, d); break;
+    case 11: if (d < 4096) pack_frag_t(B + BOFF_WN1TH, a.nw1, 128, 0, d); break;
+    case 12: if (d < 4096) pack_frag_t(B + BOFF_WN1TM, a.nw1, 128, HID, d); break;
+    case 13: if (d < 4096) pack_frag_t(B + BOFF_WAT, a.w1, a.ld1, a.colA, d); break;
+    case 14: if (d < 4096) pack_frag_t(B + BOFF_WBT, a.w1, a.ld1, a.colB, d); break;
+    case 15:
+      if (d < 512) {
+        const int kf = d >> 8, l = (d >> 2) & 63, mo = d & 3;
+        const int row = 16 * mo + (l & 15), fi = 4 * kf + (l >> 4);
+        float val = 0.f;
+        if (fi == 0) val = a.w1[row * a.ld1 + a.colS];
+        else if (fi - 1 < a.ne) val = a.w1[row * a.ld1 + 2 * HID + 1 + (fi - 1)];
+        B[BOFF_FEAT + d] = val;
+      } else if (d < 512 + BV_COUNT * 64) {
+        const int dd = d - 512, v = dd >> 6, i = dd & 63;
+        float val = 0.f;
+        switch (v) {
+          case BV_B1: val = vp_src(a.b1, 1, i); break;
+          case BV_B2: val = vp_src(a.b2, 1, i); break;
+          case BV_BC1: val = vp_src(a.cb1, 1, i); break;
+          case BV_WC2: val = vp_src(a.cw2, 1, i); break;
+          case BV_BV1: val = vp_src(a.vb1, 1, i); break;
+          case BV_WV2: val = vp_src(a.vw2, 1, i); break;
+          case BV_BN1: val = vp_src(a.nb1, 1, i); break;
+          case BV_BN2: val = vp_src(a.nb2, 1, i); break;
+          case BV_WS: val = vp_src(a.w1 + a.colS, a.ld1, i); break;
+        }
+        B[BOFF_VEC + dd] = val;
+      } else if (d < 512 + BV_COUNT * 64 + 64) {
+        const int i = d - 512 - BV_COUNT * 64;
+        B[BOFF_SCAL + i] = (i == 0) ? a.cb2[0] : (i == 1 && a.vb2) ? a.vb2[0] : 0.f;
+      }
+      break;
+  }
+}
+
+// ---- true-scale SiLU and its derivative ---------------------------------------------------------
+__device__ __forceinline__ float sigm(float z) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z * NEG_LOG2E)); }
+__device__ __forceinline__ void silu_true(f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[mt][q] *= sigm(a[mt][q]);
+}
+// g *= silu'(z) = s (1 + z (1 - s))
+__device__ __forceinline__ void mul_dsilu(f4 (&gz)[4], const f4 (&z)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float s = sigm(z[mt][q]);
+      gz[mt][q] *= s * fmaf(z[mt][q], 1.f - s, 1.f);
+    }
+}
+__device__ __forceinline__ void zero4(f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) a[mt] = f4{0.f, 0.f, 0.f, 0.f};
+}
+
+// ---- training-forward helpers -----------------------------------------------------------------
+// h0[t*BN + c] = emb_w[:, :din] h_in[c] + etab[c % Bt][t]   (egno.py:63-76; same arithmetic as
+// tconv_kernel<true>), and x, v replicated over T (egno.py:89-96)
+__global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, const float* emb_w, int emb_ld,
+                          const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= BN * 64) return;
+  const int o = idx & 63, c = idx >> 6;
+  float base = 0.f;
+  for (int k = 0; k < din; ++k) base = fmaf(emb_w[o * emb_ld + k], hin[(size_t)c * din + k], base);
+  const float* et = etab + (size_t)(c % Bt) * T * 64;
+  for (int t = 0; t < T; ++t) {
+    const size_t row = (size_t)t * BN + c;
+    h0[row * 64 + o] = et[t * 64 + o] + base;
+    if (o < 3) { xr[row * 3 + o] = x[(size_t)c * 3 + o]; vr[row * 3 + o] = v[(size_t)c * 3 + o]; }
+  }
+}
+
+// emb_in[t*BN + c] = [h_in[c], temb(t_out[c % Bt][t])]  (the embedding Linear's input rows)
+__global__ void emb_in_kernel(int BN, int T, int din, int dim, int Bt, const float* hin, const float* t_out,
+                              float* emb_in) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int w = din + dim;
+  if (idx >= BN * T * w) return;
+  const int k = idx % w, row = idx / w;
+  const int t = row / BN, c = row - t * BN;
+  float val;
+  if (k < din) {
+    val = hin[(size_t)c * din + k];
+  } else {
+    const int kk = k - din, half = dim / 2;
+    const float scale = (float)(log(10000.0) / (double)(half - 1));
+    const float tv = t_out[(size_t)(c % Bt) * T + t];
+    const int j = kk < half ? kk : kk - half;
+    const float arg = tv * expf((float)j * -scale);
+    val = kk < half ? sinf(arg) : cosf(arg);
+  }
+  emb_in[idx] = val;
+}
+
+// ---- node backward (basic.py:174-185 reversed) ---------------------------------------------------
+struct NodeBwdArgs {
+  int n, N;
+  const float* h; const float* v; const float* M; const float* F;   // layer inputs + saved sums
+  const float* gxo; const float* gvo; const float* gho;              // grads of the layer outputs
+  const float* bb;                                                   // backward blob
+  float* gv; float* gF; float* gM; float* ghp;                       // outputs
+  float* op_gt; float* op_t; float* op_gphi; float* op_z; float* op_gz;   // GEMM operands
+};
+
+__global__ __launch_bounds__(256) void node_bwd_kernel(NodeBwdArgs p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x * 4 + wave;
+  const int r0 = tile * 16;
+  if (r0 >= p.n) return;
+  const int r = min(r0 + e, p.n - 1);
+  const bool valid = r0 + e < p.n;
+  const float* bb = p.bb;
+  f4 hr[4], Mr[4];
+  load_ecl(hr, p.h + (size_t)r * HID, g);
+  load_ecl(Mr, p.M + (size_t)r * HID, g);
+  // phi_v(h) = wv2 . SiLU(WV1 h + bv1) + bv2
+  f4 tp[4];
+  load_vp(tp, bb + BOFF_VEC + BV_BV1 * 64, g);
+  mfma_dense<4>(tp, bb + BOFF_WV1, hr, lane);
+  f4 t[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) t[mt] = tp[mt];
+  silu_true(t);
+  const float phi = dot_vp(t, bb + BOFF_VEC + BV_WV2 * 64, g) + bb[BOFF_SCAL + 1];
+  const float gx0 = p.gxo[(size_t)r * 3 + 0], gx1 = p.gxo[(size_t)r * 3 + 1], gx2 = p.gxo[(size_t)r * 3 + 2];
+  const float v0 = p.v[(size_t)r * 3 + 0], v1 = p.v[(size_t)r * 3 + 1], v2 = p.v[(size_t)r * 3 + 2];
+  const float gphi = gx0 * v0 + gx1 * v1 + gx2 * v2;
+  // clamp(F / (N-1), +-100) passes the gradient inside [-100, 100]
+  const float inv = 1.f / (float)(p.N - 1);
+  const float F0 = p.F[(size_t)r * 4 + 0] * inv, F1 = p.F[(size_t)r * 4 + 1] * inv, F2 = p.F[(size_t)r * 4 + 2] * inv;
+  const float gF0 = (F0 >= -100.f && F0 <= 100.f) ? gx0 * inv : 0.f;
+  const float gF1 = (F1 >= -100.f && F1 <= 100.f) ? gx1 * inv : 0.f;
+  const float gF2 = (F2 >= -100.f && F2 <= 100.f) ? gx2 * inv : 0.f;
+  // gt_pre = gphi * wv2 (.) silu'(tp);  gh = WV1^T gt_pre
+  f4 gt[4];
+  load_vp(gt, bb + BOFF_VEC + BV_WV2 * 64, g);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) gt[mt] *= gphi;
+  mul_dsilu(gt, tp);
+  f4 gh[4];
+  zero4(gh);
+  mfma_dense<4>(gh, bb + BOFF_WV1T, gt, lane);
+  // node MLP: z = SiLU(WN1 [h, M] + bn1), h' = WN2 z + bn2
+  f4 in8[8];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
+  f4 zp[4];
+  load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
+  mfma_dense<8>(zp, bb + BOFF_WN1, in8, lane);
+  f4 z[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
+  silu_true(z);
+  f4 gho[4], gz[4];
+  load_ecl(gho, p.gho + (size_t)r * HID, g);
+  zero4(gz);
+  mfma_dense<4>(gz, bb + BOFF_WN2T, gho, lane);
+  mul_dsilu(gz, zp);
+  mfma_dense<4>(gh, bb + BOFF_WN1TH, gz, lane);
+  f4 gM[4];
+  zero4(gM);
+  mfma_dense<4>(gM, bb + BOFF_WN1TM, gz, lane);
+  if (valid) {
+    const size_t o = (size_t)r * HID;
+    store_ecl(p.ghp + o, gh, g);
+    store_ecl(p.gM + o, gM, g);
+    store_ecl(p.op_gt + o, gt, g);
+    store_ecl(p.op_t + o, t, g);
+    store_ecl(p.op_z + o, z, g);
+    store_ecl(p.op_gz + o, gz, g);
+    if (g == 0) {
+      p.gv[(size_t)r * 3 + 0] = p.gvo[(size_t)r * 3 + 0] + phi * gx0;
+      p.gv[(size_t)r * 3 + 1] = p.gvo[(size_t)r * 3 + 1] + phi * gx1;
+      p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
+      *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
+      p.op_gphi[r] = gphi;
+    }
+  }
+}
+
+// ---- edge backward (basic.py:107-144, 167-173 reversed) ----------------------------------------
+constexpr int ESC = 8;   // per-edge scalar row: [gc, s, e_0 .. e_{ne-1}, 0 ...]
+struct EdgeBwdArgs {
+  int n_graphs, N, ne, ef_mod, ct, s_max;
+  const float* h; const float* x; const float* ef; const float* bb;
+  const float* gF; const float* gM;
+  float* GA; float* GB; float* GX;                                    // per node (GB, GX atomically)
+  float* e_gz1; float* e_gz2; float* e_gz3; float* e_a; float* e_m; float* e_c1; float* e_sc;
+};
+
+size_t edge_bwd_lds_floats(int ct, int N, int* s_max_out) {
+  const int s_max = ((16 * ct - 1) / N + 2) * N;
+  if (s_max_out) *s_max_out = s_max;
+  // sP, sGM, sGA [ct*16][ROWP]; sQ, sGB [s_max][ROWP]; sX, sGX [s_max][4]; sGF [ct*16][4]
+  return (size_t)ct * 16 * ROWP * 3 + (size_t)s_max * ROWP * 2 + (size_t)s_max * 8 + (size_t)ct * 16 * 4;
+}
+
+__global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int NW = 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
+  const int N = p.N, Nm1 = N - 1;
+  float* sP = smem;
+  float* sGM = sP + p.ct * 16 * ROWP;
+  float* sGA = sGM + p.ct * 16 * ROWP;
+  float* sQ = sGA + p.ct * 16 * ROWP;
+  float* sGB = sQ + p.s_max * ROWP;
+  float* sX = sGB + p.s_max * ROWP;
+  float* sGX = sX + p.s_max * 4;
+  float* sGF = sGX + p.s_max * 4;
+  const float* bb = p.bb;
+  const float bc2 = bb[BOFF_SCAL + 0];
+  const int G = gridDim.x;
+  const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;
+  const int nend = (int)(((long long)(blockIdx.x + 1) * p.n_graphs) / G) * N;
+  const int ntw = (nend - nb + 15) >> 4;
+  const int nch = (ntw + p.ct - 1) / p.ct;
+  for (int ci = 0; ci < nch; ++ci) {
+    const int c0 = (ci * ntw) / nch;
+    const int ctc = ((ci + 1) * ntw) / nch - c0;
+    const int rbase = nb + c0 * 16;
+    const int r_last = min(rbase + ctc * 16, nend) - 1;
+    const int g_lo = rbase / N, g_hi = r_last / N;
+    const int s0 = g_lo * N;
+    const int S = (g_hi - g_lo + 1) * N;
+    const int nsT = (S + 15) >> 4;
+    // ---- A: tables ----
+    for (int i = tid; i < ctc * 16 * ROWP; i += NW * 64) sGA[i] = 0.f;
+    for (int i = tid; i < S * ROWP; i += NW * 64) sGB[i] = 0.f;
+    for (int i = tid; i < S * 4; i += NW * 64) sGX[i] = 0.f;
+    for (int i = tid; i < S * 3; i += NW * 64) {
+      const int s = i / 3, d = i - 3 * s;
+      sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
+    }
+    for (int i = tid; i < ctc * 16 * 4; i += NW * 64) {
+      const int rr = rbase + i / 4;
+      sGF[i] = rr < nend ? p.gF[(size_t)rr * 4 + (i & 3)] : 0.f;
+    }
+    for (int job = wave; job < ctc + nsT; job += NW) {
+      const bool isP = job < ctc;
+      const int local = (isP ? job : job - ctc) * 16 + e;
+      int node = isP ? rbase + local : s0 + local;
+      const bool valid = isP ? (node < nend) : (local < S);
+      node = valid ? node : (isP ? nend - 1 : s0);
+      f4 hin[4], acc[4];
+      load_ecl(hin, p.h + (size_t)node * HID, g);
+      if (isP) load_vp(acc, bb + BOFF_VEC + BV_B1 * 64, g);
+      else zero4(acc);
+      mfma_dense<4>(acc, bb + (isP ? BOFF_WA : BOFF_WB), hin, lane);
+      if (valid) {
+        store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
+        if (isP) {
+          f4 gm[4];
+          load_ecl(gm, p.gM + (size_t)node * HID, g);
+          store_ecl(sGM + local * ROWP, gm, g);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- B: one unit (16 edges: receivers of a tile x sender offset k) at a time ----
+    const int U = ctc * Nm1;
+    for (int u = wave; u < U; u += NW) {
+      const int tau = u / Nm1, k = u - tau * Nm1 + 1;
+      const int rl = 16 * tau + e;
+      const int r = rbase + rl;
+      const bool rvalid = r < nend;
+      const int rc = rvalid ? r : nend - 1;
+      const int gr = rc / N, n = rc - gr * N;
+      int j = n + k;
+      j = (j >= N) ? j - N : j;
+      const int jj = (j < n) ? j : j - 1;
+      const int sb = gr * N - s0;
+      const int sl = sb + j, rls = sb + n;
+      const float r0 = sX[rls * 4 + 0] - sX[sl * 4 + 0];
+      const float r1 = sX[rls * 4 + 1] - sX[sl * 4 + 1];
+      const float r2 = sX[rls * 4 + 2] - sX[sl * 4 + 2];
+      const float s2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+      const size_t eidx = (size_t)rc * Nm1 + jj;
+      const float* efp = p.ef + (((size_t)(gr % p.ef_mod) * N + n) * Nm1 + jj) * p.ne;
+      float ev[2];
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf) {
+        const int fi = 4 * kf + g;
+        ev[kf] = fi == 0 ? s2 : (fi - 1 < p.ne ? efp[fi - 1] : 0.f);
+      }
+      // forward recompute: z1 = P_r + Q_s + W1[:, s|e] [s, e];  a = SiLU(z1)
+      f4 z1[4], q4[4];
+      load_ecl(z1, sP + rl * ROWP, g);
+      load_ecl(q4, sQ + sl * ROWP, g);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) z1[mt] += q4[mt];
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf) {
+        if (kf * 4 < 1 + p.ne) {
+          const f4 wf = *reinterpret_cast<const f4*>(bb + BOFF_FEAT + kf * 256 + lane * 4);
+#pragma unroll
+          for (int mo = 0; mo < 4; ++mo) z1[mo] = mfma(wf[mo], ev[kf], z1[mo]);
+        }
+      }
+      f4 a[4], z2[4], m[4], z3[4], c1[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt];
+      silu_true(a);
+      load_vp(z2, bb + BOFF_VEC + BV_B2 * 64, g);
+      mfma_dense<4>(z2, bb + BOFF_W2, a, lane);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt];
+      silu_true(m);
+      load_vp(z3, bb + BOFF_VEC + BV_BC1 * 64, g);
+      mfma_dense<4>(z3, bb + BOFF_WC1, m, lane);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) c1[mt] = z3[mt];
+      silu_true(c1);
+      const float c = dot_vp(c1, bb + BOFF_VEC + BV_WC2 * 64, g) + bc2;
+      // reverse: f = r c
+      const float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
+      const float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
+      float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
+      // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
+      f4 gz3[4];
+      load_vp(gz3, bb + BOFF_VEC + BV_WC2 * 64, g);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) gz3[mt] *= gc;
+      mul_dsilu(gz3, z3);
+      // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m)
+      f4 gz2[4];
+      load_ecl(gz2, sGM + rl * ROWP, g);
+      if (!rvalid) zero4(gz2);
+      mfma_dense<4>(gz2, bb + BOFF_WC1T, gz3, lane);
+      mul_dsilu(gz2, z2);                       // m = SiLU(z2)
+      f4 gz1[4];
+      zero4(gz1);
+      mfma_dense<4>(gz1, bb + BOFF_W2T, gz2, lane);
+      mul_dsilu(gz1, z1);                       // a = SiLU(z1)
+      // s = |r|^2 input column
+      const float gs = dot_vp(gz1, bb + BOFF_VEC + BV_WS * 64, g);
+      gr0 = fmaf(2.f * gs, r0, gr0);
+      gr1 = fmaf(2.f * gs, r1, gr1);
+      gr2 = fmaf(2.f * gs, r2, gr2);
+      if (rvalid) {
+        // per-receiver / per-sender sums of gz1 (the W_A h_i and W_B h_j inputs) and x terms
+        float* ga = sGA + rl * ROWP + 4 * g;
+        float* gb = sGB + sl * ROWP + 4 * g;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            atomicAdd(ga + 16 * mt + q, gz1[mt][q]);
+            atomicAdd(gb + 16 * mt + q, gz1[mt][q]);
+          }
+        if (g == 0) {
+          atomicAdd(sGX + rls * 4 + 0, gr0); atomicAdd(sGX + rls * 4 + 1, gr1); atomicAdd(sGX + rls * 4 + 2, gr2);
+          atomicAdd(sGX + sl * 4 + 0, -gr0); atomicAdd(sGX + sl * 4 + 1, -gr1); atomicAdd(sGX + sl * 4 + 2, -gr2);
+        }
+        // GEMM operands of this edge (row eidx, the reference edge order)
+        const size_t o = eidx * HID;
+        store_ecl(p.e_gz1 + o, gz1, g);
+        store_ecl(p.e_gz2 + o, gz2, g);
+        store_ecl(p.e_gz3 + o, gz3, g);
+        store_ecl(p.e_a + o, a, g);
+        store_ecl(p.e_m + o, m, g);
+        store_ecl(p.e_c1 + o, c1, g);
+        if (g == 0) {
+          float* sc = p.e_sc + eidx * ESC;
+          sc[0] = gc; sc[1] = s2;
+          for (int kk = 0; kk < p.ne; ++kk) sc[2 + kk] = efp[kk];
+        }
+      }
+    }
+    __syncthreads();
+    // ---- C: write the chunk's sums (senders can be shared with the next chunk: atomics) ----
+    for (int i = tid; i < ctc * 16 * HID; i += NW * 64) {
+      const int rl = i / HID, ch = i - rl * HID;
+      const int r = rbase + rl;
+      if (r < nend) p.GA[(size_t)r * HID + ch] = sGA[rl * ROWP + ch];
+    }
+    for (int i = tid; i < S * HID; i += NW * 64) {
+      const int sl = i / HID, ch = i - sl * HID;
+      atomicAdd(p.GB + (size_t)(s0 + sl) * HID + ch, sGB[sl * ROWP + ch]);
+    }
+    for (int i = tid; i < S * 3; i += NW * 64) {
+      const int sl = i / 3, d = i - 3 * sl;
+      atomicAdd(p.GX + (size_t)(s0 + sl) * 4 + d, sGX[sl * 4 + d]);
+    }
+    __syncthreads();
+  }
+}
+
+// gh = ghp + W_A^T GA + W_B^T GB ;  gx = gxo + GX
+__global__ __launch_bounds__(256) void node_post_kernel(int n, const float* ghp, const float* GA, const float* GB,
+                                                        const float* gxo, const float* GX, const float* bb,
+                                                        float* gh, float* gx) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
+  const int r0 = (blockIdx.x * 4 + wave) * 16;
+  if (r0 >= n) return;
+  const int r = min(r0 + e, n - 1);
+  f4 acc[4], ga[4], gb[4];
+  load_ecl(acc, ghp + (size_t)r * HID, g);
+  load_ecl(ga, GA + (size_t)r * HID, g);
+  load_ecl(gb, GB + (size_t)r * HID, g);
+  mfma_dense<4>(acc, bb + BOFF_WAT, ga, lane);
+  mfma_dense<4>(acc, bb + BOFF_WBT, gb, lane);
+  if (r0 + e < n) {
+    store_ecl(gh + (size_t)r * HID, acc, g);
+    if (g < 3) gx[(size_t)r * 3 + g] = gxo[(size_t)r * 3 + g] + GX[(size_t)r * 4 + g];
+  }
+}
+
+// ---- TimeConv / TimeConv_x reverse (layer_no.py:80-178; oracle/egno_grad.py spectral_bwd) ------
+// One 64-thread block per column c (channel = thread). Recomputes X = DFT_T(h), Y = X W,
+// y = sum_m (c_m/T)(Yr cos - Yi sin), gy = gout * leaky'(y); then
+// gY_r = sum_t (c_m/T) cos gy, gY_i = -sum_t (c_m/T) sin gy, gX = gY W^T (complex),
+// gh = gout + sum_m (gXr cos - gXi sin). Writes Xr, Xi, gYr, gYi [m][BN][64] for the weight GEMMs.
+__global__ __launch_bounds__(64) void tconv_bwd_kernel(int BN, int T, int M, int Mfull, const float* h, const float* gout,
+                                                       const float* w, float* gh, float* Xr_o, float* Xi_o,
+                                                       float* gYr_o, float* gYi_o) {
+  __shared__ float sXr[MMAX][64], sXi[MMAX][64], sGr[MMAX][64], sGi[MMAX][64];
+  __shared__ float sCos[MMAX][TMAX], sSin[MMAX][TMAX];
+  const int c = blockIdx.x, ch = threadIdx.x;
+  if (ch < M * T) {
+    const int m = ch / T, t = ch % T;
+    const double ang = 2.0 * (double)m * (double)t / (double)T;
+    sCos[m][t] = (float)cospi(ang);
+    sSin[m][t] = (float)sinpi(ang);
+  }
+  __syncthreads();
+  float hv[TMAX], gv[TMAX];
+  for (int t = 0; t < T; ++t) {
+    hv[t] = h[((size_t)t * BN + c) * 64 + ch];
+    gv[t] = gout[((size_t)t * BN + c) * 64 + ch];
+  }
+  for (int m = 0; m < M; ++m) {
+    float xr = 0.f, xi = 0.f;
+    for (int t = 0; t < T; ++t) { xr = fmaf(hv[t], sCos[m][t], xr); xi = fmaf(-hv[t], sSin[m][t], xi); }
+    sXr[m][ch] = xr; sXi[m][ch] = xi;
+  }
+  __syncthreads();
+  // thread = output channel o: Y_m[o] = sum_i X_m[i] W[i][o][m]
+  float y[TMAX];
+  for (int t = 0; t < T; ++t) y[t] = 0.f;
+  for (int m = 0; m < M; ++m) {
+    float yr = 0.f, yi = 0.f;
+    for (int i = 0; i < 64; ++i) {
+      const float wr = w[(((size_t)i * 64 + ch) * Mfull + m) * 2 + 0], wi = w[(((size_t)i * 64 + ch) * Mfull + m) * 2 + 1];
+      yr = fmaf(sXr[m][i], wr, fmaf(-sXi[m][i], wi, yr));
+      yi = fmaf(sXr[m][i], wi, fmaf(sXi[m][i], wr, yi));
+    }
+    const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
+    for (int t = 0; t < T; ++t) y[t] += cm * (yr * sCos[m][t] - yi * sSin[m][t]);
+  }
+  for (int t = 0; t < T; ++t) y[t] = gv[t] * (y[t] > 0.f ? 1.f : 0.01f);   // gy
+  for (int m = 0; m < M; ++m) {
+    const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
+    float gr = 0.f, gi = 0.f;
+    for (int t = 0; t < T; ++t) { gr = fmaf(cm * sCos[m][t], y[t], gr); gi = fmaf(-cm * sSin[m][t], y[t], gi); }
+    sGr[m][ch] = gr; sGi[m][ch] = gi;
+  }
+  __syncthreads();
+  // thread = input channel i: gX_m[i] = sum_o gY_m[o] conj-mix
+  for (int t = 0; t < T; ++t) hv[t] = gv[t];
+  for (int m = 0; m < M; ++m) {
+    float gxr = 0.f, gxi = 0.f;
+    for (int o = 0; o < 64; ++o) {
+      const float wr = w[(((size_t)ch * 64 + o) * Mfull + m) * 2 + 0], wi = w[(((size_t)ch * 64 + o) * Mfull + m) * 2 + 1];
+      gxr = fmaf(sGr[m][o], wr, fmaf(sGi[m][o], wi, gxr));
+      gxi = fmaf(-sGr[m][o], wi, fmaf(sGi[m][o], wr, gxi));
+    }
+    for (int t = 0; t < T; ++t) hv[t] += gxr * sCos[m][t] - gxi * sSin[m][t];
+    const size_t o = ((size_t)m * BN + c) * 64 + ch;
+    Xr_o[o] = sXr[m][ch]; Xi_o[o] = sXi[m][ch]; gYr_o[o] = sGr[m][ch]; gYi_o[o] = sGi[m][ch];
+  }
+  for (int t = 0; t < T; ++t) gh[((size_t)t * BN + c) * 64 + ch] = hv[t];
+}
+
+// TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. One thread per (c, d).
+// Writes gx, gv and per-thread weight-gradient terms part[(c*3+d)][i][o][m][2].
+__global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x, const float* v, const float* lm,
+                                  const float* gxo, const float* gvo, const float* w, float* gx, float* gv,
+                                  float* part) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= BN * 3) return;
+  const int c = idx / 3, d = idx - 3 * c;
+  float X[2][TMAX], G[2][TMAX], GO[2][TMAX];
+  const float lmv = lm[(size_t)c * 3 + d];
+  for (int t = 0; t < T; ++t) {
+    const size_t row = (size_t)t * BN + c;
+    X[0][t] = x[row * 3 + d] - lmv;
+    X[1][t] = v[row * 3 + d];
+    GO[0][t] = G[0][t] = gxo[row * 3 + d];
+    GO[1][t] = G[1][t] = gvo[row * 3 + d];
+  }
+  float* pp = part + (size_t)idx * (2 * 2 * MMAX * 2);
+  for (int k = 0; k < 2 * 2 * MMAX * 2; ++k) pp[k] = 0.f;
+  for (int m = 0; m < M; ++m) {
+    const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
+    float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f}, gYr[2] = {0.f, 0.f}, gYi[2] = {0.f, 0.f};
+    for (int t = 0; t < T; ++t) {
+      const double ang = 2.0 * (double)m * (double)t / (double)T;
+      const float cs = (float)cospi(ang), sn = (float)sinpi(ang);
+      for (int i = 0; i < 2; ++i) {
+        Xr[i] = fmaf(X[i][t], cs, Xr[i]); Xi[i] = fmaf(-X[i][t], sn, Xi[i]);
+        gYr[i] = fmaf(cm * cs, GO[i][t], gYr[i]); gYi[i] = fmaf(-cm * sn, GO[i][t], gYi[i]);
+      }
+    }
+    for (int i = 0; i < 2; ++i) {
+      float gxr = 0.f, gxi = 0.f;
+      for (int o = 0; o < 2; ++o) {
+        const float wr = w[((i * 2 + o) * Mfull + m) * 2 + 0], wi = w[((i * 2 + o) * Mfull + m) * 2 + 1];
+        gxr += gYr[o] * wr + gYi[o] * wi;
+        gxi += -gYr[o] * wi + gYi[o] * wr;
+        pp[((i * 2 + o) * MMAX + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
+        pp[((i * 2 + o) * MMAX + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
+      }
+      for (int t = 0; t < T; ++t) {
+        const double ang = 2.0 * (double)m * (double)t / (double)T;
+        G[i][t] += gxr * (float)cospi(ang) - gxi * (float)sinpi(ang);
+      }
+    }
+  }
+  for (int t = 0; t < T; ++t) {
+    const size_t row = (size_t)t * BN + c;
+    gx[row * 3 + d] = G[0][t];
+    gv[row * 3 + d] = G[1][t];
+  }
+}
+
+// ---- weight-gradient GEMMs ---------------------------------------------------------------------
+// partial[blk][i][j] = sum over rows k of this block's K-slice of G[k*ldg + i] * A[k*lda + j]
+// (j < N; j == N is the ones column: the bias gradient sum_k G[k][i]). M <= 64, N <= 64.
+constexpr int GEMM_KROWS = 64;
+__global__ __launch_bounds__(256) void gemm_tn_partial(const float* G, int ldg, int M, const float* A, int lda,
+                                                       int N, long long K, long long kslice, float* partial) {
+  __shared__ float sG[GEMM_KROWS][64], sA[GEMM_KROWS][65];
+  const int tid = threadIdx.x;
+  const long long k0 = (long long)blockIdx.x * kslice;
+  const long long k1 = min(K, k0 + kslice);
+  const int NO = M * (N + 1);
+  float acc[17];
+  for (int q = 0; q < 17; ++q) acc[q] = 0.f;
+  for (long long kb = k0; kb < k1; kb += GEMM_KROWS) {
+    const int rows = (int)min((long long)GEMM_KROWS, k1 - kb);
+    __syncthreads();
+    for (int i = tid; i < GEMM_KROWS * 64; i += 256) {
+      const int kr = i >> 6, col = i & 63;
+      sG[kr][col] = (kr < rows && col < M) ? G[(kb + kr) * ldg + col] : 0.f;
+      sA[kr][col] = (kr < rows && col < N) ? A[(kb + kr) * lda + col] : 0.f;
+    }
+    if (tid < GEMM_KROWS) sA[tid][64] = tid < rows ? 1.f : 0.f;
+    __syncthreads();
+    for (int q = 0; q < 17; ++q) {
+      const int o = tid + q * 256;
+      if (o < NO) {
+        const int i = o / (N + 1), j = o - i * (N + 1);
+        const int jj = j == N ? 64 : j;
+        float s = acc[q];
+        for (int kr = 0; kr < GEMM_KROWS; ++kr) s = fmaf(sG[kr][i], sA[kr][jj], s);
+        acc[q] = s;
+      }
+    }
+  }
+  for (int q = 0; q < 17; ++q) {
+    const int o = tid + q * 256;
+    if (o < NO) partial[(size_t)blockIdx.x * NO + o] = acc[q];
+  }
+}
+
+// dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
+// partial[b][i][N]; partials added in a fixed order (deterministic)
+__global__ void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld, int col0, int cs,
+                            float* bias, int accumulate, float scale) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  const int NO = M * (N + 1);
+  if (o >= NO) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partial[(size_t)b * NO + o];
+  s *= scale;
+  const int i = o / (N + 1), j = o - i * (N + 1);
+  if (j < N) {
+    if (dst) { float* p = dst + (size_t)i * ld + (size_t)(col0 + j) * cs; *p = accumulate ? *p + s : s; }
+  } else if (bias) {
+    bias[i] = accumulate ? bias[i] + s : s;
+  }
+}
+
+// sum over rows of part[rows][cnt] -> dst[cnt] (fixed order)
+__global__ void rows_reduce(const float* part, long long rows, int cnt, float* dst) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= cnt) return;
+  double s = 0.0;
+  for (long long r = 0; r < rows; ++r) s += part[r * cnt + o];
+  dst[o] = (float)s;
+}
+
+struct Gemm {
+  float* partial;
+  int max_blk;
+  hipStream_t s;
+  // C[M][N] = sum_k G[k] (x) A[k] into dst (row stride ld, column offset col0) and bias
+  int operator()(const float* G, int ldg, int M, const float* A, int lda, int N, long long K, float* dst,
+                 int ld, int col0, float* bias, int accumulate = 0, int cs = 1, float scale = 1.f) const {
+    if (M > 64 || N > 64 || M * (N + 1) > 17 * 256) return fail(NONODE_EINVAL, "gemm: M=%d N=%d", M, N);
+    long long kslice = (K + max_blk - 1) / max_blk;
+    kslice = ((kslice + GEMM_KROWS - 1) / GEMM_KROWS) * GEMM_KROWS;
+    if (kslice < GEMM_KROWS) kslice = GEMM_KROWS;
+    const int nblk = (int)((K + kslice - 1) / kslice);
+    if (nblk < 1) return NONODE_OK;
+    hipLaunchKernelGGL(gemm_tn_partial, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice, partial);
+    if (int rc = check_launch("gemm_tn_partial")) return rc;
+    const int NO = M * (N + 1);
+    hipLaunchKernelGGL(gemm_reduce, dim3((NO + 255) / 256), dim3(256), 0, s, partial, nblk, M, N, dst, ld, col0,
+                       cs, bias, accumulate, scale);
+    return check_launch("gemm_reduce");
+  }
+};
+
+// ---- state layout of the training forward ---------------------------------------------------------
+struct TrainState {
+  float *hs, *xs, *vs;        // (L+1) x n x {64, 3, 3}: inputs of each layer's TimeConv (hs[0] = h0)
+  float *he, *xe, *ve;        // L x n x {64, 3, 3}: TimeConv outputs = EGNN inputs
+  float *Ms, *Fs;             // L x n x {64, 4}: message / force sums of each EGNN layer
+  float *emb_in;              // n x (in_node + temb): embedding Linear inputs
+  size_t floats;
+};
+TrainState train_state(void* base, int B, int N, int T, int L, int in_node, int temb) {
+  const size_t n = (size_t)B * N * T;
+  TrainState st;
+  float* p = (float*)base;
+  auto take = [&](size_t cnt) { float* q = p; if (p) p += cnt; return q; };
+  st.hs = take((L + 1) * n * 64); st.xs = take((L + 1) * n * 3); st.vs = take((L + 1) * n * 3);
+  st.he = take(L * n * 64); st.xe = take(L * n * 3); st.ve = take(L * n * 3);
+  st.Ms = take(L * n * 64); st.Fs = take(L * n * 4);
+  st.emb_in = take(n * (in_node + temb));
+  st.floats = (size_t)((L + 1) * n * 70 + L * n * 70 + L * n * 68 + n * (in_node + temb));
+  return st;
+}
+
+// backward workspace
+struct BwdWs {
+  float *gx[2], *gv[2], *gh[2];          // ping-pong grads of the current layer outputs (n rows)
+  float *gF, *gM, *ghp, *GA, *GB, *GX, *gxe, *gve, *ghe;
+  float *op_gt, *op_t, *op_gphi, *op_z, *op_gz;
+  float *e_gz1, *e_gz2, *e_gz3, *e_a, *e_m, *e_c1, *e_sc;
+  float *tXr, *tXi, *tgYr, *tgYi, *xpart;
+  float *partial;
+  size_t floats;
+};
+constexpr int GEMM_MAX_BLK = 1024;
+BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
+  const size_t BN = (size_t)B * N, n = BN * T, E = n * (N - 1);
+  BwdWs w;
+  float* p = (float*)base;
+  size_t tot = 0;
+  auto take = [&](size_t cnt) { float* q = p ? p + tot : nullptr; tot += (cnt + 63) & ~size_t(63); return q; };
+  for (int i = 0; i < 2; ++i) { w.gx[i] = take(n * 3); w.gv[i] = take(n * 3); w.gh[i] = take(n * 64); }
+  w.gF = take(n * 4); w.gM = take(n * 64); w.ghp = take(n * 64); w.GA = take(n * 64); w.GB = take(n * 64);
+  w.GX = take(n * 4); w.gxe = take(n * 3); w.gve = take(n * 3); w.ghe = take(n * 64);
+  w.op_gt = take(n * 64); w.op_t = take(n * 64); w.op_gphi = take(n); w.op_z = take(n * 64); w.op_gz = take(n * 64);
+  w.e_gz1 = take(E * 64); w.e_gz2 = take(E * 64); w.e_gz3 = take(E * 64);
+  w.e_a = take(E * 64); w.e_m = take(E * 64); w.e_c1 = take(E * 64); w.e_sc = take(E * ESC);
+  w.tXr = take(M * BN * 64); w.tXi = take(M * BN * 64); w.tgYr = take(M * BN * 64); w.tgYi = take(M * BN * 64);
+  w.xpart = take(BN * 3 * 2 * 2 * MMAX * 2);
+  w.partial = take((size_t)GEMM_MAX_BLK * 17 * 256);
+  w.floats = tot;
+  return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t nonode_bwd_blob_floats(void) { return BBLOB_FLOATS; }
+
+int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat, float* bblob,
+                          void* stream) {
+  if (!w || !bblob) return fail(NONODE_EINVAL, "pack_layer_bwd: null pointer");
+  if (hidden != HID || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "pack_layer_bwd: hidden=%d n_edge_feat=%d", hidden, n_edge_feat);
+  if (variant != NONODE_VARIANT_EGNO) return fail(NONODE_EUNSUPPORTED, "pack_layer_bwd: EGNO only");
+  if (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2)
+    return fail(NONODE_EINVAL, "pack_layer_bwd: EGNO needs node_v_net weights");
+  PackArgs a;
+  a.ld1 = 2 * HID + 1 + n_edge_feat;
+  a.colS = 0; a.colA = 1; a.colB = 1 + HID;
+  a.w1 = w->edge_w1; a.b1 = w->edge_b1; a.w2 = w->edge_w2; a.b2 = w->edge_b2;
+  a.cw1 = w->coord_w1; a.cb1 = w->coord_b1; a.cw2 = w->coord_w2; a.cb2 = w->coord_b2;
+  a.vw1 = w->vel_w1; a.vb1 = w->vel_b1; a.vw2 = w->vel_w2; a.vb2 = w->vel_b2;
+  a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
+  a.ne = n_edge_feat;
+  a.blob = bblob;
+  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 16), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("pack_bwd_kernel");
+}
+
+size_t nonode_egno_train_state_bytes(int B, int N, int T, int n_layers, int in_node, int time_emb_dim) {
+  return train_state(nullptr, B, N, T, n_layers, in_node, time_emb_dim).floats * sizeof(float);
+}
+
+int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                              int modes, int Bt, const float* x, const float* h, const float* v,
+                              const float* loc_mean, const float* edge_fea, const float* t_out,
+                              const float* emb_w, const float* emb_b, const float* const* blobs,
+                              const float* const* tconv_blobs, const float* const* tconvx_w, float* x_out,
+                              float* v_out, float* h_out, void* state, size_t state_bytes, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || in_node < 0 || in_node > 8 || modes < 1 ||
+      modes > MMAX || time_emb_dim < 4 || time_emb_dim > 64 || (time_emb_dim & 1) || Bt <= 0 || (B * N) % Bt)
+    return fail(NONODE_EUNSUPPORTED, "egno_forward_train: B=%d N=%d T=%d", B, N, T);
+  if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_blobs || !tconvx_w ||
+      !x_out || !v_out || !h_out || !state || !workspace)
+    return fail(NONODE_EINVAL, "egno_forward_train: null pointer");
+  if (state_bytes < nonode_egno_train_state_bytes(B, N, T, n_layers, in_node, time_emb_dim))
+    return fail(NONODE_EINVAL, "egno_forward_train: state too small");
+  if (workspace_bytes < nonode_egno_workspace_bytes(B, N, T, Bt))
+    return fail(NONODE_EINVAL, "egno_forward_train: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int BN = B * N;
+  const size_t n = (size_t)BN * T;
+  const int L = n_layers;
+  TrainState st = train_state(state, B, N, T, L, in_node, time_emb_dim);
+  float* etab = (float*)workspace + n * 64 + n * 3;
+  const int emb_ld = in_node + time_emb_dim;
+  {
+    const int tot = Bt * T * 64;
+    hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim, t_out,
+                       emb_w, emb_ld, emb_b, etab);
+    if (int rc = check_launch("temb_kernel")) return rc;
+    hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
+                       etab, x, v, st.hs, st.xs, st.vs);
+    if (int rc = check_launch("h0_kernel")) return rc;
+    const size_t tot2 = n * emb_ld;
+    hipLaunchKernelGGL(emb_in_kernel, dim3((unsigned)((tot2 + 255) / 256)), dim3(256), 0, s, BN, T, in_node,
+                       time_emb_dim, Bt, h, t_out, st.emb_in);
+    if (int rc = check_launch("emb_in_kernel")) return rc;
+  }
+  for (int l = 0; l < L; ++l) {
+    TconvArgs a{};
+    a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
+    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l];
+    a.h = st.hs + l * n * 64; a.x = st.xs + l * n * 3; a.v = st.vs + l * n * 3; a.lm = loc_mean;
+    a.h_out = st.he + l * n * 64; a.x_out = st.xe + l * n * 3; a.v_out = st.ve + l * n * 3;
+    if (int rc = launch_tconv(false, a, s)) return rc;
+    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, B, a.h_out, a.x_out, a.v_out, edge_fea, blobs[l], 0.f, 1.f,
+                                    0, st.hs + (l + 1) * n * 64, st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
+                                    st.Ms + l * n * 64, st.Fs + l * n * 4))
+      return rc;
+    hipMemcpyAsync(st.vs + (l + 1) * n * 3, a.v_out, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  }
+  hipMemcpyAsync(x_out, st.xs + L * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(v_out, st.vs + L * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(h_out, st.hs + L * n * 64, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  return check_launch("egno_forward_train copies");
+}
+
+size_t nonode_egno_backward_workspace_bytes(int B, int N, int T, int modes) {
+  return bwd_ws(nullptr, B, N, T, effective_modes(T, modes)).floats * sizeof(float);
+}
+
+int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                         int modes, int Bt, const float* loc_mean, const float* edge_fea,
+                         const float* const* bblobs, const float* const* tconv_w, const float* const* tconvx_w,
+                         const void* state, const float* g_x, const float* g_v, const float* g_h,
+                         const nonode_layer_grads* layer_grads, float* const* g_tconv, float* const* g_tconvx,
+                         float* g_emb_w, float* g_emb_b, void* workspace, size_t workspace_bytes, void* stream) {
+  if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || modes < 1 || modes > MMAX || Bt <= 0 ||
+      n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "egno_backward: B=%d N=%d T=%d", B, N, T);
+  if (!loc_mean || !bblobs || !tconv_w || !tconvx_w || !state || !g_x || !layer_grads || !g_tconv || !g_tconvx ||
+      !g_emb_w || !g_emb_b || !workspace || (n_edge_feat > 0 && !edge_fea))
+    return fail(NONODE_EINVAL, "egno_backward: null pointer");
+  const int M = effective_modes(T, modes);
+  if (workspace_bytes < nonode_egno_backward_workspace_bytes(B, N, T, modes))
+    return fail(NONODE_EINVAL, "egno_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int BN = B * N, L = n_layers, ne = n_edge_feat;
+  const size_t n = (size_t)BN * T;
+  const long long E = (long long)n * (N - 1);
+  TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, time_emb_dim);
+  BwdWs w = bwd_ws(workspace, B, N, T, M);
+  Gemm gemm{w.partial, GEMM_MAX_BLK, s};
+  // grads of the final outputs
+  float *gx = w.gx[0], *gv = w.gv[0], *gh = w.gh[0];
+  hipMemcpyAsync(gx, g_x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (g_v) hipMemcpyAsync(gv, g_v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  else hipMemsetAsync(gv, 0, n * 3 * sizeof(float), s);
+  if (g_h) hipMemcpyAsync(gh, g_h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  else hipMemsetAsync(gh, 0, n * 64 * sizeof(float), s);
+  int cur = 0;
+  const int ld1 = 2 * HID + 1 + ne;
+  for (int l = L - 1; l >= 0; --l) {
+    const nonode_layer_grads& lg = layer_grads[l];
+    const float* he = st.he + l * n * 64;
+    const float* xe = st.xe + l * n * 3;
+    const float* ve = st.ve + l * n * 3;
+    const float* bb = bblobs[l];
+    // ---- EGNN_Layer reverse ----
+    NodeBwdArgs na;
+    na.n = (int)n; na.N = N; na.h = he; na.v = ve; na.M = st.Ms + l * n * 64; na.F = st.Fs + l * n * 4;
+    na.gxo = gx; na.gvo = gv; na.gho = gh; na.bb = bb;
+    na.gv = w.gve; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp;
+    na.op_gt = w.op_gt; na.op_t = w.op_t; na.op_gphi = w.op_gphi; na.op_z = w.op_z; na.op_gz = w.op_gz;
+    const int ntile = (int)((n + 15) / 16);
+    hipLaunchKernelGGL(node_bwd_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, na);
+    if (int rc = check_launch("node_bwd_kernel")) return rc;
+    hipMemsetAsync(w.GB, 0, n * 64 * sizeof(float), s);
+    hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
+    {
+      const int n_graphs = T * B;
+      const int cus = num_cus();
+      const int G = n_graphs < cus ? n_graphs : cus;
+      const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
+      int ct = 8 < tiles_per ? 8 : tiles_per;
+      int s_max = 0;
+      while (ct > 1 && edge_bwd_lds_floats(ct, N, &s_max) * 4 > 160 * 1024) --ct;
+      const size_t lds = edge_bwd_lds_floats(ct, N, &s_max) * 4;
+      if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "egno_backward: N=%d too large", N);
+      static std::once_flag once;
+      std::call_once(once, [] {
+        hipFuncSetAttribute((const void*)edge_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      });
+      EdgeBwdArgs ea;
+      ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = ct; ea.s_max = s_max;
+      ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
+      ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX;
+      ea.e_gz1 = w.e_gz1; ea.e_gz2 = w.e_gz2; ea.e_gz3 = w.e_gz3; ea.e_a = w.e_a; ea.e_m = w.e_m;
+      ea.e_c1 = w.e_c1; ea.e_sc = w.e_sc;
+      if (ne == 0) ea.ne = 0;
+      hipLaunchKernelGGL(edge_bwd_kernel, dim3(G), dim3(256), lds, s, ea);
+      if (int rc = check_launch("edge_bwd_kernel")) return rc;
+    }
+    hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, (int)n, w.ghp, w.GA, w.GB, gx,
+                       w.GX, bb, w.ghe, w.gxe);
+    if (int rc = check_launch("node_post_kernel")) return rc;
+    // ---- weight gradients of this layer ----
+    // edge Linear 1: columns [s | h_i | h_j | e] (EGNO order, basic.py:152-154, 170); its bias
+    // gradient sum_e gz1 = sum_i GA_i comes with the h_i block
+    if (int rc = gemm(w.e_gz1, 64, 64, w.e_sc + 1, ESC, 1, E, lg.edge_w1, ld1, 0, nullptr)) return rc;
+    if (ne > 0)
+      if (int rc = gemm(w.e_gz1, 64, 64, w.e_sc + 2, ESC, ne, E, lg.edge_w1, ld1, 2 * HID + 1, nullptr)) return rc;
+    if (int rc = gemm(w.GA, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1, lg.edge_b1)) return rc;
+    if (int rc = gemm(w.GB, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1 + HID, nullptr)) return rc;
+    if (int rc = gemm(w.e_gz2, 64, 64, w.e_a, 64, 64, E, lg.edge_w2, 64, 0, lg.edge_b2)) return rc;
+    if (int rc = gemm(w.e_gz3, 64, 64, w.e_m, 64, 64, E, lg.coord_w1, 64, 0, lg.coord_b1)) return rc;
+    if (int rc = gemm(w.e_sc, ESC, 1, w.e_c1, 64, 64, E, lg.coord_w2, 64, 0, lg.coord_b2)) return rc;
+    if (int rc = gemm(w.op_gt, 64, 64, he, 64, 64, (long long)n, lg.vel_w1, 64, 0, lg.vel_b1)) return rc;
+    if (int rc = gemm(w.op_gphi, 1, 1, w.op_t, 64, 64, (long long)n, lg.vel_w2, 64, 0, lg.vel_b2)) return rc;
+    if (int rc = gemm(w.op_gz, 64, 64, he, 64, 64, (long long)n, lg.node_w1, 128, 0, lg.node_b1)) return rc;
+    if (int rc = gemm(w.op_gz, 64, 64, st.Ms + l * n * 64, 64, 64, (long long)n, lg.node_w1, 128, HID, nullptr))
+      return rc;
+    if (int rc = gemm(gh, 64, 64, w.op_z, 64, 64, (long long)n, lg.node_w2, 64, 0, lg.node_b2)) return rc;
+    // ---- TimeConv_x reverse: x, v of the layer's TimeConv input ----
+    const int nxt = cur ^ 1;
+    hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes,
+                       st.xs + l * n * 3, st.vs + l * n * 3, loc_mean, w.gxe, w.gve, tconvx_w[l], w.gx[nxt],
+                       w.gv[nxt], w.xpart);
+    if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
+    {
+      // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M stay zero)
+      hipMemsetAsync(g_tconvx[l], 0, 2 * 2 * modes * 2 * sizeof(float), s);
+      float* tmp = w.partial;
+      hipLaunchKernelGGL(rows_reduce, dim3(1), dim3(64), 0, s, w.xpart, (long long)BN * 3, 2 * 2 * MMAX * 2, tmp);
+      if (int rc = check_launch("rows_reduce")) return rc;
+      for (int io = 0; io < 4; ++io)
+        hipMemcpyAsync(g_tconvx[l] + io * modes * 2, tmp + io * MMAX * 2, M * 2 * sizeof(float),
+                       hipMemcpyDeviceToDevice, s);
+    }
+    // ---- TimeConv reverse: h of the layer's TimeConv input ----
+    hipLaunchKernelGGL(tconv_bwd_kernel, dim3(BN), dim3(64), 0, s, BN, T, M, modes, st.hs + l * n * 64, w.ghe,
+                       tconv_w[l], w.gh[nxt], w.tXr, w.tXi, w.tgYr, w.tgYi);
+    if (int rc = check_launch("tconv_bwd_kernel")) return rc;
+    hipMemsetAsync(g_tconv[l], 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);
+    for (int m = 0; m < M; ++m) {
+      // weights1 [i][o][Mfull][2]: gWr = Xr^T gYr + Xi^T gYi, gWi = -Xi^T gYr + Xr^T gYi (K = BN columns)
+      const float* Xr = w.tXr + (size_t)m * BN * 64;
+      const float* Xi = w.tXi + (size_t)m * BN * 64;
+      const float* gYr = w.tgYr + (size_t)m * BN * 64;
+      const float* gYi = w.tgYi + (size_t)m * BN * 64;
+      float* gw = g_tconv[l] + m * 2;
+      const int ldw = 64 * modes * 2, csw = modes * 2;
+      if (int rc = gemm(Xr, 64, 64, gYr, 64, 64, BN, gw, ldw, 0, nullptr, 0, csw)) return rc;
+      if (int rc = gemm(Xi, 64, 64, gYi, 64, 64, BN, gw, ldw, 0, nullptr, 1, csw)) return rc;
+      if (int rc = gemm(Xi, 64, 64, gYr, 64, 64, BN, gw + 1, ldw, 0, nullptr, 0, csw, -1.f)) return rc;
+      if (int rc = gemm(Xr, 64, 64, gYi, 64, 64, BN, gw + 1, ldw, 0, nullptr, 1, csw)) return rc;
+    }
+    cur = nxt;
+    gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
+  }
+  // ---- embedding Linear (egno.py:63-76): dW = sum_rows gh0 (x) [h_in, temb], db = sum gh0 ----
+  const int emb_ld = in_node + time_emb_dim;
+  if (int rc = gemm(gh, 64, 64, st.emb_in, emb_ld, emb_ld, (long long)n, g_emb_w, emb_ld, 0, g_emb_b)) return rc;
+  return NONODE_OK;
+}
+
+}  // extern "C"

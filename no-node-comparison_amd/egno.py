@@ -158,6 +158,29 @@ class EGNO(nn.Module):
         self._blobs, self._blob_key = (blobs, tblobs), key
         return self._blobs
 
+    def layer_param_names(self, i):
+        """Parameter names of layer i in nonode_layer_weights / nonode_layer_grads field order."""
+        pre = f"layers.{i}."
+        e, c, v, n = ("edge_message_net.scalar_net.mlp", "coord_net.mlp", "node_v_net.mlp", "node_net.mlp")
+        return [pre + f"{mlp}.{k}.{wb}" for mlp in (e, c, v, n) for k in (0, 2) for wb in ("weight", "bias")]
+
+    def _packed_bwd(self):
+        """Backward fragments (unscaled forward + transposed) per layer, rebuilt like _packed()."""
+        params = [p for l in self.layers for p in l.parameters()]
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if getattr(self, "_bblobs", None) is not None and key == self._bblob_key:
+            return self._bblobs
+        L = _lib.lib()
+        dev = self.embedding.weight.device
+        bb = torch.empty(self.n_layers, L.nonode_bwd_blob_floats(), dtype=torch.float32, device=dev)
+        stream = _lib.stream_of(bb)
+        for i, layer in enumerate(self.layers):
+            w = layer.weight_struct()
+            _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), _lib.VARIANT_EGNO, self.hidden_nf, self.in_edge_nf,
+                                               _lib.ptr(bb[i]), stream))
+        self._bblobs, self._bblob_key = bb, key
+        return bb
+
     def forward(self, x, h, edge_index, edge_fea, v=None, loc_mean=None, timesteps_in=None, timesteps_out=None):
         """egno.py:37-111. x, v, loc_mean: [BN, 3]; h: [BN, in_node_nf]; edge_index: 2 x [E]
         (fully connected, the dataset's edge order); edge_fea: [E, in_edge_nf];

@@ -149,3 +149,25 @@ def test_segno_gravity_n100():
     assert maxnorm_rel(x, fx["step::x"]) < TOL32
     assert maxnorm_rel(v, fx["step::v"]) < TOL32
     assert maxnorm_rel(h, fx["step::h"]) < TOL32
+
+
+def test_oracle_gradients_match_reference_golden():
+    """oracle/egno_grad.py (hand-written reverse pass) vs the reference's autograd gradients of one
+    training step (main_simulation_simple_no.py:267-280), recorded in egno_grad.npz."""
+    from oracle import egno_grad as og
+    fx = load_golden("egno_fwd")
+    gd = load_golden("egno_grad")
+    p = {k: v.astype(np.float64) for k, v in params_of(fx).items()}
+    i = lambda k: fx["in::" + k].astype(np.float64)  # noqa: E731
+    loss, losses, g = og.egno_loss_and_grads(p, i("x"), i("h"), fx["in::row"], fx["in::col"], i("edge_attr"),
+                                             i("v"), i("loc_mean"), fx["in::t_out"],
+                                             gd["in::loc_true"].astype(np.float64), T=int(fx["cfg::T"]))
+    assert abs(loss - float(gd["out::loss"])) <= 1e-5 * abs(float(gd["out::loss"]))
+    np.testing.assert_allclose(losses, gd["out::losses"], rtol=1e-5)
+    assert set(g) == set(p)
+    for k in p:
+        ref = gd["grad::" + k]
+        if np.abs(ref).max() == 0:          # parameters that do not reach the loss (nograd list)
+            assert np.abs(g[k]).max() == 0, k
+        else:
+            assert maxnorm_rel(g[k], ref) < 2e-6, k
