@@ -261,6 +261,54 @@ def run_segno(args, world, rank, dev, gravity=False):
     return res
 
 
+def run_egno_train(args, world, rank, dev):
+    """C4: EGNO training step, charged N=20, T=10, B=512 per GPU (4096 over 8 GPUs): forward with
+    saved state, the reference loss (main_simulation_simple_no.py:273-280), backward through the HIP
+    kernels, ONE all-reduce of the flat gradient buffer (RCCL over xGMI), Adam(lr 1e-4, wd 1e-8,
+    model_confs.yaml:15-17)."""
+    import no_node_comparison_amd as pkg
+    from no_node_comparison_amd.sharding import FlatGrads, max_over_ranks
+    from no_node_comparison_amd import _lib
+    B, N, T = args.batch, 20, 10
+    torch.manual_seed(0)
+    model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                     num_timesteps=T, time_emb_dim=32, device=dev).train()
+    case = build_egno_case(B, N, T, seed=1234, dev=dev, world=world, rank=rank)
+    g = torch.Generator().manual_seed(777 + rank)
+    loc_true = torch.randn(B, N, T, 3, generator=g).to(dev)
+    fg = FlatGrads(model.parameters())
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=1e-8)
+
+    def step():
+        fg.zero_()
+        x, _, _ = model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],
+                        loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
+        pred = x.reshape(T, B, N, 3).permute(1, 2, 0, 3)
+        loss = torch.nn.functional.mse_loss(pred, loc_true, reduction="none").mean((0, 1, 3)).mean()
+        loss.backward()
+        fg.allreduce_()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    barrier_sync(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    value = B * world * args.steps / el
+    return {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d, seeded)",
+            "loss": float(loss.detach()),
+            "config": {"workload": f"C4: EGNO training step (fwd + bwd + 1 all-reduce + Adam), charged N=20, T=10, "
+                                   f"B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world, "n_balls": N,
+                       "num_timesteps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                       "parallelism": f"data-parallel x{world}, one RCCL all-reduce per step"}}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -277,8 +325,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=512, help="samples per GPU")
-    ap.add_argument("--workload", default="egno", choices=["egno", "segno", "segno_gravity"],
-                    help="egno = C2 (the headline line); segno = C3; segno_gravity = C5")
+    ap.add_argument("--workload", default="egno", choices=["egno", "segno", "segno_gravity", "egno_train"],
+                    help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", dest="kernel_events", action="store_false")
     args = ap.parse_args()
@@ -287,6 +335,8 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     if args.workload == "egno":
         res = run_egno(args, world, rank, dev)
+    elif args.workload == "egno_train":
+        res = run_egno_train(args, world, rank, dev)
     else:
         res = run_segno(args, world, rank, dev, gravity=args.workload == "segno_gravity")
     if rank == 0:

@@ -661,8 +661,10 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         load_h16frags(fwc1, reinterpret_cast<const h8*>(sW + 4096), lane);
       }
       // PAIR (one wave per SIMD): b2 / bc1 / wc2 also stay in registers for the edge phase
+      // (8-wave PAIR: two waves share a SIMD's 512 registers, so these stay in LDS)
+      constexpr bool RV = PAIR && NW <= 4;
       f4 rB2[4], rBC1[4], rWC2[4];
-      if (PAIR) {
+      if (RV) {
         load_vp(rB2, vB2_, g);
         load_vp(rBC1, vBC1_, g);
         load_vp(rWC2, vWC2_, g);
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         };
         auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
           silu_ecl_dbg(c1, p.debug);
-          const float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2, g)) + bc2;
+          const float c = (RV ? dot_r(c1, rWC2) : dot_vp(c1, vWC2, g)) + bc2;
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
           if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
             f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -753,7 +755,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           // before its sums are committed. So the scheduler can put one unit's MFMAs beside the
           // other unit's SiLU work.
           f4 pr[4];
-          load_ecl(pr, Prow, g);                       // receiver projection, fixed for the segment
+          if (RV) load_ecl(pr, Prow, g);               // receiver projection, fixed for the segment
           auto head2 = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
               __attribute__((always_inline)) {
             int j = n + k;
@@ -763,6 +765,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
             const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
             load_ecl(a, sQ + sl * ROWP, g);
+            if (!RV) load_ecl(pr, Prow, g);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
 #pragma unroll
@@ -777,7 +780,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           auto edge_f = [&](f4 (&c1)[4], float r0, float r1, float r2, float& f0, float& f1, float& f2)
               __attribute__((always_inline)) {
             silu_ecl(c1);
-            const float c = dot_r(c1, rWC2) + bc2;
+            const float c = (RV ? dot_r(c1, rWC2) : dot_vp(c1, vWC2, g)) + bc2;
             f0 = r0 * c; f1 = r1 * c; f2 = r2 * c;
             if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
               f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -794,10 +797,12 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             silu_ecl(a);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
+            if (!RV) load_vp(m, vB2, g);
             mfma_dense<4>(m, w2f, a, lane);
             silu_ecl(m);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
+            if (!RV) load_vp(c, vBC1, g);
             mfma_dense<4>(c, wc1f, m, lane);
             edge_f(c, r0, r1, r2, f0, f1, f2);
           };
@@ -824,6 +829,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             float gmax = fmaxf(amax_ecl(a0), amax_ecl(a1));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; }
+            if (!RV) { load_vp(m0, vB2, g); load_vp(m1, vB2, g); }
             {
               h8 ah0[2], al0[2], ah1[2], al1[2];
               h16_split(a0, ah0, al0);
@@ -841,6 +847,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               a0[mt] = rBC1[mt];
               a1[mt] = rBC1[mt];
             }
+            if (!RV) { load_vp(a0, vBC1, g); load_vp(a1, vBC1, g); }
             {
               h8 mh0[2], ml0[2], mh1[2], ml1[2];
               h16_split(m0, mh0, ml0);

@@ -599,90 +599,128 @@ __global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* 
 }
 
 // ---- weight-gradient GEMMs ---------------------------------------------------------------------
-// partial[blk][i][j] = sum over rows k of this block's K-slice of G[k*ldg + i] * A[k*lda + j]
-// (j < N; j == N is the ones column: the bias gradient sum_k G[k][i]). M <= 64, N <= 64.
-constexpr int GEMM_KROWS = 64;
-__global__ __launch_bounds__(256) void gemm_tn_partial(const float* G, int ldg, int M, const float* A, int lda,
-                                                       int N, long long K, long long kslice, float* partial) {
-  __shared__ float sG[GEMM_KROWS][64], sA[GEMM_KROWS][65];
-  const int tid = threadIdx.x;
-  const long long k0 = (long long)blockIdx.x * kslice;
-  const long long k1 = min(K, k0 + kslice);
-  const int NO = M * (N + 1);
-  float acc[17];
-  for (int q = 0; q < 17; ++q) acc[q] = 0.f;
-  for (long long kb = k0; kb < k1; kb += GEMM_KROWS) {
-    const int rows = (int)min((long long)GEMM_KROWS, k1 - kb);
-    __syncthreads();
-    for (int i = tid; i < GEMM_KROWS * 64; i += 256) {
-      const int kr = i >> 6, col = i & 63;
-      sG[kr][col] = (kr < rows && col < M) ? G[(kb + kr) * ldg + col] : 0.f;
-      sA[kr][col] = (kr < rows && col < N) ? A[(kb + kr) * lda + col] : 0.f;
+// partial[wave][i][j] = sum over this wave's K-slice of G[k*ldg + i] * A[k*lda + j]  (j < N), and
+// partial[wave][i][N] = sum_k G[k][i] (the bias gradient). M, N <= 64. Each wave streams its rows
+// straight into v_mfma_f32_16x16x4_f32: lane (l & 15, l >> 4) supplies G[k0 + (l>>4)][16 ti + (l&15)]
+// as the A operand and A[k0 + (l>>4)][16 tj + (l&15)] as the B operand, so K runs along the lane
+// groups and the 64 x 64 result stays in 16 accumulator tiles. HBM-bound (one pass over G and A).
+__global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__ G, int ldg, int M,
+                                                       const float* __restrict__ A, int lda, int N, long long K,
+                                                       long long kslice, float* partial) {
+  const int lane = threadIdx.x & 63, il = lane & 15, kr = lane >> 4;
+  const long long gw = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long long k0 = gw * kslice, k1 = min(K, k0 + kslice);
+  f4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+  for (long long k = k0; k < k1; k += 4) {
+    const long long row = k + kr;
+    const bool ok = row < k1;
+    float gv[4], av[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int cg = 16 * t + il;
+      gv[t] = (ok && cg < M) ? G[row * ldg + cg] : 0.f;
+      av[t] = (ok && cg < N) ? A[row * lda + cg] : 0.f;
+      bsum[t] += gv[t];
     }
-    if (tid < GEMM_KROWS) sA[tid][64] = tid < rows ? 1.f : 0.f;
-    __syncthreads();
-    for (int q = 0; q < 17; ++q) {
-      const int o = tid + q * 256;
-      if (o < NO) {
-        const int i = o / (N + 1), j = o - i * (N + 1);
-        const int jj = j == N ? 64 : j;
-        float s = acc[q];
-        for (int kr = 0; kr < GEMM_KROWS; ++kr) s = fmaf(sG[kr][i], sA[kr][jj], s);
-        acc[q] = s;
-      }
-    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[a], av[b], acc[a][b]);
   }
-  for (int q = 0; q < 17; ++q) {
-    const int o = tid + q * 256;
-    if (o < NO) partial[(size_t)blockIdx.x * NO + o] = acc[q];
+  const int NO = M * (N + 1);
+  float* out = partial + (size_t)gw * NO;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * a + 4 * kr + q, jj = 16 * b + il;   // accumulator: C[4(l>>4)+q][l&15]
+        if (i < M && jj < N) out[i * (N + 1) + jj] = acc[a][b][q];
+      }
+    const float bs = group_sum(bsum[a]);
+    if (kr == 0 && 16 * a + il < M) out[(16 * a + il) * (N + 1) + N] = bs;
   }
 }
 
 // dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
-// partial[b][i][N]; partials added in a fixed order (deterministic)
-__global__ void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld, int col0, int cs,
-                            float* bias, int accumulate, float scale) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+// partial[b][i][N]. 256 threads = 16 outputs x 16 strided partial sums, combined in a fixed order
+// (deterministic).
+// (columns j >= split go to col1 + (j - split) instead: the [s | ... | e] blocks of edge W1)
+__global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld,
+                                                   int col0, int cs, float* bias, int accumulate, float scale,
+                                                   int split, int col1) {
+  __shared__ float red[16][17];
   const int NO = M * (N + 1);
-  if (o >= NO) return;
+  const int ol = threadIdx.x & 15, part = threadIdx.x >> 4;
+  const int o = blockIdx.x * 16 + ol;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[(size_t)b * NO + o];
+  if (o < NO)
+    for (int b = part; b < nblk; b += 16) s += partial[(size_t)b * NO + o];
+  red[part][ol] = s;
+  __syncthreads();
+  if (part != 0 || o >= NO) return;
+  s = 0.f;
+  for (int q = 0; q < 16; ++q) s += red[q][ol];
   s *= scale;
   const int i = o / (N + 1), j = o - i * (N + 1);
   if (j < N) {
-    if (dst) { float* p = dst + (size_t)i * ld + (size_t)(col0 + j) * cs; *p = accumulate ? *p + s : s; }
+    const int col = j < split ? col0 + j : col1 + (j - split);
+    if (dst) { float* p = dst + (size_t)i * ld + (size_t)col * cs; *p = accumulate ? *p + s : s; }
   } else if (bias) {
     bias[i] = accumulate ? bias[i] + s : s;
   }
 }
 
-// sum over rows of part[rows][cnt] -> dst[cnt] (fixed order)
-__global__ void rows_reduce(const float* part, long long rows, int cnt, float* dst) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= cnt) return;
-  double s = 0.0;
-  for (long long r = 0; r < rows; ++r) s += part[r * cnt + o];
-  dst[o] = (float)s;
+// out[blk][o] = sum over this block's row slice of part[rows][cnt] (cnt <= 32): 256 threads =
+// 32 values x 8 strided row lanes, combined in a fixed order; a second launch with one block
+// sums the block partials (deterministic)
+__global__ __launch_bounds__(256) void rows_reduce(const float* part, long long rows, int cnt, long long slice,
+                                                   float* out) {
+  __shared__ float red[8][33];
+  const int o = threadIdx.x & 31, lanei = threadIdx.x >> 5;
+  const long long r0 = (long long)blockIdx.x * slice, r1 = min(rows, r0 + slice);
+  float s = 0.f;
+  if (o < cnt)
+    for (long long r = r0 + lanei; r < r1; r += 8) s += part[r * cnt + o];
+  red[lanei][o] = s;
+  __syncthreads();
+  if (lanei == 0 && o < cnt) {
+    s = 0.f;
+    for (int q = 0; q < 8; ++q) s += red[q][o];
+    out[(size_t)blockIdx.x * cnt + o] = s;
+  }
 }
 
 struct Gemm {
   float* partial;
-  int max_blk;
+  int max_waves;
   hipStream_t s;
-  // C[M][N] = sum_k G[k] (x) A[k] into dst (row stride ld, column offset col0) and bias
+  // C[M][N] = sum_k G[k] (x) A[k] into dst (row stride ld, column (col0 + j) * cs; columns j >= split
+  // at col1 + j - split), bias[i] = sum_k G[k][i]; scale multiplies both
   int operator()(const float* G, int ldg, int M, const float* A, int lda, int N, long long K, float* dst,
-                 int ld, int col0, float* bias, int accumulate = 0, int cs = 1, float scale = 1.f) const {
-    if (M > 64 || N > 64 || M * (N + 1) > 17 * 256) return fail(NONODE_EINVAL, "gemm: M=%d N=%d", M, N);
-    long long kslice = (K + max_blk - 1) / max_blk;
-    kslice = ((kslice + GEMM_KROWS - 1) / GEMM_KROWS) * GEMM_KROWS;
-    if (kslice < GEMM_KROWS) kslice = GEMM_KROWS;
-    const int nblk = (int)((K + kslice - 1) / kslice);
-    if (nblk < 1) return NONODE_OK;
+                 int ld, int col0, float* bias, int accumulate = 0, int cs = 1, float scale = 1.f,
+                 int split = 1 << 30, int col1 = 0) const {
+    if (M > 64 || N > 64) return fail(NONODE_EINVAL, "gemm: M=%d N=%d", M, N);
+    if (K <= 0) return NONODE_OK;
+    long long waves = (K + 255) / 256;                 // >= 256 rows per wave
+    if (waves > max_waves) waves = max_waves;
+    long long kslice = (K + waves - 1) / waves;
+    kslice = (kslice + 3) & ~3LL;
+    waves = (K + kslice - 1) / kslice;
+    const int nblk = (int)((waves + 3) / 4);
+    const int nparts = nblk * 4;
+    const int NO = M * (N + 1);
+    hipMemsetAsync(partial, 0, (size_t)nparts * NO * sizeof(float), s);   // waves past K write nothing
     hipLaunchKernelGGL(gemm_tn_partial, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice, partial);
     if (int rc = check_launch("gemm_tn_partial")) return rc;
-    const int NO = M * (N + 1);
-    hipLaunchKernelGGL(gemm_reduce, dim3((NO + 255) / 256), dim3(256), 0, s, partial, nblk, M, N, dst, ld, col0,
-                       cs, bias, accumulate, scale);
+    hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, partial, nparts, M, N, dst, ld, col0,
+                       cs, bias, accumulate, scale, split, col1);
     return check_launch("gemm_reduce");
   }
 };
@@ -718,7 +756,7 @@ struct BwdWs {
   float *partial;
   size_t floats;
 };
-constexpr int GEMM_MAX_BLK = 1024;
+constexpr int GEMM_MAX_WAVES = 1024;
 BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   const size_t BN = (size_t)B * N, n = BN * T, E = n * (N - 1);
   BwdWs w;
@@ -733,7 +771,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.e_a = take(E * 64); w.e_m = take(E * 64); w.e_c1 = take(E * 64); w.e_sc = take(E * ESC);
   w.tXr = take(M * BN * 64); w.tXi = take(M * BN * 64); w.tgYr = take(M * BN * 64); w.tgYi = take(M * BN * 64);
   w.xpart = take(BN * 3 * 2 * 2 * MMAX * 2);
-  w.partial = take((size_t)GEMM_MAX_BLK * 17 * 256);
+  w.partial = take((size_t)(GEMM_MAX_WAVES + 4) * 64 * 65);
   w.floats = tot;
   return w;
 }
@@ -850,7 +888,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
   const long long E = (long long)n * (N - 1);
   TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, time_emb_dim);
   BwdWs w = bwd_ws(workspace, B, N, T, M);
-  Gemm gemm{w.partial, GEMM_MAX_BLK, s};
+  Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
   // grads of the final outputs
   float *gx = w.gx[0], *gv = w.gv[0], *gh = w.gh[0];
   hipMemcpyAsync(gx, g_x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -907,9 +945,9 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
     // ---- weight gradients of this layer ----
     // edge Linear 1: columns [s | h_i | h_j | e] (EGNO order, basic.py:152-154, 170); its bias
     // gradient sum_e gz1 = sum_i GA_i comes with the h_i block
-    if (int rc = gemm(w.e_gz1, 64, 64, w.e_sc + 1, ESC, 1, E, lg.edge_w1, ld1, 0, nullptr)) return rc;
-    if (ne > 0)
-      if (int rc = gemm(w.e_gz1, 64, 64, w.e_sc + 2, ESC, ne, E, lg.edge_w1, ld1, 2 * HID + 1, nullptr)) return rc;
+    if (int rc = gemm(w.e_gz1, 64, 64, w.e_sc + 1, ESC, 1 + ne, E, lg.edge_w1, ld1, 0, nullptr, 0, 1, 1.f, 1,
+                      2 * HID + 1))
+      return rc;
     if (int rc = gemm(w.GA, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1, lg.edge_b1)) return rc;
     if (int rc = gemm(w.GB, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1 + HID, nullptr)) return rc;
     if (int rc = gemm(w.e_gz2, 64, 64, w.e_a, 64, 64, E, lg.edge_w2, 64, 0, lg.edge_b2)) return rc;
@@ -931,7 +969,12 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
       // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M stay zero)
       hipMemsetAsync(g_tconvx[l], 0, 2 * 2 * modes * 2 * sizeof(float), s);
       float* tmp = w.partial;
-      hipLaunchKernelGGL(rows_reduce, dim3(1), dim3(64), 0, s, w.xpart, (long long)BN * 3, 2 * 2 * MMAX * 2, tmp);
+      const int cnt = 2 * 2 * MMAX * 2;
+      const long long rows = (long long)BN * 3, slice = 256;
+      const int nb = (int)((rows + slice - 1) / slice);
+      hipLaunchKernelGGL(rows_reduce, dim3(nb), dim3(256), 0, s, w.xpart, rows, cnt, slice, tmp + 64);
+      if (int rc = check_launch("rows_reduce")) return rc;
+      hipLaunchKernelGGL(rows_reduce, dim3(1), dim3(256), 0, s, tmp + 64, (long long)nb, cnt, (long long)nb, tmp);
       if (int rc = check_launch("rows_reduce")) return rc;
       for (int io = 0; io < 4; ++io)
         hipMemcpyAsync(g_tconvx[l] + io * modes * 2, tmp + io * MMAX * 2, M * 2 * sizeof(float),

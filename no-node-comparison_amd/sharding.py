@@ -65,3 +65,32 @@ def gather_samples(local, total):
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
     return torch.cat([p[: hi - lo] for p, (lo, hi) in zip(parts, sizes)]).to(local.device)
+
+
+class FlatGrads:
+    """Data-parallel gradient exchange with ONE collective per step.
+
+    Every parameter's .grad is a view into one contiguous fp32 buffer, so autograd accumulates
+    straight into it and the step needs a single all-reduce (sum) of the flat buffer (0.81 MB
+    for EGNO) followed by a division by the world size: with equal shards this is the gradient of
+    the global mean loss. With world size 1 (or no process group) it is a no-op."""
+
+    def __init__(self, params):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        off = 0
+        for p in self.params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero_(self):
+        self.flat.zero_()
+
+    def allreduce_(self):
+        if not _initialized() or dist.get_world_size() == 1:
+            return self.flat
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+        self.flat.div_(dist.get_world_size())
+        return self.flat

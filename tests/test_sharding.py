@@ -123,3 +123,48 @@ def test_egno_sharded_equals_whole_batch_gloo_ws2():
     if "w::embedding.weight" not in fx:
         pytest.skip("golden weights missing")
     _run(2, _egno_sharded, 5)
+
+
+def _dp_grads(rank, world, total):
+    """Each rank: the oracle's gradients of the mean loss over its sample shard, written into a
+    FlatGrads buffer and all-reduced; the result must equal the whole-batch gradients (SURVEY
+    §8e: one all-reduce of the flat gradient buffer, then / world)."""
+    from oracle import egno_grad as og
+    from oracle import harness as oh
+    from no_node_comparison_amd.sharding import FlatGrads
+    fx = load_golden("egno_fwd")
+    p = {k: v.astype(np.float64) for k, v in params_of(fx).items()}
+    N, T = 5, 10
+    rng = np.random.default_rng(3)
+    loc = rng.standard_normal((total, N, 3))
+    vel = rng.standard_normal((total, N, 3))
+    q = rng.choice([-1.0, 1.0], size=(total, N, 1))
+    target = rng.standard_normal((total, N, T, 3))
+
+    def grads(lo, hi):
+        B = hi - lo
+        r, c = oh.full_edges(B, N)
+        qq = q[lo:hi].reshape(-1, 1)
+        x, v, ea, nodes, lm = oh.prepare_inputs(loc[lo:hi], vel[lo:hi], qq[r] * qq[c], r, c, N, q[lo:hi])
+        t_out = np.tile(np.arange(1, T + 1), (B, 1))
+        _, _, g = og.egno_loss_and_grads(p, x, nodes, r, c, ea, v, lm, t_out, target[lo:hi], T=T)
+        return g
+
+    names = sorted(p)
+    params = [torch.nn.Parameter(torch.zeros(p[k].shape, dtype=torch.float32)) for k in names]
+    fg = FlatGrads(params)
+    lo, hi = shard_range(total, world, rank)
+    g = grads(lo, hi)
+    for prm, k in zip(params, names):
+        prm.grad.copy_(torch.from_numpy(g[k]))
+    fg.allreduce_()
+    if rank == 0:
+        ref = grads(0, total)
+        for prm, k in zip(params, names):
+            want = ref[k]
+            if np.abs(want).max() > 0:
+                assert maxnorm_rel(prm.grad.numpy(), want) < 1e-5, k
+
+
+def test_dp_allreduce_equals_whole_batch_gradients_gloo_ws2():
+    _run(2, _dp_grads, 4)
