@@ -131,14 +131,19 @@ def run_egno(args, world, rank, dev):
         for _ in range(args.warmup):
             out = call()
         barrier_sync(world, dev)
-        if args.kernel_events:
-            _lib.profile_begin(16 * args.steps + 64)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             out = call()
         barrier_sync(world, dev)
         el = time.perf_counter() - t0
-        records = _lib.profile_end() if args.kernel_events else []
+        # kernel durations for the roofline: a separate instrumented pass over the same workload
+        # (hipEvents recorded around every launch on its stream; kept out of the timed loop above)
+        records = []
+        if args.kernel_events:
+            _lib.profile_begin(16 * args.steps + 64)
+            for _ in range(args.steps):
+                out = call()
+            records = _lib.profile_end()
     layer_events = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
     tconv_ms = [ms for kind, ms in records if kind in (2, 3)]
     from no_node_comparison_amd.sharding import max_over_ranks

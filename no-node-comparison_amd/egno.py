@@ -206,12 +206,24 @@ class EGNO(nn.Module):
             return egno_forward_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N)
         return self._forward_kernels(x, h, edge_fea, v, loc_mean, timesteps_out, B, N)
 
+    def _t_out_f32(self, t_out):
+        """timesteps_out as f32 (cached per tensor/version: callers pass the same int64 tensor)."""
+        if t_out.dtype == torch.float32 and t_out.is_contiguous():
+            return t_out
+        key = (t_out.data_ptr(), t_out._version, tuple(t_out.shape), t_out.dtype)
+        c = getattr(self, "_tcache", None)
+        if c is not None and c[0] == key:
+            return c[1]
+        tt = t_out.detach().to(torch.float32).contiguous()
+        self._tcache = (key, tt, t_out)      # keep t_out alive so its pointer cannot be reused
+        return tt
+
     @torch.no_grad()
     def _forward_kernels(self, x, h, edge_fea, v, loc_mean, t_out, B, N):
         T = self.num_timesteps
         f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
         x, h, v, lm, ef = f32(x), f32(h), f32(v), f32(loc_mean), f32(edge_fea)
-        tt = f32(t_out)
+        tt = self._t_out_f32(t_out)
         blobs, tblobs = self._packed()
         dev = x.device
         n = T * B * N
