@@ -253,37 +253,147 @@ __global__ __launch_bounds__(256) void node_bwd_kernel(NodeBwdArgs p) {
 }
 
 // ---- edge backward (basic.py:107-144, 167-173 reversed) ----------------------------------------
-constexpr int ESC = 8;   // per-edge scalar row: [gc, s, e_0 .. e_{ne-1}, 0 ...]
+// One kernel per layer does the per-edge reverse pass AND the edge-level weight gradients: each
+// wave keeps dW2 = sum_e gz2 (x) a and dWc1 = sum_e gz3 (x) m in MFMA accumulators (plus the bias,
+// coord-output and scalar-input-column sums in per-lane registers) and writes one partial per wave;
+// gemm_reduce adds the partials in a fixed order (deterministic). No per-edge operand ever goes to
+// HBM (the unfused version wrote 6 x 64 floats per edge, 3 GB per layer at C2).
+//
+// Weight-gradient MFMA: v_mfma_f32_16x16x4_f32 with K = edges. The ECL holds edges along
+// lane & 15, so a unit's [16 edges][64] operands go through a per-wave LDS tile ([edge][ROWT]) and
+// come back with channels along lane & 15: k-step ks, lane (e', g) reads edge 4g + ks, channel
+// 16t + e' (row stride 84 floats puts the four lane groups on disjoint banks). Columns 64..79 of
+// the first operand's rows carry the edge's scalar inputs [|r|^2, e_0, ..] (zero past NF), the B
+// operand of the W1 scalar-column gradient.
+//
+// Per-wave partial (floats), blocks in gemm_reduce's [M][N+1] layout (column N = bias):
+constexpr int EW_W2 = 0;                  // dW2  [64][65], column 64 = db2
+constexpr int EW_WC1 = 64 * 65;           // dWc1 [64][65], column 64 = dbc1
+constexpr int EW_WC2 = 2 * 64 * 65;       // dwc2 [1][65],  column 64 = dbc2
+constexpr int EW_FEAT = EW_WC2 + 68;      // dW1 scalar-input columns [64][NF + 1] (NF = 1 + ne <= 5)
+constexpr int EW_STRIDE = EW_FEAT + 64 * 6;
+constexpr int EB_MAX_BLOCKS = 256;        // edge_bwd grid cap: EB_MAX_BLOCKS * 4 wave partials
+constexpr int ROWT = 84;                  // transpose-tile row stride (floats)
+constexpr int EB_TSTRIDE = 2 * 16 * ROWT; // per-wave transpose tile (two [16][ROWT] operands)
+
 struct EdgeBwdArgs {
   int n_graphs, N, ne, ef_mod, ct, s_max;
   const float* h; const float* x; const float* ef; const float* bb;
   const float* gF; const float* gM;
   float* GA; float* GB; float* GX;                                    // per node (GB, GX atomically)
-  float* e_gz1; float* e_gz2; float* e_gz3; float* e_a; float* e_m; float* e_c1; float* e_sc;
+  float* wpart;                                                       // [grid * 4][EW_STRIDE]
+  int dbg;   // ablation bits (timing only, NONODE_EBDBG): 1 GA/GB atomics, 2 GX atomics, 4 wgrad,
+             // 8 feat wgrad, 16 phase C, 32 Wc1^T, 64 W2^T
 };
 
-size_t edge_bwd_lds_floats(int ct, int N, int* s_max_out) {
+// PASS 1 sums GA (per receiver), GB (per sender) and GX in WAVE-PRIVATE LDS tables by plain
+// read-add-write (the 16 receivers and the 16 senders of one unit are distinct, and one wave's
+// units run in order), and the four tables are added at the end of the chunk: LDS float atomics
+// (ds_add_f32, 38 per unit) had cost more than the whole rest of the pass.
+size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
   const int s_max = ((16 * ct - 1) / N + 2) * N;
   if (s_max_out) *s_max_out = s_max;
-  // sP, sGM, sGA [ct*16][ROWP]; sQ, sGB [s_max][ROWP]; sX, sGX [s_max][4]; sGF [ct*16][4]
-  return (size_t)ct * 16 * ROWP * 3 + (size_t)s_max * ROWP * 2 + (size_t)s_max * 8 + (size_t)ct * 16 * 4;
+  // sP, sGM [ct*16][ROWP]; sQ [s_max][ROWP]; sX [s_max][4]; sGF [ct*16][4]; 4 x tile;
+  // PASS 1: 4 x (sGA [ct*16][ROWP], sGB [s_max][ROWP], sGX [s_max][4])
+  return (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
+         4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (size_t)s_max * (ROWP + 4)) : 0);
 }
 
+// acc[ot][it] += sum over the unit's 16 edges of G[e][16 ot + .] (x) A[e][16 it + .]; lane (e, g)
+// of acc[ot][it][q] holds dW[16 ot + 4 g + q][16 it + e]. bsum[t] += G summed over the lane's four
+// edges 4g..4g+3 at channel 16 t + e (the bias gradient, finished by group_sum).
+__device__ __forceinline__ void wgrad_unit(f4 (&acc)[4][4], float (&bsum)[4], const f4 (&G)[4], const f4 (&A)[4],
+                                           float* tile, int g, int e) {
+  float* tG = tile;
+  float* tA = tile + 16 * ROWT;
+  store_ecl(tG + e * ROWT, G, g);
+  store_ecl(tA + e * ROWT, A, g);
+  __builtin_amdgcn_wave_barrier();   // one wave writes and reads its own tile: LDS keeps wave order
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int row = (4 * g + ks) * ROWT + e;
+    float gv[4], av[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { gv[t] = tG[row + 16 * t]; av[t] = tA[row + 16 * t]; bsum[t] += gv[t]; }
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ot], av[it], acc[ot][it]);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// acc[ot] += sum over the unit's edges of G[e][16 ot + .] (x) fe[e][.]: lane (e, g) of acc[ot][q]
+// holds dW1[16 ot + 4 g + q][scalar column e] (e < NF)
+template <int NF>
+__device__ __forceinline__ void wgrad_feat(f4 (&acc)[4], const f4 (&G)[4], const float (&fe)[NF], float* tile, int g,
+                                           int e) {
+  store_ecl(tile + e * ROWT, G, g);
+  if (g == 0) {
+#pragma unroll
+    for (int k = 0; k < NF; ++k) tile[e * ROWT + 64 + k] = fe[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int row = (4 * g + ks) * ROWT + e;
+    float gv[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) gv[t] = tile[row + 16 * t];
+    const float fv = tile[row + 64];
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot) acc[ot] = mfma(gv[ot], fv, acc[ot]);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// sum over the 16 lanes of a lane group (the edges of a unit)
+__device__ __forceinline__ float edge_sum16(float v) {
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Two launches per layer (register budget: one wave cannot hold both 64x64 accumulators next to the
+// per-edge working set): PASS 0 recomputes the edge up to gz3 and accumulates dWc1, dbc1, dwc2,
+// dbc2; PASS 1 does the whole reverse pass with dW2, db2, the W1 scalar columns and GA / GB / GX.
+template <int NE, int PASS>
 __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NW = 4;
+  constexpr int NF = 1 + NE;   // scalar inputs of edge W1: |r|^2, e_0 .. e_{NE-1}
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
+  const int rows = p.ct * 16;
   float* sP = smem;
-  float* sGM = sP + p.ct * 16 * ROWP;
-  float* sGA = sGM + p.ct * 16 * ROWP;
-  float* sQ = sGA + p.ct * 16 * ROWP;
-  float* sGB = sQ + p.s_max * ROWP;
-  float* sX = sGB + p.s_max * ROWP;
-  float* sGX = sX + p.s_max * 4;
-  float* sGF = sGX + p.s_max * 4;
+  float* sGM = sP + rows * ROWP;
+  float* sQ = sGM + rows * ROWP;
+  float* sX = sQ + p.s_max * ROWP;
+  float* sGF = sX + p.s_max * 4;
+  float* tile = sGF + rows * 4 + wave * EB_TSTRIDE;
+  float* sGA = sGF + rows * 4 + NW * EB_TSTRIDE;   // [NW][rows][ROWP]     (PASS 1)
+  float* sGB = sGA + NW * rows * ROWP;              // [NW][s_max][ROWP]
+  float* sGX = sGB + NW * p.s_max * ROWP;           // [NW][s_max][4]
+  float* myGA = sGA + wave * rows * ROWP;
+  float* myGB = sGB + wave * p.s_max * ROWP;
+  float* myGX = sGX + wave * p.s_max * 4;
   const float* bb = p.bb;
   const float bc2 = bb[BOFF_SCAL + 0];
+  const float* wW2 = bb + BOFF_W2;
+  const float* wWc1 = bb + BOFF_WC1;
+  const float* wWc1T = bb + BOFF_WC1T;
+  const float* wW2T = bb + BOFF_W2T;
+  f4 accW[4][4];   // PASS 0: dWc1, PASS 1: dW2
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) accW[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 accFe[4], sWC2[4];
+  zero4(accFe); zero4(sWC2);
+  float sB[4] = {0.f, 0.f, 0.f, 0.f};   // PASS 0: dbc1, PASS 1: db2
+  float sGC = 0.f;
+  // scalar-input columns 64..79 of the tile rows: zero once (columns past NF stay zero)
+  for (int i = lane; i < 16 * 16; i += 64) tile[(i >> 4) * ROWT + 64 + (i & 15)] = 0.f;
   const int G = gridDim.x;
   const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;
   const int nend = (int)(((long long)(blockIdx.x + 1) * p.n_graphs) / G) * N;
@@ -299,9 +409,10 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
     const int S = (g_hi - g_lo + 1) * N;
     const int nsT = (S + 15) >> 4;
     // ---- A: tables ----
-    for (int i = tid; i < ctc * 16 * ROWP; i += NW * 64) sGA[i] = 0.f;
-    for (int i = tid; i < S * ROWP; i += NW * 64) sGB[i] = 0.f;
-    for (int i = tid; i < S * 4; i += NW * 64) sGX[i] = 0.f;
+    if (PASS == 1) {
+      for (int i = tid; i < NW * rows * ROWP; i += NW * 64) sGA[i] = 0.f;
+      for (int i = tid; i < NW * p.s_max * (ROWP + 4); i += NW * 64) sGB[i] = 0.f;   // sGB and sGX
+    }
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
       sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
@@ -321,7 +432,10 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       if (isP) load_vp(acc, bb + BOFF_VEC + BV_B1 * 64, g);
       else zero4(acc);
       mfma_dense<4>(acc, bb + (isP ? BOFF_WA : BOFF_WB), hin, lane);
-      if (valid) {
+      // rows of receivers past the range are zero: their lanes' a, m feed the weight-gradient
+      // MFMAs (multiplied by zero gradients, so they must be finite)
+      if (isP && !valid) zero4(acc);
+      if (valid || isP) {
         store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
         if (isP) {
           f4 gm[4];
@@ -334,6 +448,9 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
     // ---- B: one unit (16 edges: receivers of a tile x sender offset k) at a time ----
     const int U = ctc * Nm1;
     for (int u = wave; u < U; u += NW) {
+      // the weight fragments are loop-invariant: without this barrier the compiler hoists all four
+      // 64x64 matrices (256 VGPRs) out of the loop and spills
+      asm volatile("" ::: "memory");
       const int tau = u / Nm1, k = u - tau * Nm1 + 1;
       const int rl = 16 * tau + e;
       const int r = rbase + rl;
@@ -349,13 +466,18 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       const float r1 = sX[rls * 4 + 1] - sX[sl * 4 + 1];
       const float r2 = sX[rls * 4 + 2] - sX[sl * 4 + 2];
       const float s2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
-      const size_t eidx = (size_t)rc * Nm1 + jj;
-      const float* efp = p.ef + (((size_t)(gr % p.ef_mod) * N + n) * Nm1 + jj) * p.ne;
+      const float* efp = p.ef + (((size_t)(gr % p.ef_mod) * N + n) * Nm1 + jj) * NE;
+      float fe[NF];
+      fe[0] = s2;
+#pragma unroll
+      for (int kk = 0; kk < NE; ++kk) fe[1 + kk] = efp[kk];
       float ev[2];
 #pragma unroll
       for (int kf = 0; kf < 2; ++kf) {
         const int fi = 4 * kf + g;
-        ev[kf] = fi == 0 ? s2 : (fi - 1 < p.ne ? efp[fi - 1] : 0.f);
+        ev[kf] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < NF; ++kk) ev[kf] = (fi == kk) ? fe[kk] : ev[kf];
       }
       // forward recompute: z1 = P_r + Q_s + W1[:, s|e] [s, e];  a = SiLU(z1)
       f4 z1[4], q4[4];
@@ -365,7 +487,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       for (int mt = 0; mt < 4; ++mt) z1[mt] += q4[mt];
 #pragma unroll
       for (int kf = 0; kf < 2; ++kf) {
-        if (kf * 4 < 1 + p.ne) {
+        if (kf * 4 < NF) {
           const f4 wf = *reinterpret_cast<const f4*>(bb + BOFF_FEAT + kf * 256 + lane * 4);
 #pragma unroll
           for (int mo = 0; mo < 4; ++mo) z1[mo] = mfma(wf[mo], ev[kf], z1[mo]);
@@ -376,12 +498,12 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt];
       silu_true(a);
       load_vp(z2, bb + BOFF_VEC + BV_B2 * 64, g);
-      mfma_dense<4>(z2, bb + BOFF_W2, a, lane);
+      mfma_dense<4>(z2, wW2, a, lane);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt];
       silu_true(m);
       load_vp(z3, bb + BOFF_VEC + BV_BC1 * 64, g);
-      mfma_dense<4>(z3, bb + BOFF_WC1, m, lane);
+      mfma_dense<4>(z3, wWc1, m, lane);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) c1[mt] = z3[mt];
       silu_true(c1);
@@ -396,16 +518,28 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) gz3[mt] *= gc;
       mul_dsilu(gz3, z3);
+      // dWc1 += gz3 (x) m ; dwc2 += gc c1 ; dbc1 += gz3 ; dbc2 += gc
+      if (PASS == 0) {
+        wgrad_unit(accW, sB, gz3, m, tile, g, e);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * c1[mt];
+        sGC += gc;
+        continue;
+      }
       // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m)
       f4 gz2[4];
       load_ecl(gz2, sGM + rl * ROWP, g);
       if (!rvalid) zero4(gz2);
-      mfma_dense<4>(gz2, bb + BOFF_WC1T, gz3, lane);
+      if (!(p.dbg & 32)) mfma_dense<4>(gz2, wWc1T, gz3, lane);
       mul_dsilu(gz2, z2);                       // m = SiLU(z2)
+      // dW2 += gz2 (x) a ; db2 += gz2
+      if (!(p.dbg & 4)) wgrad_unit(accW, sB, gz2, a, tile, g, e);
       f4 gz1[4];
       zero4(gz1);
-      mfma_dense<4>(gz1, bb + BOFF_W2T, gz2, lane);
+      if (!(p.dbg & 64)) mfma_dense<4>(gz1, wW2T, gz2, lane);
       mul_dsilu(gz1, z1);                       // a = SiLU(z1)
+      // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
+      if (!(p.dbg & 8)) wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
       // s = |r|^2 input column
       const float gs = dot_vp(gz1, bb + BOFF_VEC + BV_WS * 64, g);
       gr0 = fmaf(2.f * gs, r0, gr0);
@@ -413,51 +547,120 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       gr2 = fmaf(2.f * gs, r2, gr2);
       if (rvalid) {
         // per-receiver / per-sender sums of gz1 (the W_A h_i and W_B h_j inputs) and x terms
-        float* ga = sGA + rl * ROWP + 4 * g;
-        float* gb = sGB + sl * ROWP + 4 * g;
+        if (!(p.dbg & 1)) {
+          f4 t[4];
+          load_ecl(t, myGA + rl * ROWP, g);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+          for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
+          store_ecl(myGA + rl * ROWP, t, g);
+          load_ecl(t, myGB + sl * ROWP, g);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            atomicAdd(ga + 16 * mt + q, gz1[mt][q]);
-            atomicAdd(gb + 16 * mt + q, gz1[mt][q]);
-          }
-        if (g == 0) {
-          atomicAdd(sGX + rls * 4 + 0, gr0); atomicAdd(sGX + rls * 4 + 1, gr1); atomicAdd(sGX + rls * 4 + 2, gr2);
-          atomicAdd(sGX + sl * 4 + 0, -gr0); atomicAdd(sGX + sl * 4 + 1, -gr1); atomicAdd(sGX + sl * 4 + 2, -gr2);
+          for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
+          store_ecl(myGB + sl * ROWP, t, g);
         }
-        // GEMM operands of this edge (row eidx, the reference edge order)
-        const size_t o = eidx * HID;
-        store_ecl(p.e_gz1 + o, gz1, g);
-        store_ecl(p.e_gz2 + o, gz2, g);
-        store_ecl(p.e_gz3 + o, gz3, g);
-        store_ecl(p.e_a + o, a, g);
-        store_ecl(p.e_m + o, m, g);
-        store_ecl(p.e_c1 + o, c1, g);
-        if (g == 0) {
-          float* sc = p.e_sc + eidx * ESC;
-          sc[0] = gc; sc[1] = s2;
-          for (int kk = 0; kk < p.ne; ++kk) sc[2 + kk] = efp[kk];
+        if (g == 0 && !(p.dbg & 2)) {
+          // receiver rows first, then sender rows (a receiver of one lane can be the sender of another)
+          f4* xr = reinterpret_cast<f4*>(myGX + rls * 4);
+          *xr += f4{gr0, gr1, gr2, 0.f};
+          __builtin_amdgcn_wave_barrier();
+          f4* xs = reinterpret_cast<f4*>(myGX + sl * 4);
+          *xs -= f4{gr0, gr1, gr2, 0.f};
         }
       }
     }
     __syncthreads();
+    if (PASS == 0 || (p.dbg & 16)) continue;
     // ---- C: write the chunk's sums (senders can be shared with the next chunk: atomics) ----
+    // (the four wave-private tables added in wave order)
     for (int i = tid; i < ctc * 16 * HID; i += NW * 64) {
       const int rl = i / HID, ch = i - rl * HID;
       const int r = rbase + rl;
-      if (r < nend) p.GA[(size_t)r * HID + ch] = sGA[rl * ROWP + ch];
+      const int o = rl * ROWP + ch;
+      if (r < nend) p.GA[(size_t)r * HID + ch] = ((sGA[o] + sGA[rows * ROWP + o]) + sGA[2 * rows * ROWP + o]) +
+                                                 sGA[3 * rows * ROWP + o];
     }
     for (int i = tid; i < S * HID; i += NW * 64) {
       const int sl = i / HID, ch = i - sl * HID;
-      atomicAdd(p.GB + (size_t)(s0 + sl) * HID + ch, sGB[sl * ROWP + ch]);
+      const int o = sl * ROWP + ch, st = p.s_max * ROWP;
+      atomicAdd(p.GB + (size_t)(s0 + sl) * HID + ch, ((sGB[o] + sGB[st + o]) + sGB[2 * st + o]) + sGB[3 * st + o]);
     }
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int sl = i / 3, d = i - 3 * sl;
-      atomicAdd(p.GX + (size_t)(s0 + sl) * 4 + d, sGX[sl * 4 + d]);
+      const int o = sl * 4 + d, st = p.s_max * 4;
+      atomicAdd(p.GX + (size_t)(s0 + sl) * 4 + d, ((sGX[o] + sGX[st + o]) + sGX[2 * st + o]) + sGX[3 * st + o]);
     }
     __syncthreads();
   }
+  // ---- D: this wave's weight-gradient partial ----
+  float* wp = p.wpart + (size_t)(blockIdx.x * NW + wave) * EW_STRIDE;
+  const int wo = PASS == 0 ? EW_WC1 : EW_W2;
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = accW[ot][it][q];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float bs = group_sum(sB[t]);
+    if (g == 0) wp[wo + (16 * t + e) * 65 + 64] = bs;
+  }
+  if (PASS == 1) {
+#pragma unroll
+    for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ch = 16 * ot + 4 * g + q;
+        if (e < NF) wp[EW_FEAT + ch * (NF + 1) + e] = accFe[ot][q];
+        if (e == NF) wp[EW_FEAT + ch * (NF + 1) + NF] = 0.f;
+      }
+    return;
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float wc2 = edge_sum16(sWC2[mt][q]);
+      if (e == 0) wp[EW_WC2 + 16 * mt + 4 * g + q] = wc2;
+    }
+  const float gcs = edge_sum16(sGC);   // every lane group holds the same gc per edge: take group 0
+  if (lane == 0) wp[EW_WC2 + 64] = gcs;
+}
+// per-pass chunk size (tiles per LDS chunk) and dynamic LDS bytes
+int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_max_out, size_t* lds_out) {
+  const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
+  int ct = 8 < tiles_per ? 8 : tiles_per;
+  int s_max = 0;
+  while (ct > 1 && edge_bwd_lds_floats(pass, ct, N, &s_max) * 4 > 160 * 1024) --ct;
+  const size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max) * 4;
+  if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "egno_backward: N=%d too large", N);
+  *ct_out = ct; *s_max_out = s_max; *lds_out = lds;
+  return NONODE_OK;
+}
+
+int launch_edge_bwd(int ne, EdgeBwdArgs a, int G, hipStream_t s) {
+  static std::once_flag once[5];
+  auto go = [&](void (*k0)(EdgeBwdArgs), void (*k1)(EdgeBwdArgs)) {
+    std::call_once(once[ne], [&] {
+      hipFuncSetAttribute((const void*)k0, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    size_t lds = 0;
+    if (int rc = edge_bwd_config(0, a.n_graphs, a.N, G, &a.ct, &a.s_max, &lds)) return rc;
+    hipLaunchKernelGGL(k0, dim3(G), dim3(256), lds, s, a);
+    if (int rc = check_launch("edge_bwd_kernel<pass 0>")) return rc;
+    if (int rc = edge_bwd_config(1, a.n_graphs, a.N, G, &a.ct, &a.s_max, &lds)) return rc;
+    hipLaunchKernelGGL(k1, dim3(G), dim3(256), lds, s, a);
+    return check_launch("edge_bwd_kernel<pass 1>");
+  };
+  switch (ne) {
+    case 0: return go(edge_bwd_kernel<0, 0>, edge_bwd_kernel<0, 1>);
+    case 1: return go(edge_bwd_kernel<1, 0>, edge_bwd_kernel<1, 1>);
+    case 2: return go(edge_bwd_kernel<2, 0>, edge_bwd_kernel<2, 1>);
+    case 3: return go(edge_bwd_kernel<3, 0>, edge_bwd_kernel<3, 1>);
+    case 4: return go(edge_bwd_kernel<4, 0>, edge_bwd_kernel<4, 1>);
+  }
+  return fail(NONODE_EUNSUPPORTED, "edge_bwd: n_edge_feat=%d", ne);
 }
 
 // gh = ghp + W_A^T GA + W_B^T GB ;  gx = gxo + GX
@@ -654,14 +857,14 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
 // (columns j >= split go to col1 + (j - split) instead: the [s | ... | e] blocks of edge W1)
 __global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld,
                                                    int col0, int cs, float* bias, int accumulate, float scale,
-                                                   int split, int col1) {
+                                                   int split, int col1, long long pstride) {
   __shared__ float red[16][17];
   const int NO = M * (N + 1);
   const int ol = threadIdx.x & 15, part = threadIdx.x >> 4;
   const int o = blockIdx.x * 16 + ol;
   float s = 0.f;
   if (o < NO)
-    for (int b = part; b < nblk; b += 16) s += partial[(size_t)b * NO + o];
+    for (int b = part; b < nblk; b += 16) s += partial[(size_t)b * pstride + o];
   red[part][ol] = s;
   __syncthreads();
   if (part != 0 || o >= NO) return;
@@ -708,7 +911,7 @@ struct Gemm {
                  int split = 1 << 30, int col1 = 0) const {
     if (M > 64 || N > 64) return fail(NONODE_EINVAL, "gemm: M=%d N=%d", M, N);
     if (K <= 0) return NONODE_OK;
-    long long waves = (K + 255) / 256;                 // >= 256 rows per wave
+    long long waves = (K + 31) / 32;                   // >= 32 rows per wave
     if (waves > max_waves) waves = max_waves;
     long long kslice = (K + waves - 1) / waves;
     kslice = (kslice + 3) & ~3LL;
@@ -716,11 +919,10 @@ struct Gemm {
     const int nblk = (int)((waves + 3) / 4);
     const int nparts = nblk * 4;
     const int NO = M * (N + 1);
-    hipMemsetAsync(partial, 0, (size_t)nparts * NO * sizeof(float), s);   // waves past K write nothing
     hipLaunchKernelGGL(gemm_tn_partial, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice, partial);
     if (int rc = check_launch("gemm_tn_partial")) return rc;
     hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, partial, nparts, M, N, dst, ld, col0,
-                       cs, bias, accumulate, scale, split, col1);
+                       cs, bias, accumulate, scale, split, col1, (long long)NO);
     return check_launch("gemm_reduce");
   }
 };
@@ -751,14 +953,14 @@ struct BwdWs {
   float *gx[2], *gv[2], *gh[2];          // ping-pong grads of the current layer outputs (n rows)
   float *gF, *gM, *ghp, *GA, *GB, *GX, *gxe, *gve, *ghe;
   float *op_gt, *op_t, *op_gphi, *op_z, *op_gz;
-  float *e_gz1, *e_gz2, *e_gz3, *e_a, *e_m, *e_c1, *e_sc;
+  float *wpart;
   float *tXr, *tXi, *tgYr, *tgYi, *xpart;
   float *partial;
   size_t floats;
 };
 constexpr int GEMM_MAX_WAVES = 1024;
 BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
-  const size_t BN = (size_t)B * N, n = BN * T, E = n * (N - 1);
+  const size_t BN = (size_t)B * N, n = BN * T;
   BwdWs w;
   float* p = (float*)base;
   size_t tot = 0;
@@ -767,8 +969,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.gF = take(n * 4); w.gM = take(n * 64); w.ghp = take(n * 64); w.GA = take(n * 64); w.GB = take(n * 64);
   w.GX = take(n * 4); w.gxe = take(n * 3); w.gve = take(n * 3); w.ghe = take(n * 64);
   w.op_gt = take(n * 64); w.op_t = take(n * 64); w.op_gphi = take(n); w.op_z = take(n * 64); w.op_gz = take(n * 64);
-  w.e_gz1 = take(E * 64); w.e_gz2 = take(E * 64); w.e_gz3 = take(E * 64);
-  w.e_a = take(E * 64); w.e_m = take(E * 64); w.e_c1 = take(E * 64); w.e_sc = take(E * ESC);
+  w.wpart = take((size_t)EB_MAX_BLOCKS * 4 * EW_STRIDE);
   w.tXr = take(M * BN * 64); w.tXi = take(M * BN * 64); w.tgYr = take(M * BN * 64); w.tgYi = take(M * BN * 64);
   w.xpart = take(BN * 3 * 2 * 2 * MMAX * 2);
   w.partial = take((size_t)(GEMM_MAX_WAVES + 4) * 64 * 65);
@@ -917,42 +1118,38 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
     hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
     {
       const int n_graphs = T * B;
-      const int cus = num_cus();
-      const int G = n_graphs < cus ? n_graphs : cus;
-      const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
-      int ct = 8 < tiles_per ? 8 : tiles_per;
-      int s_max = 0;
-      while (ct > 1 && edge_bwd_lds_floats(ct, N, &s_max) * 4 > 160 * 1024) --ct;
-      const size_t lds = edge_bwd_lds_floats(ct, N, &s_max) * 4;
-      if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "egno_backward: N=%d too large", N);
-      static std::once_flag once;
-      std::call_once(once, [] {
-        hipFuncSetAttribute((const void*)edge_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      });
+      int G = num_cus();
+      G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
+      G = n_graphs < G ? n_graphs : G;
       EdgeBwdArgs ea;
-      ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = ct; ea.s_max = s_max;
+      static const int ebdbg = getenv("NONODE_EBDBG") ? atoi(getenv("NONODE_EBDBG")) : 0;
+      ea.dbg = ebdbg;
+      ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
       ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
-      ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX;
-      ea.e_gz1 = w.e_gz1; ea.e_gz2 = w.e_gz2; ea.e_gz3 = w.e_gz3; ea.e_a = w.e_a; ea.e_m = w.e_m;
-      ea.e_c1 = w.e_c1; ea.e_sc = w.e_sc;
-      if (ne == 0) ea.ne = 0;
-      hipLaunchKernelGGL(edge_bwd_kernel, dim3(G), dim3(256), lds, s, ea);
-      if (int rc = check_launch("edge_bwd_kernel")) return rc;
+      ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
+      if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
+      // edge-level weight gradients: fixed-order sums of the G*4 wave partials
+      const int nparts = G * 4;
+      const int nf = 1 + ne;
+      auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int split, int col1) {
+        const int NO = M_ * (N_ + 1);
+        hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, w.wpart + off, nparts, M_, N_, dst,
+                           ld, 0, 1, bias, 0, 1.f, split, col1, (long long)EW_STRIDE);
+        return check_launch("gemm_reduce(edge)");
+      };
+      if (int rc = red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 1 << 30, 0)) return rc;
+      if (int rc = red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 1 << 30, 0)) return rc;
+      if (int rc = red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 1 << 30, 0)) return rc;
+      // edge Linear 1 scalar columns [s | e] (EGNO order [s, h_i, h_j, e], basic.py:152-154, 170)
+      if (int rc = red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1)) return rc;
     }
     hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, (int)n, w.ghp, w.GA, w.GB, gx,
                        w.GX, bb, w.ghe, w.gxe);
     if (int rc = check_launch("node_post_kernel")) return rc;
-    // ---- weight gradients of this layer ----
-    // edge Linear 1: columns [s | h_i | h_j | e] (EGNO order, basic.py:152-154, 170); its bias
-    // gradient sum_e gz1 = sum_i GA_i comes with the h_i block
-    if (int rc = gemm(w.e_gz1, 64, 64, w.e_sc + 1, ESC, 1 + ne, E, lg.edge_w1, ld1, 0, nullptr, 0, 1, 1.f, 1,
-                      2 * HID + 1))
-      return rc;
+    // ---- node-level weight gradients of this layer ----
+    // edge Linear 1 h_i / h_j blocks; its bias gradient sum_e gz1 = sum_i GA_i comes with the h_i block
     if (int rc = gemm(w.GA, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1, lg.edge_b1)) return rc;
     if (int rc = gemm(w.GB, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1 + HID, nullptr)) return rc;
-    if (int rc = gemm(w.e_gz2, 64, 64, w.e_a, 64, 64, E, lg.edge_w2, 64, 0, lg.edge_b2)) return rc;
-    if (int rc = gemm(w.e_gz3, 64, 64, w.e_m, 64, 64, E, lg.coord_w1, 64, 0, lg.coord_b1)) return rc;
-    if (int rc = gemm(w.e_sc, ESC, 1, w.e_c1, 64, 64, E, lg.coord_w2, 64, 0, lg.coord_b2)) return rc;
     if (int rc = gemm(w.op_gt, 64, 64, he, 64, 64, (long long)n, lg.vel_w1, 64, 0, lg.vel_b1)) return rc;
     if (int rc = gemm(w.op_gphi, 1, 1, w.op_t, 64, 64, (long long)n, lg.vel_w2, 64, 0, lg.vel_b2)) return rc;
     if (int rc = gemm(w.op_gz, 64, 64, he, 64, 64, (long long)n, lg.node_w1, 128, 0, lg.node_b1)) return rc;
