@@ -347,6 +347,13 @@ __device__ __forceinline__ void wgrad_feat(f4 (&acc)[4], const f4 (&G)[4], const
   __builtin_amdgcn_wave_barrier();
 }
 
+// dst[o] = sum of the block's four wave partials (LDS, EW_STRIDE apart) for o in [o0, o1)
+__device__ __forceinline__ void block_partial(const float* red, float* dst, int o0, int o1) {
+  __syncthreads();
+  for (int o = o0 + (int)threadIdx.x; o < o1; o += 256)
+    dst[o] = ((red[o] + red[EW_STRIDE + o]) + red[2 * EW_STRIDE + o]) + red[3 * EW_STRIDE + o];
+}
+
 // sum over the 16 lanes of a lane group (the edges of a unit)
 __device__ __forceinline__ float edge_sum16(float v) {
 #pragma unroll
@@ -591,8 +598,9 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
     }
     __syncthreads();
   }
-  // ---- D: this wave's weight-gradient partial ----
-  float* wp = p.wpart + (size_t)(blockIdx.x * NW + wave) * EW_STRIDE;
+  // ---- D: weight-gradient partials: each wave's to LDS, then one per block (waves added in order) ----
+  __syncthreads();   // the last chunk's tables are dead: reuse the LDS
+  float* wp = smem + wave * EW_STRIDE;
   const int wo = PASS == 0 ? EW_WC1 : EW_W2;
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot)
@@ -614,6 +622,8 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         if (e < NF) wp[EW_FEAT + ch * (NF + 1) + e] = accFe[ot][q];
         if (e == NF) wp[EW_FEAT + ch * (NF + 1) + NF] = 0.f;
       }
+    block_partial(smem, p.wpart + (size_t)blockIdx.x * EW_STRIDE, EW_W2, EW_WC1);
+    block_partial(smem, p.wpart + (size_t)blockIdx.x * EW_STRIDE, EW_FEAT, EW_FEAT + 64 * (NF + 1));
     return;
   }
 #pragma unroll
@@ -625,6 +635,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
     }
   const float gcs = edge_sum16(sGC);   // every lane group holds the same gc per edge: take group 0
   if (lane == 0) wp[EW_WC2 + 64] = gcs;
+  block_partial(smem, p.wpart + (size_t)blockIdx.x * EW_STRIDE, EW_WC1, EW_WC2 + 65);
 }
 // per-pass chunk size (tiles per LDS chunk) and dynamic LDS bytes
 int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_max_out, size_t* lds_out) {
@@ -632,8 +643,10 @@ int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_ma
   int ct = 8 < tiles_per ? 8 : tiles_per;
   int s_max = 0;
   while (ct > 1 && edge_bwd_lds_floats(pass, ct, N, &s_max) * 4 > 160 * 1024) --ct;
-  const size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max) * 4;
+  size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max) * 4;
   if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "egno_backward: N=%d too large", N);
+  const size_t red = (size_t)4 * EW_STRIDE * 4;   // the end-of-kernel partial combine
+  lds = lds > red ? lds : red;
   *ct_out = ct; *s_max_out = s_max; *lds_out = lds;
   return NONODE_OK;
 }
@@ -683,70 +696,236 @@ __global__ __launch_bounds__(256) void node_post_kernel(int n, const float* ghp,
   }
 }
 
-// ---- TimeConv / TimeConv_x reverse (layer_no.py:80-178; oracle/egno_grad.py spectral_bwd) ------
-// One 64-thread block per column c (channel = thread). Recomputes X = DFT_T(h), Y = X W,
-// y = sum_m (c_m/T)(Yr cos - Yi sin), gy = gout * leaky'(y); then
-// gY_r = sum_t (c_m/T) cos gy, gY_i = -sum_t (c_m/T) sin gy, gX = gY W^T (complex),
-// gh = gout + sum_m (gXr cos - gXi sin). Writes Xr, Xi, gYr, gYi [m][BN][64] for the weight GEMMs.
-__global__ __launch_bounds__(64) void tconv_bwd_kernel(int BN, int T, int M, int Mfull, const float* h, const float* gout,
-                                                       const float* w, float* gh, float* Xr_o, float* Xi_o,
-                                                       float* gYr_o, float* gYi_o) {
-  __shared__ float sXr[MMAX][64], sXi[MMAX][64], sGr[MMAX][64], sGi[MMAX][64];
-  __shared__ float sCos[MMAX][TMAX], sSin[MMAX][TMAX];
-  const int c = blockIdx.x, ch = threadIdx.x;
-  if (ch < M * T) {
-    const int m = ch / T, t = ch % T;
+// ---- TimeConv reverse (layer_no.py:80-126; oracle/egno_grad.py spectral_bwd) -------------------
+// Persistent: each 4-wave workgroup walks 16-column tiles (columns c = (b, n)). Per tile:
+//   1. DFT of the input h (wave w: input channels 16w..16w+15) -> sX (the forward's layout);
+//   2. forward mixing recompute on MFMA -> Yr, Yi (output channels 16w..);
+//   3. gy[t] = gout[t] * leaky'(y[t]);  gYr_m = (c_m/T) sum_t cos gy,  gYi_m = -(c_m/T) sum_t sin gy
+//      -> sG (zero for columns past BN);
+//   4. backward mixing on MFMA: gXr = Wr gYr + Wi gYi, gXi = -Wi gYr + Wr gYi (wave w: input
+//      channels 16w..) and gh[t] = gout[t] + sum_m (gXr_m cos - gXi_m sin)   (Xi = -sum_t h sin);
+//   5. weight gradient: gWr_m += Xr (x) gYr + Xi (x) gYi,  gWi_m += -Xi (x) gYr + Xr (x) gYi over the
+//      tile's columns (K = columns, read straight from sX / sG with channels along lane & 15),
+//      wave w owning rows i = 16w..16w+15.
+// One partial per workgroup [M][re|im][64][64]; tconv_wgrad_reduce adds them in a fixed order.
+constexpr int TB_MAX_BLOCKS = 256;
+
+// backward mixing fragments: mode m < M, c = re|im: frag(mo, mt)[lane][q] = W[i][o][m][c] with
+// i = 16 mo + (l & 15), o = 16 mt + 4 (l >> 4) + q  (A operand over o, unscaled)
+__global__ void tconv_pack_bwd_kernel(const float* w, int Mfull, int M, float* out) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= M * 2 * 4096) return;
+  const int mat = d >> 12, r = d & 4095;
+  const int m = mat >> 1, c = mat & 1;
+  const int q = r & 3, l = (r >> 2) & 63, rest = r >> 8, mt = rest & 3, mo = rest >> 2;
+  const int i = 16 * mo + (l & 15), o = 16 * mt + 4 * (l >> 4) + q;
+  out[d] = w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
+}
+
+struct TconvBwdArgs {
+  int BN, T, M, ntiles;
+  const float* h;      // TimeConv input [T][BN][64]
+  const float* gout;   // gradient of its output
+  const float* wp;     // forward fragments (tconv_pack_kernel layout)
+  const float* wb;     // backward fragments (tconv_pack_bwd_kernel layout)
+  float* gh;           // gradient of the input
+  float* wpart;        // [grid][M][2][64][64]
+};
+
+template <int MM>
+__global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
+  __shared__ __attribute__((aligned(16))) float sX[2 * MM - 1][16][ROWP];   // Xr_0, (Xr_m, Xs_m)
+  __shared__ __attribute__((aligned(16))) float sG[2 * MM][16][ROWP];       // (gYr_m, gYi_m)
+  __shared__ float sCos[MM * TMAX], sSin[MM * TMAX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
+  const int T = p.T, BN = p.BN;
+  if (tid < MM * T) {
+    const int m = tid / T, t = tid - (tid / T) * T;
     const double ang = 2.0 * (double)m * (double)t / (double)T;
-    sCos[m][t] = (float)cospi(ang);
-    sSin[m][t] = (float)sinpi(ang);
+    sCos[m * TMAX + t] = (float)cospi(ang);
+    sSin[m * TMAX + t] = (float)sinpi(ang);
   }
+  const int ch = 16 * wave + 4 * g;   // this lane's 4 channels (input side and output side)
+  f4 aR[MM][4], aI[MM][4];            // gWr_m / gWi_m rows 16 wave.., column tiles it
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int it = 0; it < 4; ++it) aR[m][it] = aI[m][it] = f4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
-  float hv[TMAX], gv[TMAX];
-  for (int t = 0; t < T; ++t) {
-    hv[t] = h[((size_t)t * BN + c) * 64 + ch];
-    gv[t] = gout[((size_t)t * BN + c) * 64 + ch];
-  }
-  for (int m = 0; m < M; ++m) {
-    float xr = 0.f, xi = 0.f;
-    for (int t = 0; t < T; ++t) { xr = fmaf(hv[t], sCos[m][t], xr); xi = fmaf(-hv[t], sSin[m][t], xi); }
-    sXr[m][ch] = xr; sXi[m][ch] = xi;
-  }
-  __syncthreads();
-  // thread = output channel o: Y_m[o] = sum_i X_m[i] W[i][o][m]
-  float y[TMAX];
-  for (int t = 0; t < T; ++t) y[t] = 0.f;
-  for (int m = 0; m < M; ++m) {
-    float yr = 0.f, yi = 0.f;
-    for (int i = 0; i < 64; ++i) {
-      const float wr = w[(((size_t)i * 64 + ch) * Mfull + m) * 2 + 0], wi = w[(((size_t)i * 64 + ch) * Mfull + m) * 2 + 1];
-      yr = fmaf(sXr[m][i], wr, fmaf(-sXi[m][i], wi, yr));
-      yi = fmaf(sXr[m][i], wi, fmaf(sXi[m][i], wr, yi));
+  for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
+    const int col = tile * 16 + e;
+    const bool cvalid = col < BN;
+    const int c = cvalid ? col : BN - 1;
+    auto hval = [&](const float* base, int t) -> f4 {
+      return *reinterpret_cast<const f4*>(base + ((size_t)t * BN + c) * 64 + ch);
+    };
+    // ---- 1: DFT ----
+    {
+      f4 Xr[MM], Xs[MM];
+#pragma unroll
+      for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < T) {
+          const f4 hv = hval(p.h, t);
+#pragma unroll
+          for (int m = 0; m < MM; ++m) {
+            Xr[m] += hv * sCos[m * TMAX + t];
+            if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
+          }
+        }
+      }
+      *reinterpret_cast<f4*>(&sX[0][e][ch]) = Xr[0];
+#pragma unroll
+      for (int m = 1; m < MM; ++m) {
+        *reinterpret_cast<f4*>(&sX[2 * m - 1][e][ch]) = Xr[m];
+        *reinterpret_cast<f4*>(&sX[2 * m][e][ch]) = Xs[m];
+      }
     }
-    const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
-    for (int t = 0; t < T; ++t) y[t] += cm * (yr * sCos[m][t] - yi * sSin[m][t]);
-  }
-  for (int t = 0; t < T; ++t) y[t] = gv[t] * (y[t] > 0.f ? 1.f : 0.01f);   // gy
-  for (int m = 0; m < M; ++m) {
-    const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
-    float gr = 0.f, gi = 0.f;
-    for (int t = 0; t < T; ++t) { gr = fmaf(cm * sCos[m][t], y[t], gr); gi = fmaf(-cm * sSin[m][t], y[t], gi); }
-    sGr[m][ch] = gr; sGi[m][ch] = gi;
-  }
-  __syncthreads();
-  // thread = input channel i: gX_m[i] = sum_o gY_m[o] conj-mix
-  for (int t = 0; t < T; ++t) hv[t] = gv[t];
-  for (int m = 0; m < M; ++m) {
-    float gxr = 0.f, gxi = 0.f;
-    for (int o = 0; o < 64; ++o) {
-      const float wr = w[(((size_t)ch * 64 + o) * Mfull + m) * 2 + 0], wi = w[(((size_t)ch * 64 + o) * Mfull + m) * 2 + 1];
-      gxr = fmaf(sGr[m][o], wr, fmaf(sGi[m][o], wi, gxr));
-      gxi = fmaf(-sGr[m][o], wi, fmaf(sGi[m][o], wr, gxi));
+    __syncthreads();
+    // ---- 2: forward mixing recompute (output tile mo = wave) ----
+    auto mix = [&](f4& acc, const float* frags, int mat, const float (*src)[ROWP]) {
+      f4 in[4];
+      load_ecl(in, &src[e][0], g);
+      const float* wf = frags + (size_t)mat * 4096;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const f4 a = *reinterpret_cast<const f4*>(wf + ((wave * 4 + mt) * 64 + lane) * 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
+      }
+    };
+    f4 Yr[MM], Yi[MM];
+    Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
+    mix(Yr[0], p.wp, 0, sX[0]);
+#pragma unroll
+    for (int m = 1; m < MM; ++m) {
+      const int mat = 1 + 3 * (m - 1);
+      Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
+      Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
+      mix(Yr[m], p.wp, mat + 0, sX[2 * m - 1]);
+      mix(Yr[m], p.wp, mat + 1, sX[2 * m]);
+      mix(Yi[m], p.wp, mat + 1, sX[2 * m - 1]);
+      mix(Yi[m], p.wp, mat + 2, sX[2 * m]);
     }
-    for (int t = 0; t < T; ++t) hv[t] += gxr * sCos[m][t] - gxi * sSin[m][t];
-    const size_t o = ((size_t)m * BN + c) * 64 + ch;
-    Xr_o[o] = sXr[m][ch]; Xi_o[o] = sXi[m][ch]; gYr_o[o] = sGr[m][ch]; gYi_o[o] = sGi[m][ch];
+    // ---- 3: gy and its spectral coefficients ----
+    {
+      f4 gR[MM], gI[MM];
+#pragma unroll
+      for (int m = 0; m < MM; ++m) { gR[m] = f4{0.f, 0.f, 0.f, 0.f}; gI[m] = gR[m]; }
+#pragma unroll
+      for (int t = 0; t < TMAX; ++t) {
+        if (t < T) {
+          f4 y = Yr[0];
+#pragma unroll
+          for (int m = 1; m < MM; ++m) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
+          f4 gy = hval(p.gout, t);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) gy[q] *= (y[q] > 0.f ? 1.f : 0.01f);
+#pragma unroll
+          for (int m = 0; m < MM; ++m) {
+            gR[m] += gy * sCos[m * TMAX + t];
+            gI[m] -= gy * sSin[m * TMAX + t];
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
+        const f4 z = {0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(&sG[2 * m][e][ch]) = cvalid ? gR[m] * cm : z;
+        *reinterpret_cast<f4*>(&sG[2 * m + 1][e][ch]) = cvalid ? gI[m] * cm : z;
+      }
+    }
+    __syncthreads();
+    // ---- 4: backward mixing (input tile mo = wave) and gh ----
+    {
+      f4 gXr[MM], gXi[MM];
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        gXr[m] = f4{0.f, 0.f, 0.f, 0.f};
+        gXi[m] = f4{0.f, 0.f, 0.f, 0.f};
+        mix(gXr[m], p.wb, 2 * m + 0, sG[2 * m]);       //  Wr gYr
+        mix(gXr[m], p.wb, 2 * m + 1, sG[2 * m + 1]);   //  Wi gYi
+        mix(gXi[m], p.wb, 2 * m + 0, sG[2 * m + 1]);   //  Wr gYi
+        f4 t = {0.f, 0.f, 0.f, 0.f};
+        mix(t, p.wb, 2 * m + 1, sG[2 * m]);            //  Wi gYr
+        gXi[m] -= t;
+      }
+      if (cvalid) {
+#pragma unroll
+        for (int t = 0; t < TMAX; ++t) {
+          if (t < T) {
+            f4 o = hval(p.gout, t);
+#pragma unroll
+            for (int m = 0; m < MM; ++m) o += gXr[m] * sCos[m * TMAX + t] - gXi[m] * sSin[m * TMAX + t];
+            *reinterpret_cast<f4*>(p.gh + ((size_t)t * BN + c) * 64 + ch) = o;
+          }
+        }
+      }
+    }
+    // ---- 5: weight gradient over this tile's 16 columns ----
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int row = 4 * g + ks;
+#pragma unroll
+      for (int m = 0; m < MM; ++m) {
+        const float xr = sX[m == 0 ? 0 : 2 * m - 1][row][16 * wave + e];
+        const float xs = m == 0 ? 0.f : sX[2 * m][row][16 * wave + e];
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const float gyr = sG[2 * m][row][16 * it + e], gyi = sG[2 * m + 1][row][16 * it + e];
+          aR[m][it] = mfma(xr, gyr, aR[m][it]);          // Xr gYr
+          aI[m][it] = mfma(xr, gyi, aI[m][it]);          // Xr gYi
+          if (m > 0) {
+            aR[m][it] = mfma(-xs, gyi, aR[m][it]);       // + Xi gYi  (Xi = -Xs)
+            aI[m][it] = mfma(xs, gyr, aI[m][it]);        // - Xi gYr
+          }
+        }
+      }
+    }
+    __syncthreads();
   }
-  for (int t = 0; t < T; ++t) gh[((size_t)t * BN + c) * 64 + ch] = hv[t];
+  float* wp = p.wpart + (size_t)blockIdx.x * p.M * 2 * 4096;
+#pragma unroll
+  for (int m = 0; m < MM; ++m)
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 16 * wave + 4 * g + q, o = 16 * it + e;
+        wp[((m * 2 + 0) * 64 + i) * 64 + o] = aR[m][it][q];
+        wp[((m * 2 + 1) * 64 + i) * 64 + o] = aI[m][it][q];
+      }
+}
+
+// dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
+// strided partial lanes, combined in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst) {
+  __shared__ float red[4][64];
+  const int per = M * 2 * 4096;
+  const int ol = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int d = blockIdx.x * 64 + ol;
+  float s = 0.f;
+  if (d < per)
+    for (int b = pl; b < nblk; b += 4) s += part[(size_t)b * per + d];
+  red[pl][ol] = s;
+  __syncthreads();
+  if (pl != 0 || d >= per) return;
+  s = ((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol];
+  const int mc = d >> 12, r = d & 4095, m = mc >> 1, c = mc & 1, i = r >> 6, o = r & 63;
+  dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = s;
+}
+
+int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
+  switch (M) {
+    case 1: hipLaunchKernelGGL(tconv_bwd_kernel<1>, dim3(G), dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(tconv_bwd_kernel<2>, dim3(G), dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(tconv_bwd_kernel<3>, dim3(G), dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(tconv_bwd_kernel<4>, dim3(G), dim3(256), 0, s, a); break;
+    default: return fail(NONODE_EUNSUPPORTED, "tconv_bwd: modes=%d", M);
+  }
+  return check_launch("tconv_bwd_kernel");
 }
 
 // TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. One thread per (c, d).
@@ -835,8 +1014,11 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
 #pragma unroll
       for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[a], av[b], acc[a][b]);
   }
+  // the block's four wave partials are added through LDS in wave order: one partial per block
+  __shared__ float red[4][64 * 65];
   const int NO = M * (N + 1);
-  float* out = partial + (size_t)gw * NO;
+  const int wv = threadIdx.x >> 6;
+  float* out = red[wv];
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
 #pragma unroll
@@ -849,6 +1031,9 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
     const float bs = group_sum(bsum[a]);
     if (kr == 0 && 16 * a + il < M) out[(16 * a + il) * (N + 1) + N] = bs;
   }
+  __syncthreads();
+  float* dst = partial + (size_t)blockIdx.x * NO;
+  for (int o = threadIdx.x; o < NO; o += 256) dst[o] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
 }
 
 // dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
@@ -917,7 +1102,7 @@ struct Gemm {
     kslice = (kslice + 3) & ~3LL;
     waves = (K + kslice - 1) / kslice;
     const int nblk = (int)((waves + 3) / 4);
-    const int nparts = nblk * 4;
+    const int nparts = nblk;   // one partial per block
     const int NO = M * (N + 1);
     hipLaunchKernelGGL(gemm_tn_partial, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice, partial);
     if (int rc = check_launch("gemm_tn_partial")) return rc;
@@ -954,7 +1139,7 @@ struct BwdWs {
   float *gF, *gM, *ghp, *GA, *GB, *GX, *gxe, *gve, *ghe;
   float *op_gt, *op_t, *op_gphi, *op_z, *op_gz;
   float *wpart;
-  float *tXr, *tXi, *tgYr, *tgYi, *xpart;
+  float *twf, *twb, *tpart, *xpart;
   float *partial;
   size_t floats;
 };
@@ -969,8 +1154,9 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.gF = take(n * 4); w.gM = take(n * 64); w.ghp = take(n * 64); w.GA = take(n * 64); w.GB = take(n * 64);
   w.GX = take(n * 4); w.gxe = take(n * 3); w.gve = take(n * 3); w.ghe = take(n * 64);
   w.op_gt = take(n * 64); w.op_t = take(n * 64); w.op_gphi = take(n); w.op_z = take(n * 64); w.op_gz = take(n * 64);
-  w.wpart = take((size_t)EB_MAX_BLOCKS * 4 * EW_STRIDE);
-  w.tXr = take(M * BN * 64); w.tXi = take(M * BN * 64); w.tgYr = take(M * BN * 64); w.tgYi = take(M * BN * 64);
+  w.wpart = take((size_t)EB_MAX_BLOCKS * EW_STRIDE);
+  w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
+  w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take(BN * 3 * 2 * 2 * MMAX * 2);
   w.partial = take((size_t)(GEMM_MAX_WAVES + 4) * 64 * 65);
   w.floats = tot;
@@ -1129,7 +1315,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
       ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
       // edge-level weight gradients: fixed-order sums of the G*4 wave partials
-      const int nparts = G * 4;
+      const int nparts = G;   // one partial per block
       const int nf = 1 + ne;
       auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int split, int col1) {
         const int NO = M_ * (N_ + 1);
@@ -1178,22 +1364,25 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
                        hipMemcpyDeviceToDevice, s);
     }
     // ---- TimeConv reverse: h of the layer's TimeConv input ----
-    hipLaunchKernelGGL(tconv_bwd_kernel, dim3(BN), dim3(64), 0, s, BN, T, M, modes, st.hs + l * n * 64, w.ghe,
-                       tconv_w[l], w.gh[nxt], w.tXr, w.tXi, w.tgYr, w.tgYi);
-    if (int rc = check_launch("tconv_bwd_kernel")) return rc;
-    hipMemsetAsync(g_tconv[l], 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);
-    for (int m = 0; m < M; ++m) {
-      // weights1 [i][o][Mfull][2]: gWr = Xr^T gYr + Xi^T gYi, gWi = -Xi^T gYr + Xr^T gYi (K = BN columns)
-      const float* Xr = w.tXr + (size_t)m * BN * 64;
-      const float* Xi = w.tXi + (size_t)m * BN * 64;
-      const float* gYr = w.tgYr + (size_t)m * BN * 64;
-      const float* gYi = w.tgYi + (size_t)m * BN * 64;
-      float* gw = g_tconv[l] + m * 2;
-      const int ldw = 64 * modes * 2, csw = modes * 2;
-      if (int rc = gemm(Xr, 64, 64, gYr, 64, 64, BN, gw, ldw, 0, nullptr, 0, csw)) return rc;
-      if (int rc = gemm(Xi, 64, 64, gYi, 64, 64, BN, gw, ldw, 0, nullptr, 1, csw)) return rc;
-      if (int rc = gemm(Xi, 64, 64, gYr, 64, 64, BN, gw + 1, ldw, 0, nullptr, 0, csw, -1.f)) return rc;
-      if (int rc = gemm(Xr, 64, 64, gYi, 64, 64, BN, gw + 1, ldw, 0, nullptr, 1, csw)) return rc;
+    {
+      const int nmat = 1 + 3 * (M - 1);
+      hipLaunchKernelGGL(tconv_pack_kernel, dim3((nmat * 4096 + 255) / 256), dim3(256), 0, s, tconv_w[l], modes, M, T,
+                         w.twf);
+      if (int rc = check_launch("tconv_pack_kernel")) return rc;
+      hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, tconv_w[l], modes,
+                         M, w.twb);
+      if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
+      TconvBwdArgs ta;
+      ta.BN = BN; ta.T = T; ta.M = M; ta.ntiles = (BN + 15) / 16;
+      ta.h = st.hs + l * n * 64; ta.gout = w.ghe; ta.wp = w.twf; ta.wb = w.twb; ta.gh = w.gh[nxt]; ta.wpart = w.tpart;
+      int TG = num_cus();
+      TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;
+      TG = ta.ntiles < TG ? ta.ntiles : TG;
+      if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
+      hipMemsetAsync(g_tconv[l], 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);
+      hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 + 63) / 64), dim3(256), 0, s, w.tpart, TG, M, modes,
+                         g_tconv[l]);
+      if (int rc = check_launch("tconv_wgrad_reduce")) return rc;
     }
     cur = nxt;
     gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
