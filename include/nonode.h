@@ -208,6 +208,58 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
                          float* const* g_tconvx, float* g_emb_w, float* g_emb_b,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+
+/* ---- rollout drivers (rollout_fn / prepare_inputs / energy on the GPU) ---- */
+
+/* prepare_inputs (EGNO/main_simulation_simple_no.py:311-339, num_inputs == 1) for B fully connected
+ * graphs of N nodes, from frame f_b of F frames: loc, vel [F][B*N][3]; f_b = (t_in[b] - 1) mod F
+ * (the reference's loc_all[timesteps_in.T - 1], python indexing) or the last frame if t_in is NULL.
+ * Writes x_out, v_out [B*N][3], nodes [B*N][1 + (charges != NULL)] = [|v|, q],
+ * edge_attr [B*N*(N-1)][n_eo + 1] = [edge_attr_o, |x_i - x_j|^2] (reference edge order), and
+ * loc_mean [B*N][3] (per-graph mean; may be NULL). SEGNO's re-featurisation
+ * (SEGNO/train_nbody.py:222-234) is the same call with charges = NULL, loc_mean = NULL. */
+int nonode_prepare_inputs(int B, int N, int F, const float* loc, const float* vel, const int* t_in,
+                          const float* charges, const float* edge_attr_o, int n_eo, float* x_out,
+                          float* v_out, float* nodes, float* edge_attr, float* loc_mean, void* stream);
+
+/* conserved_energy_fun (utils.py:197-219) of F frames x B graphs: loc, vel [F][B*N][3], weights [B*N]
+ * (charges for kind 0 = charged, tot_energy_charged_batch utils.py:126-144; masses for kind 1 =
+ * gravity, tot_energy_gravity_batch utils.py:175-195). out [F][B]. */
+int nonode_energy(int kind, int F, int B, int N, const float* loc, const float* vel, const float* weights,
+                  float* out, void* stream);
+
+size_t nonode_egno_rollout_workspace_bytes(int B, int N, int T, int Bt, int in_node, int n_edge_feat);
+
+/* rollout_fn (EGNO/main_simulation_simple_no.py:342-384, num_inputs == 1): traj_len segments of
+ * nonode_egno_forward, each restarted from frame t_in[b]-1 (NULL: the last) through
+ * nonode_prepare_inputs. x, h, v, loc_mean, edge_fea: segment-0 inputs (prepared by the caller);
+ * t_out_all [Bt][traj_len*T] (segment i uses columns i*T.. minus i*T, :361-362); charges
+ * [B*N] or NULL (nodes = [|v|(, q)] so in_node = 1 + (charges != NULL)); edge_attr_o [E][n_eo]
+ * (n_edge_feat = n_eo + 1). Outputs loc_preds [traj_len*T][B*N][3]; energies (NULL = skip)
+ * [traj_len*T][B] of every predicted frame with energy_kind / energy_w as in nonode_energy
+ * (the reference's energies_allsteps; its per-segment `energies` are frames T-1, 2T-1, ...). */
+int nonode_egno_rollout(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                        int modes, int Bt, int traj_len, const float* x, const float* h, const float* v,
+                        const float* loc_mean, const float* edge_fea, const float* t_out_all, const int* t_in,
+                        const float* charges, const float* edge_attr_o, int n_eo, int energy_kind,
+                        const float* energy_w, const float* emb_w, const float* emb_b,
+                        const float* const* blobs, const float* const* tconv_blobs,
+                        const float* const* tconvx_w, float* loc_preds, float* energies,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+size_t nonode_segno_rollout_workspace_bytes(int B, int N, int in_node, int n_edge_feat);
+
+/* rollout_fn (SEGNO/train_nbody.py:200-236, num_prev == 1): segment i runs SEGNO.forward with
+ * substeps[i] (host array; the list form of num_steps, :209-212) integrator substeps, then
+ * re-featurises h = |v|, edge_attr = [edge_attr_o, |x_i - x_j|^2]. his, x, v, edge_attr: segment-0
+ * inputs. Outputs loc_preds [traj_len][B*N][3], energies [traj_len][B] (NULL = skip). */
+int nonode_segno_rollout(int B, int N, int in_node, int n_edge_feat, int traj_len, const int* substeps,
+                         const float* his, const float* x, const float* v, const float* edge_attr,
+                         const float* edge_attr_o, int n_eo, int energy_kind, const float* energy_w,
+                         const float* emb_w, const float* emb_b, const float* blob, float coords_weight,
+                         int recurrent, float* loc_preds, float* energies, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

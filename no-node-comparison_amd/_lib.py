@@ -20,6 +20,8 @@ SYMBOLS = (
     "nonode_profile_end", "nonode_tconv_blob_floats", "nonode_pack_tconv",
     "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
     "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
+    "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
+    "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout",
 )
 
 VARIANT_EGNO = 0
@@ -86,6 +88,16 @@ def lib():
     L.nonode_egno_backward.argtypes = ([_i] * 9 + [_vp] * 2 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
                                        + [ctypes.POINTER(LayerGrads), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]
                                        + [_vp] * 3 + [_sz, _vp])
+    L.nonode_prepare_inputs.argtypes = [_i, _i, _i] + [_vp] * 5 + [_i] + [_vp] * 6
+    L.nonode_energy.argtypes = [_i] * 4 + [_vp] * 5
+    L.nonode_egno_rollout_workspace_bytes.argtypes = [_i] * 6
+    L.nonode_egno_rollout_workspace_bytes.restype = _sz
+    L.nonode_egno_rollout.argtypes = ([_i] * 10 + [_vp] * 9 + [_i, _i] + [_vp] * 3 + [ctypes.POINTER(_vp)] * 3
+                                      + [_vp] * 3 + [_sz, _vp])
+    L.nonode_segno_rollout_workspace_bytes.argtypes = [_i] * 4
+    L.nonode_segno_rollout_workspace_bytes.restype = _sz
+    L.nonode_segno_rollout.argtypes = ([_i] * 5 + [_vp] * 6 + [_i, _i] + [_vp] * 4 + [_f, _i] + [_vp] * 3
+                                       + [_sz, _vp])
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

@@ -1,12 +1,23 @@
-"""Device-side counterparts of the reference's hot-path callers.
+"""GPU counterparts of the reference's hot-path callers.
 
-prepare_inputs / rollout_fn keep the reference's argument meaning and return values
-(EGNO/main_simulation_simple_no.py:311-384, SEGNO/train_nbody.py:200-236) but keep every
-tensor on the GPU: no per-frame host round trip.
+prepare_inputs / conserved_energy / egno_rollout / segno_rollout keep the reference's argument
+meaning and return values (EGNO/main_simulation_simple_no.py:311-384, SEGNO/train_nbody.py:200-236,
+utils.py:197-219) but run as HIP kernels (csrc/nonode_rollout.hip): the rollouts are ONE C call
+each (segments, re-featurisation and per-frame energies on the device, no host round trip).
+Like the models, these have no CPU path: tensors must be on the ROCm device.
 """
+import ctypes
+
 import torch
 
+from . import _lib
 from .graph import full_edges  # noqa: F401  (re-exported: get_edges counterpart)
+
+ENERGY_KIND = {"charged": 0, "gravity": 1}
+
+
+def _f32(t):
+    return t.detach().to(torch.float32).contiguous() if t is not None else None
 
 
 def get_edges(batch_size, n_nodes, device="cpu"):
@@ -15,89 +26,149 @@ def get_edges(batch_size, n_nodes, device="cpu"):
     return [r, c]
 
 
-def prepare_inputs(loc, vel, edge_attr_o, edges, n_nodes, num_inputs=1, charges=None):
-    """main_simulation_simple_no.py:311-339 for num_inputs == 1."""
+@torch.no_grad()
+def prepare_inputs(loc, vel, edge_attr_o, edges, n_nodes, num_inputs=1, charges=None, t_in=None):
+    """main_simulation_simple_no.py:311-339 for num_inputs == 1 (nonode_prepare_inputs).
+
+    loc, vel: [B, N, 3] (one frame) or [F, B, N, 3] with ``t_in`` [B] choosing frame t_in-1 per
+    sample (rollout_fn's loc_all[timesteps_in.T - 1]). edges must be the dataset's fully connected
+    list (only its size is used: the kernel indexes pairs implicitly). Returns
+    (loc [BN,3], vel [BN,3], edge_attr [E, n_eo+1], nodes [BN, 1(+1)], loc_mean [BN,3])."""
     if num_inputs != 1:
         raise NotImplementedError("prepare_inputs: num_inputs > 1")
-    rows, cols = edges
-    loc_mean = loc.mean(dim=1, keepdim=True).repeat(1, n_nodes, 1).view(-1, loc.size(-1))
-    loc = loc.reshape(-1, loc.size(-1))
-    vel = vel.reshape(-1, vel.size(-1))
-    nodes = torch.sqrt(torch.sum(vel ** 2, dim=1)).unsqueeze(1)
-    if charges is not None:
-        nodes = torch.cat([nodes, charges.reshape(-1, 1)], dim=1)
-    loc_dist = torch.sum((loc[rows] - loc[cols]) ** 2, 1).unsqueeze(1)
-    edge_attr = torch.cat([edge_attr_o, loc_dist], 1)
-    return loc, vel, edge_attr, nodes, loc_mean
+    _lib.require_device(loc, vel, edge_attr_o, charges)
+    if loc.dim() == 3:
+        loc, vel = loc.unsqueeze(0), vel.unsqueeze(0)
+    F, B, N = loc.shape[0], loc.shape[1], loc.shape[2]
+    if N != n_nodes:
+        raise ValueError(f"prepare_inputs: loc has {N} nodes per graph, n_nodes={n_nodes}")
+    E = B * N * (N - 1)
+    if edges is not None and edges[0].numel() != E:
+        raise ValueError("prepare_inputs: edges must be the fully connected list of B graphs")
+    eo = _f32(edge_attr_o).reshape(E, -1)
+    n_eo = eo.shape[1]
+    loc, vel = _f32(loc), _f32(vel)
+    q = _f32(charges).reshape(-1) if charges is not None else None
+    ti = t_in.reshape(-1).to(torch.int32).contiguous() if t_in is not None else None
+    dev = loc.device
+    BN = B * N
+    x = torch.empty(BN, 3, device=dev)
+    v = torch.empty(BN, 3, device=dev)
+    nodes = torch.empty(BN, 2 if q is not None else 1, device=dev)
+    ea = torch.empty(E, n_eo + 1, device=dev)
+    lm = torch.empty(BN, 3, device=dev)
+    L = _lib.lib()
+    _lib.check(L.nonode_prepare_inputs(B, N, F, _lib.ptr(loc), _lib.ptr(vel), _lib.ptr(ti), _lib.ptr(q), _lib.ptr(eo),
+                                       n_eo, _lib.ptr(x), _lib.ptr(v), _lib.ptr(nodes), _lib.ptr(ea), _lib.ptr(lm),
+                                       _lib.stream_of(loc)))
+    return x, v, ea, nodes, lm
 
 
+@torch.no_grad()
 def conserved_energy(dataset, loc, vel, charges, batch_size):
-    """utils.py:197-219 (equal-size graphs) on device: returns [B] energies."""
+    """conserved_energy_fun (utils.py:197-219) on the GPU: loc, vel [..., B*N, 3] (leading frame
+    axes allowed), charges (charged) or masses (gravity) [B*N] -> energies [..., B]."""
+    _lib.require_device(loc, vel, charges)
     B = batch_size
-    loc = loc.reshape(B, -1, 3)
-    vel = vel.reshape(B, -1, 3)
-    q = charges.reshape(B, -1, 1)
-    diff = loc[:, :, None, :] - loc[:, None, :, :]
-    if dataset == "gravity":
-        ke = 0.5 * torch.sum(q * vel ** 2, dim=(-1, -2))
-        r = diff.norm(dim=-1)
-        inv = torch.where(r > 0, 1.0 / r, torch.zeros_like(r))
-        pe = torch.triu(-(q * q.transpose(1, 2)) * inv, 1).sum(dim=(-1, -2))
-        return ke + pe
-    ke = 0.5 * torch.sum(vel ** 2, dim=(-1, -2))
-    d = diff.norm(dim=-1)
-    d = torch.where(d == 0, torch.full_like(d, float("inf")), d)
-    pe = 0.5 * torch.sum((q * q.transpose(1, 2)) / d, dim=(-1, -2))
-    return ke + pe
+    lead = loc.shape[:-2]
+    BN = loc.shape[-2] if loc.dim() >= 2 else loc.numel() // 3
+    loc, vel = _f32(loc).reshape(-1, BN, 3), _f32(vel).reshape(-1, BN, 3)
+    F, N = loc.shape[0], BN // B
+    w = _f32(charges).reshape(-1)
+    out = torch.empty(F, B, device=loc.device)
+    _lib.check(_lib.lib().nonode_energy(ENERGY_KIND[dataset], F, B, N, _lib.ptr(loc), _lib.ptr(vel), _lib.ptr(w),
+                                        _lib.ptr(out), _lib.stream_of(loc)))
+    return out.reshape(*lead, B) if len(lead) else out.reshape(B)
 
 
 @torch.no_grad()
 def egno_rollout(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean, n_nodes, traj_len,
                  batch_size, charges=None, num_steps=10, timesteps_in=None, timesteps_out=None,
                  energy_dataset=None):
-    """rollout_fn (main_simulation_simple_no.py:342-384), num_inputs == 1, on device.
+    """rollout_fn (main_simulation_simple_no.py:342-384), num_inputs == 1, as one native call.
 
     Returns (loc_preds [traj_len*T, BN, 3], energies [traj_len, B, 1] or None,
-    energies_allsteps [traj_len*T, B, 1] or None)."""
+    energies_allsteps [traj_len*T, B, 1] or None). Unlike the reference, ``timesteps_out`` is not
+    modified in place (the reference's ``t_out -= i*T`` writes into the caller's tensor)."""
+    from .egno import EGNO
+    if not isinstance(model, EGNO):
+        raise TypeError("egno_rollout drives no_node_comparison_amd.EGNO (its packed weights)")
     T = model.num_timesteps
-    preds, en, en_all = [], [], []
-    for i in range(traj_len):
-        t_out = timesteps_out[:, i * T:(i + 1) * T] - i * T
-        loc_o, vel_o, _ = model(loc, nodes, edges, edge_attr, v=vel, loc_mean=loc_mean, timesteps_out=t_out,
-                                timesteps_in=timesteps_in)
-        preds.append(loc_o)
-        la = loc_o.view(num_steps, batch_size, n_nodes, 3)
-        va = vel_o.view(num_steps, batch_size, n_nodes, 3)
-        loc, vel, edge_attr, nodes, loc_mean = prepare_inputs(la[-1], va[-1], edge_attr_o, edges, n_nodes, 1,
-                                                              charges)
-        if energy_dataset is not None:
-            for j in range(num_steps):
-                e = conserved_energy(energy_dataset, la[j], va[j], charges, batch_size)
-                en_all.append(e)
-                if j == num_steps - 1:
-                    en.append(e)
-    out = torch.stack(preds).reshape(traj_len * T, -1, 3)
-    if energy_dataset is None:
-        return out, None, None
-    return out, torch.stack(en).unsqueeze(-1), torch.stack(en_all).unsqueeze(-1)
+    if num_steps != T:
+        raise ValueError("rollout_fn reshapes each segment into num_steps == model.num_timesteps frames")
+    _lib.require_device(loc, nodes, vel, edge_attr, loc_mean, model.embedding.weight)
+    B, N = batch_size, n_nodes
+    BN, E = B * N, B * N * (N - 1)
+    dev = loc.device
+    if timesteps_out is None:
+        timesteps_out = torch.arange(T * traj_len, device=dev).unsqueeze(0)
+    t_all = _f32(timesteps_out)
+    if t_all.shape[1] != T * traj_len:
+        raise ValueError(f"timesteps_out must have {T * traj_len} columns")
+    Bt = t_all.shape[0]
+    ti = timesteps_in.reshape(-1).to(torch.int32).contiguous() if timesteps_in is not None else None
+    eo = _f32(edge_attr_o).reshape(E, -1)
+    q = _f32(charges).reshape(-1) if charges is not None else None
+    x, h, v, lm, ef = _f32(loc), _f32(nodes), _f32(vel), _f32(loc_mean), _f32(edge_attr)
+    blobs, tblobs = model._packed()
+    L = _lib.lib()
+    P = ctypes.c_void_p * model.n_layers
+    tcx = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
+    blob_p = P(*[blobs[i].data_ptr() for i in range(model.n_layers)])
+    tcw_p = P(*[tblobs[i].data_ptr() for i in range(model.n_layers)])
+    tcx_p = P(*[t.data_ptr() for t in tcx])
+    ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
+    preds = torch.empty(traj_len * T, BN, 3, device=dev)
+    en_all = torch.empty(traj_len * T, B, device=dev) if energy_dataset is not None else None
+    ws_bytes = L.nonode_egno_rollout_workspace_bytes(B, N, T, Bt, model.in_node_nf, model.in_edge_nf)
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+    kind = ENERGY_KIND[energy_dataset] if energy_dataset is not None else -1
+    _lib.check(L.nonode_egno_rollout(
+        B, N, T, model.n_layers, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
+        traj_len, _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef), _lib.ptr(t_all), _lib.ptr(ti),
+        _lib.ptr(q), _lib.ptr(eo), eo.shape[1], kind, _lib.ptr(q), _lib.ptr(ew), _lib.ptr(eb), blob_p, tcw_p, tcx_p,
+        _lib.ptr(preds), _lib.ptr(en_all), _lib.ptr(ws), ws_bytes, _lib.stream_of(x)))
+    if en_all is None:
+        return preds, None, None
+    en_all = en_all.unsqueeze(-1)
+    return preds, en_all[T - 1::T], en_all
 
 
 @torch.no_grad()
 def segno_rollout(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps=10, charges=None,
                   energy_dataset=None, batch_size=None):
-    """rollout_fn (train_nbody.py:200-236), num_prev == 1, on device."""
+    """rollout_fn (train_nbody.py:200-236), num_prev == 1, as one native call.
+
+    Returns (loc_preds [traj_len, BN, 3], energies [traj_len, B, 1] or None)."""
+    from .graph import check_full_graph
+    from .segno import SEGNO
+    if not isinstance(model, SEGNO):
+        raise TypeError("segno_rollout drives no_node_comparison_amd.SEGNO (its packed weights)")
+    if model.bug_compat:
+        raise ValueError("segno_rollout integrates (bug_compat=True would return the inputs every segment)")
+    _lib.require_device(loc, h, vel, edge_attr, charges, model.embedding.weight)
+    BN = loc.shape[0]
+    B, N = check_full_graph(edge_index, BN)
+    steps = list(num_steps) if isinstance(num_steps, (list, tuple)) else [int(num_steps)] * traj_len
+    if len(steps) != traj_len:
+        raise ValueError("num_steps should be a list of length traj_len")
+    dev = loc.device
+    x, v, his, ea = _f32(loc), _f32(vel), _f32(h), _f32(edge_attr)
+    q = _f32(charges).reshape(-1)
     rows, cols = edge_index
-    prod = charges.reshape(-1, 1)[rows] * charges.reshape(-1, 1)[cols]
-    preds, energies = [], []
-    for i in range(traj_len):
-        T = num_steps[i] if isinstance(num_steps, (list, tuple)) else num_steps
-        loc_p, _, vel_p = model(h, loc, edge_index, vel, edge_attr, T=T)
-        if energy_dataset is not None:
-            energies.append(conserved_energy(energy_dataset, loc_p, vel_p, charges, batch_size))
-        preds.append(loc_p)
-        loc, vel = loc_p, vel_p
-        h = torch.sqrt(torch.sum(vel ** 2, dim=1)).unsqueeze(1)
-        loc_dist = torch.sum((loc[rows] - loc[cols]) ** 2, 1).unsqueeze(1)
-        edge_attr = torch.cat([prod, loc_dist], 1)
-    out = torch.stack(preds)
-    return out, (torch.stack(energies).unsqueeze(-1) if energy_dataset is not None else None)
+    prod = (q[rows.long()] * q[cols.long()]).reshape(-1, 1).contiguous()   # prod_charges (train_nbody.py:203)
+    blob = model._packed()
+    L = _lib.lib()
+    preds = torch.empty(traj_len, BN, 3, device=dev)
+    en = torch.empty(traj_len, B, device=dev) if energy_dataset is not None else None
+    ws_bytes = L.nonode_segno_rollout_workspace_bytes(B, N, model.in_node_nf, model.in_edge_nf)
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+    kind = ENERGY_KIND[energy_dataset] if energy_dataset is not None else -1
+    steps_arr = (ctypes.c_int * traj_len)(*[int(s) for s in steps])
+    ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
+    _lib.check(L.nonode_segno_rollout(
+        B, N, model.in_node_nf, model.in_edge_nf, traj_len, steps_arr, _lib.ptr(his), _lib.ptr(x), _lib.ptr(v),
+        _lib.ptr(ea), _lib.ptr(prod), 1, kind, _lib.ptr(q), _lib.ptr(ew), _lib.ptr(eb), _lib.ptr(blob),
+        float(model.coords_weight), int(bool(model.recurrent)), _lib.ptr(preds), _lib.ptr(en), _lib.ptr(ws), ws_bytes,
+        _lib.stream_of(x)))
+    return preds, (en.unsqueeze(-1) if en is not None else None)

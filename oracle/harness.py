@@ -68,11 +68,12 @@ def conserved_energy(dataset, loc, vel, charges, B):
 
 
 def egno_rollout(p, nodes, loc, row, col, vel, edge_attr_o, edge_attr, loc_mean, n_nodes,
-                 traj_len, B, charges, T=10, t_out=None, energy=True, **kw):
+                 traj_len, B, charges, T=10, t_out=None, energy=True, t_in=None, dataset="charged", **kw):
     """rollout_fn (main_simulation_simple_no.py:342-384) for num_inputs == 1.
 
-    Each segment: model call, keep all T frames, restart from the LAST frame
-    (timesteps_in - 1 = -1, :367-368), re-featurise with prepare_inputs (:371).
+    Each segment: model call, keep all T frames, restart from frame t_in[b] - 1 of each sample
+    (loc_all[timesteps_in.T - 1, batch_indices], :365-368; python indexing, so t_in = 0 is the
+    LAST frame; t_in None = last frame), re-featurise with prepare_inputs (:371).
     """
     preds, energies, energies_all = [], [], []
     for i in range(traj_len):
@@ -82,11 +83,13 @@ def egno_rollout(p, nodes, loc, row, col, vel, edge_attr_o, edge_attr, loc_mean,
         preds.append(loc_o)
         la = loc_o.reshape(T, B, n_nodes, 3)
         va = vel_o.reshape(T, B, n_nodes, 3)
+        fr = np.full(B, -1) if t_in is None else np.asarray(t_in).reshape(-1) - 1
+        bi = np.arange(B)
         loc, vel, edge_attr, nodes, loc_mean = prepare_inputs(
-            la[-1], va[-1], edge_attr_o, row, col, n_nodes, charges)
+            la[fr, bi], va[fr, bi], edge_attr_o, row, col, n_nodes, charges)
         if energy:
             for j in range(T):
-                en = conserved_energy("charged", la[j], va[j], charges, B)
+                en = conserved_energy(dataset, la[j], va[j], charges, B)
                 energies_all.append(en)
                 if j == T - 1:
                     energies.append(en)
@@ -97,7 +100,7 @@ def egno_rollout(p, nodes, loc, row, col, vel, edge_attr_o, edge_attr, loc_mean,
 
 
 def segno_rollout(p, h, loc, row, col, vel, edge_attr, traj_len, num_steps, charges, B,
-                  energy=True, **kw):
+                  energy=True, dataset="charged", **kw):
     """rollout_fn (train_nbody.py:200-236), num_prev == 1, through forward_step.
 
     Each segment: predict the endpoint after T substeps, feed it back, recompute h = |v| and
@@ -110,7 +113,7 @@ def segno_rollout(p, h, loc, row, col, vel, edge_attr, traj_len, num_steps, char
         hh = _egno.linear(h, p, "embedding")
         loc_p, _, vel_p = _segno.forward_step(p, hh, loc, row, col, vel, edge_attr, T=int(T), **kw)
         if energy:
-            energies.append(conserved_energy("charged", loc_p, vel_p, charges, B))
+            energies.append(conserved_energy(dataset, loc_p, vel_p, charges, B))
         preds.append(loc_p)
         loc, vel = loc_p, vel_p
         h = np.sqrt(np.sum(vel ** 2, axis=1))[:, None]

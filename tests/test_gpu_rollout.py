@@ -1,0 +1,133 @@
+"""GPU parity of the rollout drivers: prepare_inputs, the energy kernel and the
+one-call EGNO / SEGNO rollouts (csrc/nonode_rollout.hip) against the reference golden fixtures
+and the oracle (oracle/harness.py).
+
+Tolerances: featurisation 1e-6 (same fp32 ops as the reference's torch code); energies 1e-5
+relative (the reference sums in float32 numpy, the kernel in float64); positions 1e-5 max-norm
+relative.
+"""
+import numpy as np
+import pytest
+import torch
+
+import no_node_comparison_amd as pkg
+from oracle import harness as oh
+from tests.conftest import load_golden, maxnorm_rel, params_of
+from tests.test_gpu_parity import DEV, TOL, _dev, _egno, _segno
+
+pytestmark = pytest.mark.gpu
+
+
+def test_prepare_inputs_matches_reference_golden():
+    fx = load_golden("egno_fwd")
+    B, N = int(fx["cfg::B"]), int(fx["cfg::N"])
+    edges = pkg.harness.get_edges(B, N, DEV)
+    loc, vel, ea, nodes, lm = pkg.harness.prepare_inputs(
+        _dev(fx["raw::loc"]), _dev(fx["raw::vel"]), _dev(fx["raw::edge_attr_o"]), edges, N, 1, _dev(fx["raw::charges"]))
+    for got, key in [(loc, "in::x"), (vel, "in::v"), (ea, "in::edge_attr"), (nodes, "in::h"),
+                     (lm, "in::loc_mean")]:
+        np.testing.assert_allclose(got.cpu().numpy(), fx[key], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("F,B,N", [(10, 5, 7), (4, 3, 2), (10, 2, 100)])
+def test_prepare_inputs_frame_selection_matches_oracle(F, B, N):
+    """rollout_fn restarts each sample from frame timesteps_in[b] - 1 (python index; 0 -> last)."""
+    rng = np.random.default_rng(F * 100 + N)
+    loc = rng.standard_normal((F, B, N, 3)).astype(np.float32)
+    vel = rng.standard_normal((F, B, N, 3)).astype(np.float32)
+    q = rng.choice([-1.0, 1.0], size=(B, N, 1)).astype(np.float32)
+    row, col = oh.full_edges(B, N)
+    eo = (q.reshape(-1, 1)[row] * q.reshape(-1, 1)[col]).astype(np.float32)
+    t_in = rng.integers(0, F + 1, size=B)
+    x, v, ea, nodes, lm = pkg.harness.prepare_inputs(_dev(loc), _dev(vel), _dev(eo), None, N, 1, _dev(q),
+                                                     t_in=_dev(t_in))
+    fr = t_in - 1
+    ref = oh.prepare_inputs(loc[fr, np.arange(B)], vel[fr, np.arange(B)], eo, row, col, N, q)
+    for got, want in zip((x, v, ea, nodes, lm), ref):
+        np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-6, atol=1e-6)
+
+
+def test_energy_charged_matches_oracle_and_skips_coincident_pairs():
+    fx = load_golden("egno_fwd")
+    ro = load_golden("egno_rollout")
+    B = int(fx["cfg::B"])
+    frames = ro["out::loc_preds"][:3]                       # [3, BN, 3] frames of the reference rollout
+    vel = np.stack([fx["in::v"]] * 3)
+    q = fx["raw::charges"]
+    e = pkg.harness.conserved_energy("charged", _dev(frames), _dev(vel), _dev(q), B).cpu().numpy()
+    for f in range(3):
+        want = oh.conserved_energy("charged", frames[f].astype(np.float64), vel[f].astype(np.float64), q, B)
+        np.testing.assert_allclose(e[f], want, rtol=1e-5)
+    loc = frames[0].copy()
+    loc[1] = loc[0]                                          # a coincident pair: 1/0 -> no contribution
+    e1 = pkg.harness.conserved_energy("charged", _dev(loc), _dev(vel[0]), _dev(q), B).cpu().numpy()
+    want = oh.conserved_energy("charged", loc.astype(np.float64), vel[0].astype(np.float64), q, B)
+    assert np.all(np.isfinite(e1))
+    np.testing.assert_allclose(e1, want, rtol=1e-5)
+
+
+@pytest.mark.parametrize("B,N", [(3, 100), (4, 2), (1, 257)])
+def test_energy_gravity_matches_oracle(B, N):
+    rng = np.random.default_rng(N)
+    loc = rng.standard_normal((B * N, 3)).astype(np.float32)
+    vel = rng.standard_normal((B * N, 3)).astype(np.float32)
+    m = (1 + 0.1 * rng.standard_normal((B, N, 1))).astype(np.float32)
+    e = pkg.harness.conserved_energy("gravity", _dev(loc), _dev(vel), _dev(m), B).cpu().numpy()
+    want = oh.conserved_energy("gravity", loc.astype(np.float64), vel.astype(np.float64), m.astype(np.float64), B)
+    np.testing.assert_allclose(e, want, rtol=1e-5)
+
+
+def test_egno_rollout_restart_frame_matches_oracle():
+    """Two segments restarting from per-sample frames t_in - 1 (not only the last one)."""
+    fx = load_golden("egno_fwd")
+    p = params_of(fx)
+    m = _egno(p)
+    B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
+    edges = pkg.harness.get_edges(B, N, DEV)
+    t_full = np.tile(np.arange(1, 2 * T + 1), (B, 1))
+    t_in = np.array([0, 3, 10, 7])[:B]
+    preds, en, en_all = pkg.harness.egno_rollout(
+        m, _dev(fx["in::h"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(fx["raw::edge_attr_o"]),
+        _dev(fx["in::edge_attr"]), _dev(fx["in::loc_mean"]), N, 2, B, charges=_dev(fx["raw::charges"]), num_steps=T,
+        timesteps_in=_dev(t_in), timesteps_out=_dev(t_full), energy_dataset="charged")
+    row, col = oh.full_edges(B, N)
+    ref, ren, ren_all = oh.egno_rollout(p, fx["in::h"], fx["in::x"], row, col, fx["in::v"], fx["raw::edge_attr_o"],
+                                        fx["in::edge_attr"], fx["in::loc_mean"], N, 2, B, fx["raw::charges"], T=T,
+                                        t_out=t_full, t_in=t_in)
+    assert maxnorm_rel(preds[:T].cpu(), ref[:T]) < TOL
+    assert maxnorm_rel(preds.cpu(), ref) < 1e-4     # segment 2 starts from a chaotic random-init state
+    assert maxnorm_rel(en_all[:T].cpu(), ren_all[:T]) < 1e-5
+    assert maxnorm_rel(en.cpu(), ren) < 1e-4
+    assert en.shape == (2, B, 1) and en_all.shape == (2 * T, B, 1)
+
+
+def test_segno_gravity_vardt_rollout_matches_oracle():
+    """C5-shaped rollout (gravity, N=100, per-segment substep counts) at B=2, 3 segments."""
+    fx = load_golden("segno_gravity")
+    p = params_of(fx)
+    m = _segno(p)
+    B, N = int(fx["cfg::B"]), int(fx["cfg::N"])
+    steps = [5, 7, 6]
+    ei = pkg.harness.get_edges(B, N, DEV)
+    mass = fx["in::mass"]
+    preds, en = pkg.harness.segno_rollout(m, _dev(fx["in::his"]), _dev(fx["in::x"]), ei, _dev(fx["in::v"]),
+                                          _dev(fx["in::edge_attr"]), 3, num_steps=steps, charges=_dev(mass),
+                                          energy_dataset="gravity", batch_size=B)
+    row, col = oh.full_edges(B, N)
+    ref, ren = oh.segno_rollout(p, fx["in::his"], fx["in::x"], row, col, fx["in::v"], fx["in::edge_attr"], 3, steps,
+                                mass, B, dataset="gravity")
+    assert maxnorm_rel(preds[0].cpu(), ref[0]) < TOL
+    assert maxnorm_rel(preds.cpu(), ref) < 1e-4
+    assert maxnorm_rel(en.cpu(), ren) < 1e-4
+
+
+def test_rollout_rejects_mismatched_features():
+    fx = load_golden("egno_fwd")
+    m = _egno(params_of(fx))
+    B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
+    edges = pkg.harness.get_edges(B, N, DEV)
+    with pytest.raises(pkg.NonodeError):   # nodes [|v|, q] need the charges
+        pkg.harness.egno_rollout(m, _dev(fx["in::h"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]),
+                                 _dev(fx["raw::edge_attr_o"]), _dev(fx["in::edge_attr"]), _dev(fx["in::loc_mean"]), N,
+                                 2, B, charges=None, num_steps=T,
+                                 timesteps_out=torch.arange(1, 2 * T + 1, device=DEV).repeat(B, 1))
