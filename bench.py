@@ -225,10 +225,10 @@ def run_segno(args, world, rank, dev, gravity=False):
     steps = c5_substeps() if gravity else [10]
 
     def call():
-        xx, vv = x, v
-        for T in steps:
-            xx, _, vv = model(his, xx, edges, vv, ea, T=T)
-        return xx
+        if gravity:   # rollout_fn (train_nbody.py:200-236) as one native call: re-featurisation + energy
+            return pkg.harness.segno_rollout(model, his, x, edges, v, ea, len(steps), num_steps=steps, charges=q,
+                                             energy_dataset="gravity", batch_size=B)[0]
+        return model(his, x, edges, v, ea, T=steps[0])[0]
 
     from no_node_comparison_amd import _lib
     with torch.no_grad():
@@ -245,7 +245,8 @@ def run_segno(args, world, rank, dev, gravity=False):
         records = _lib.profile_end() if args.kernel_events else []
     el = max_over_ranks(el, dev)
     value = B * world * args.steps / el
-    name = "C5: SEGNO gravity N=100, 50-frame multi-horizon rollout" if gravity else \
+    name = "C5: SEGNO gravity N=100, 50-frame multi-horizon rollout (nonode_segno_rollout: per-segment " \
+        "re-featurisation + gravity energy on the GPU)" if gravity else \
         "C3: SEGNO charged N=20, 10 integrator substeps (one fused launch)"
     res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,

@@ -260,6 +260,25 @@ int nonode_segno_rollout(int B, int N, int in_node, int n_edge_feat, int traj_le
                          int recurrent, float* loc_preds, float* energies, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+
+/* ---- synthetic N-body data (synthetic_sim.py on the GPU, float64) ---- */
+
+/* ChargedParticlesSim.sample_trajectory (synthetic_sim.py:220-296) for S trajectories in one launch:
+ * loc0, vel0 [S][3][N] the initial state after the reference's velocity normalisation and wall
+ * clamp; charges [S][N]; Coulomb forces strength q_i q_j (x_i - x_j) / |x_i - x_j|^3 clamped to
+ * +-max_F per component; leapfrog with step dt. Outputs loc_out, vel_out [S][T/sample_freq - 1][3][N]
+ * (the reference's samples at steps sample_freq, 2 sample_freq, ...). N <= 1024. */
+int nonode_sim_charged(int S, int N, int T, int sample_freq, double dt, double max_F, double strength,
+                       const double* loc0, const double* vel0, const double* charges, double* loc_out,
+                       double* vel_out, void* stream);
+
+/* GravitySim.sample_trajectory_batch (synthetic_sim.py:407-481): pos0, vel0 [S][N][3] (centre-of-mass
+ * velocity already removed), mass [S][N]; softened gravity, kick-drift-kick with step dt. Outputs
+ * pos_out, vel_out, force_out (= a m) [S][T/sample_freq][N][3] sampled at steps 0, sample_freq, ... */
+int nonode_sim_gravity(int S, int N, int T, int sample_freq, double dt, double G, double softening,
+                       const double* pos0, const double* vel0, const double* mass, double* pos_out,
+                       double* vel_out, double* force_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

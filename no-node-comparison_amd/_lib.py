@@ -21,7 +21,7 @@ SYMBOLS = (
     "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
     "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
     "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
-    "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout",
+    "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout", "nonode_sim_charged", "nonode_sim_gravity",
 )
 
 VARIANT_EGNO = 0
@@ -98,6 +98,9 @@ def lib():
     L.nonode_segno_rollout_workspace_bytes.restype = _sz
     L.nonode_segno_rollout.argtypes = ([_i] * 5 + [_vp] * 6 + [_i, _i] + [_vp] * 4 + [_f, _i] + [_vp] * 3
                                        + [_sz, _vp])
+    _d = ctypes.c_double
+    L.nonode_sim_charged.argtypes = [_i] * 4 + [_d] * 3 + [_vp] * 6
+    L.nonode_sim_gravity.argtypes = [_i] * 4 + [_d] * 3 + [_vp] * 7
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

@@ -1558,3 +1558,4 @@ int nonode_debug_stamps(unsigned long long* out16) {
 // training path (forward with saved state + backward), same translation unit
 #include "nonode_train.hip"
 #include "nonode_rollout.hip"
+#include "nonode_sim.hip"
