@@ -279,6 +279,31 @@ int nonode_sim_gravity(int S, int N, int T, int sample_freq, double dt, double G
                        const double* pos0, const double* vel0, const double* mass, double* pos_out,
                        double* vel_out, double* force_out, void* stream);
 
+
+/* ---- dataset -> device batches ---- */
+
+/* One batch of NBodyDynamicsDataset (EGNO/simulation/dataset_simple.py:122-178, num_inputs == 1)
+ * gathered from a split resident on the device: loc, vel [S][Tf][N][3] (the .npy trajectories in
+ * [sample][frame][node][xyz] order), charges [S][N], edge_attr_src [S][N*(N-1)] (the loader's q_i q_j
+ * in the reference edge order, dataset_simple.py:46-72); batch row b is sample idx[b] with input
+ * frame frame0[b] and target frames out_idx[b][0..To). Writes loc0, vel0 [B][N][3],
+ * charges_out [B][N], edge_attr [B][N*(N-1)] and loc_true [B][N][To][3] (locs_out). Index arrays
+ * are device int32. */
+int nonode_gather_batch(int S, int Tf, int N, int B, int To, const float* loc, const float* vel,
+                        const float* charges, const float* edge_attr_src, const int* idx, const int* frame0, const int* out_idx,
+                        float* loc0, float* vel0, float* charges_out, float* edge_attr, float* loc_true,
+                        void* stream);
+
+
+/* ---- rollout metrics ---- */
+
+/* Per (frame t, graph b) of pred, truth [T][B*N][3]: corr[b][t] = Pearson correlation over the
+ * graph's N*3 coordinates (pearson_correlation_batch, utils.py:261-321) and sqerr[t][b] = summed
+ * squared error (the per-horizon MSE of main_simulation_simple_no.py:273 is sum_b sqerr / (B*N*3)).
+ * Either output may be NULL. */
+int nonode_rollout_metrics(int T, int B, int N, const float* pred, const float* truth, float* corr,
+                           float* sqerr, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,6 +7,6 @@ hand-written gfx950 HIP kernels (libnonode.so, C ABI in include/nonode.h). There
 from ._lib import NonodeError, lib  # noqa: F401
 from .egno import EGNO  # noqa: F401
 from .segno import SEGNO  # noqa: F401
-from . import graph, harness, sim  # noqa: F401
+from . import dataset, graph, harness, metrics, sim  # noqa: F401
 
-__all__ = ["EGNO", "SEGNO", "NonodeError", "lib", "graph", "harness", "sim"]
+__all__ = ["EGNO", "SEGNO", "NonodeError", "lib", "dataset", "graph", "harness", "metrics", "sim"]

@@ -22,6 +22,7 @@ SYMBOLS = (
     "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
     "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
     "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout", "nonode_sim_charged", "nonode_sim_gravity",
+    "nonode_gather_batch", "nonode_rollout_metrics",
 )
 
 VARIANT_EGNO = 0
@@ -101,6 +102,8 @@ def lib():
     _d = ctypes.c_double
     L.nonode_sim_charged.argtypes = [_i] * 4 + [_d] * 3 + [_vp] * 6
     L.nonode_sim_gravity.argtypes = [_i] * 4 + [_d] * 3 + [_vp] * 7
+    L.nonode_gather_batch.argtypes = [_i] * 5 + [_vp] * 13
+    L.nonode_rollout_metrics.argtypes = [_i] * 3 + [_vp] * 5
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

@@ -1559,3 +1559,4 @@ int nonode_debug_stamps(unsigned long long* out16) {
 #include "nonode_train.hip"
 #include "nonode_rollout.hip"
 #include "nonode_sim.hip"
+#include "nonode_data.hip"

@@ -1,0 +1,65 @@
+// Dataset -> device batches. The split's trajectories stay in HBM; one launch
+// assembles a batch as NBodyDynamicsDataset.__getitem__ + default_collate would
+// (EGNO/simulation/dataset_simple.py:150-178, 36-72). Edges are the implicit fully connected list
+// (no int64 edge arrays); the per-sample edge features q_i q_j are the loader's (products taken in
+// float64 from the .npy charges, then rounded, as the reference does).
+//
+// Included at the end of nonode.hip (same translation unit).
+
+namespace {
+
+struct GatherArgs {
+  int S, Tf, N, To;
+  const float* loc; const float* vel;   // [S][Tf][N][3]
+  const float* q;                       // [S][N]
+  const float* ea_src;                  // [S][N*(N-1)] q_i q_j per sample
+  const int* idx;                       // [B] sample of each batch row
+  const int* frame0;                    // [B] input frame
+  const int* out_idx;                   // [B][To] target frames
+  float* loc0; float* vel0;             // [B][N][3]
+  float* q_out;                         // [B][N]
+  float* edge_attr;                     // [B][N*(N-1)] = q_i q_j in (i, j != i) order
+  float* loc_true;                      // [B][N][To][3]
+};
+
+__global__ __launch_bounds__(256) void gather_batch_kernel(GatherArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x, N = a.N;
+  const int s = a.idx[b];
+  const float* L = a.loc + (size_t)s * a.Tf * N * 3;
+  const float* V = a.vel + (size_t)s * a.Tf * N * 3;
+  const float* q = a.q + (size_t)s * N;
+  const int f0 = a.frame0[b];
+  for (int k = tid; k < N * 3; k += 256) {
+    a.loc0[(size_t)b * N * 3 + k] = L[(size_t)f0 * N * 3 + k];
+    a.vel0[(size_t)b * N * 3 + k] = V[(size_t)f0 * N * 3 + k];
+  }
+  for (int n = tid; n < N; n += 256) a.q_out[(size_t)b * N + n] = q[n];
+  const int Nm1 = N - 1;
+  for (int k = tid; k < N * Nm1; k += 256)
+    a.edge_attr[(size_t)b * N * Nm1 + k] = a.ea_src[(size_t)s * N * Nm1 + k];
+  // loc_true[b][n][t][d] = loc[s][out_idx[b][t]][n][d]  (locs_out = loc[out_indices].transpose(1, 0))
+  const int* oi = a.out_idx + (size_t)b * a.To;
+  for (int k = tid; k < N * a.To * 3; k += 256) {
+    const int d = k % 3, t = (k / 3) % a.To, n = k / (3 * a.To);
+    a.loc_true[(size_t)b * N * a.To * 3 + k] = L[((size_t)oi[t] * N + n) * 3 + d];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int nonode_gather_batch(int S, int Tf, int N, int B, int To, const float* loc, const float* vel, const float* charges,
+                        const float* edge_attr_src, const int* idx, const int* frame0, const int* out_idx, float* loc0, float* vel0,
+                        float* charges_out, float* edge_attr, float* loc_true, void* stream) {
+  if (S <= 0 || Tf <= 0 || N < 2 || B <= 0 || To < 0)
+    return fail(NONODE_EINVAL, "gather_batch: S=%d Tf=%d N=%d B=%d To=%d", S, Tf, N, B, To);
+  if (!loc || !vel || !charges || !edge_attr_src || !idx || !frame0 || (To > 0 && (!out_idx || !loc_true)) || !loc0 || !vel0 ||
+      !charges_out || !edge_attr)
+    return fail(NONODE_EINVAL, "gather_batch: null pointer");
+  GatherArgs a{S, Tf, N, To, loc, vel, charges, edge_attr_src, idx, frame0, out_idx, loc0, vel0, charges_out, edge_attr, loc_true};
+  hipLaunchKernelGGL(gather_batch_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
+  return check_launch("gather_batch_kernel");
+}
+
+}  // extern "C"

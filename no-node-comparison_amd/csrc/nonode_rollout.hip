@@ -110,6 +110,41 @@ __global__ void shift_tout_kernel(int Bt, int T, int total, int seg, const float
   tt[i] = t_all[(size_t)b * total + seg * T + t] - (float)(seg * T);
 }
 
+
+// Rollout metrics per (frame t, graph b) over the graph's N*3 coordinates, one
+// wave each, f64 sums: Pearson correlation of prediction vs truth (pearson_correlation_batch,
+// utils.py:261-321: centred by the per-(b, t) means, cov / (|x - mx| |y - my|)) and the summed
+// squared error (the per-horizon loss criterion(loc_pred, loc_true).mean((0, 1, 3)),
+// main_simulation_simple_no.py:273). pred, truth [T][B*N][3].
+__global__ __launch_bounds__(256) void rollout_metrics_kernel(int T, int B, int N, const float* pred,
+                                                              const float* truth, float* corr, float* sqerr) {
+  const int lane = threadIdx.x & 63;
+  const long long job = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (job >= (long long)T * B) return;
+  const int t = (int)(job / B), b = (int)(job - (long long)t * B);
+  const size_t base = ((size_t)t * B * N + (size_t)b * N) * 3;
+  const int M = N * 3;
+  double sx = 0.0, sy = 0.0;
+  for (int k = lane; k < M; k += 64) { sx += pred[base + k]; sy += truth[base + k]; }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) { sx += __shfl_xor(sx, o); sy += __shfl_xor(sy, o); }
+  const float mx = (float)(sx / M), my = (float)(sy / M);
+  double cxy = 0.0, cxx = 0.0, cyy = 0.0, se = 0.0;
+  for (int k = lane; k < M; k += 64) {
+    const double a = (double)(pred[base + k] - mx), c = (double)(truth[base + k] - my);
+    const double d = (double)pred[base + k] - (double)truth[base + k];
+    cxy += a * c; cxx += a * a; cyy += c * c; se += d * d;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    cxy += __shfl_xor(cxy, o); cxx += __shfl_xor(cxx, o); cyy += __shfl_xor(cyy, o); se += __shfl_xor(se, o);
+  }
+  if (lane == 0) {
+    if (corr) corr[(size_t)b * T + t] = (float)(cxy / (sqrt(cxx) * sqrt(cyy)));
+    if (sqerr) sqerr[(size_t)t * B + b] = (float)se;
+  }
+}
+
 int launch_featurize(const FeatArgs& a, hipStream_t s) {
   if (a.N < 2 || a.N > FEAT_NMAX) return fail(NONODE_EUNSUPPORTED, "featurize: N=%d", a.N);
   hipLaunchKernelGGL(featurize_kernel, dim3(a.B), dim3(256), 0, s, a);
@@ -266,6 +301,16 @@ int nonode_segno_rollout(int B, int N, int in_node, int n_edge_feat, int traj_le
     }
   }
   return NONODE_OK;
+}
+
+int nonode_rollout_metrics(int T, int B, int N, const float* pred, const float* truth, float* corr, float* sqerr,
+                           void* stream) {
+  if (T <= 0 || B <= 0 || N <= 0) return fail(NONODE_EINVAL, "rollout_metrics: T=%d B=%d N=%d", T, B, N);
+  if (!pred || !truth || (!corr && !sqerr)) return fail(NONODE_EINVAL, "rollout_metrics: null pointer");
+  const long long jobs = (long long)T * B;
+  hipLaunchKernelGGL(rollout_metrics_kernel, dim3((unsigned)((jobs + 3) / 4)), dim3(256), 0, (hipStream_t)stream, T,
+                     B, N, pred, truth, corr, sqerr);
+  return check_launch("rollout_metrics_kernel");
 }
 
 }  // extern "C"

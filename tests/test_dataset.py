@@ -1,0 +1,37 @@
+"""The .npy dataset path against what the REFERENCE loader returns for the same
+files (tests/golden/dataset_items.npz, recorded by make_golden_dataset.py from
+EGNO/simulation/dataset_simple.py). CPU part here; the device batches are in test_gpu_dataset."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import no_node_comparison_amd as pkg  # noqa: F401
+from no_node_comparison_amd.dataset import NBodyDynamicsDataset
+from tests.conftest import GOLDEN, load_golden
+
+TINY = os.path.join(GOLDEN, "nbody_tiny")
+
+
+@pytest.mark.parametrize("dataset", ["charged", "gravity"])
+def test_items_equal_reference_loader(dataset):
+    g = load_golden("dataset_items")
+    ds = NBodyDynamicsDataset("train", data_dir=TINY, dataset=dataset, dataset_name="nbody_small", n_balls=5,
+                              num_timesteps=10)
+    assert len(ds) == int(g[f"{dataset}::len"])
+    for i in range(len(ds)):
+        got = ds[i]
+        for k, v in zip(("loc", "vel", "edge_attr", "charges", "locs_out", "frame_0", "out_indices"), got):
+            want = g[f"{dataset}::{i}::{k}"]
+            v = v.numpy() if torch.is_tensor(v) else np.asarray(v)
+            assert v.shape == want.shape and np.array_equal(v, want), (dataset, i, k)
+
+
+def test_max_samples_and_edges():
+    ds = NBodyDynamicsDataset("train", data_dir=TINY, dataset="charged", n_balls=5, max_samples=3)
+    assert len(ds) == 3 and ds.get_n_nodes() == 49
+    r, c = ds.get_edges(2, 5)
+    assert r.numel() == 2 * 20 and int(r[20]) == 5 and int(c[0]) == 1
+    with pytest.raises(NotImplementedError):
+        NBodyDynamicsDataset("train", data_dir=TINY, dataset="charged", n_balls=5, num_inputs=2)
