@@ -24,6 +24,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "N-body trajectories/s (B×T, N=20 rollout) + pos-MSE vs ref, 1/2/4/8 MI355X"
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = f32-input MFMA peak (spec)
+FP16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (spec)
+# The layer kernel delivers fp32-accurate 64x64 products as fp16x3 split MFMAs (W_lo x_hi + W_hi x_lo +
+# W_hi x_hi): three dense fp16 MFMAs per fp32 product, so the matrix-core ceiling
+# for its algorithmic (fp32-equivalent) FLOPs is the dense fp16 peak / 3.
+FP16X3_PEAK_TFLOPS = FP16_PEAK_TFLOPS / 3.0
 HBM_PEAK_GBS = 8000.0
 
 # Algorithmic work of one egnn_layer_kernel launch (SURVEY §8d decomposed count):
@@ -166,7 +171,9 @@ def run_egno(args, world, rank, dev):
         flop = 2.0 * (E * MAC_PER_EDGE + n * MAC_PER_NODE)
         achieved = flop / (avg_ms * 1e-3) / 1e12
         res["roofline"] = {"kernel": "egnn_layer_kernel<EGNO>", "bound": "mfma", "achieved": achieved,
-                           "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+                           "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP16X3_PEAK_TFLOPS,
+                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
+                           "frac_of_fp32_mfma_peak": achieved / FP32_PEAK_TFLOPS,
                            "traffic": pmc_traffic("egnn_layer_kernel<EGNO>"), "avg_launch_ms": avg_ms,
                            "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(durs),
                            "tconv_avg_launch_ms": float(np.mean(tconv_ms)) if tconv_ms else None}
@@ -261,7 +268,9 @@ def run_segno(args, world, rank, dev, gravity=False):
         flop = 2.0 * (E * MAC_PER_EDGE_SEGNO + n * MAC_PER_NODE_SEGNO)
         ach = flop / (avg * 1e-3) / 1e12
         res["roofline"] = {"kernel": "egnn_layer_kernel<SEGNO> (fused substeps)", "bound": "mfma",
-                           "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP32_PEAK_TFLOPS,
+                           "achieved": ach, "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
+                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
+                           "frac_of_fp32_mfma_peak": ach / FP32_PEAK_TFLOPS,
                            "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
                            "launches_timed": len(layer)}
     return res
@@ -315,6 +324,170 @@ def run_egno_train(args, world, rank, dev):
                        "parallelism": f"data-parallel x{world}, one RCCL all-reduce per step"}}
 
 
+def _host_cores():
+    try:
+        import threadpoolctl
+        return max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
+    except Exception:
+        return os.cpu_count() or 1
+
+
+def run_egno_rollout(args, world, rank, dev):
+    """rollout_fn (main_simulation_simple_no.py:342-384) at the C2 shape, traj_len =
+    10 segments (the script's --traj_len default, :79) with per-frame charged energies, as ONE
+    native call (nonode_egno_rollout: 10 forwards + on-device re-featurisation + energy). A
+    trajectory is one 100-frame rollout of one sample."""
+    import no_node_comparison_amd as pkg
+    from no_node_comparison_amd import _lib
+    from no_node_comparison_amd.sharding import max_over_ranks
+    B, N, T, L = args.batch, 20, 10, 10
+    torch.manual_seed(0)
+    model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                     num_timesteps=T, time_emb_dim=32, device=dev).eval()
+    loc, vel, q = rank_batch(B, world, rank, N, 1234)
+    edges = pkg.harness.get_edges(B, N, dev)
+    loc, vel, q = loc.to(dev), vel.to(dev), q.to(dev)
+    qq = q.reshape(-1, 1)
+    eao = qq[edges[0]] * qq[edges[1]]
+    x, v, ea, nodes, lm = pkg.harness.prepare_inputs(loc, vel, eao, edges, N, 1, q)
+    t_all = torch.arange(1, T * L + 1, device=dev, dtype=torch.float32).repeat(B, 1)
+    call = lambda: pkg.harness.egno_rollout(model, nodes, x, edges, v, eao, ea, lm, N, L, B,  # noqa: E731
+                                            charges=q.reshape(-1), num_steps=T, timesteps_out=t_all,
+                                            energy_dataset="charged")
+    for _ in range(args.warmup):
+        out = call()
+    barrier_sync(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = call()
+    barrier_sync(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    records = []
+    if args.kernel_events:
+        _lib.profile_begin(16 * L * 2 + 64)
+        out = call()
+        records = _lib.profile_end()
+    value = B * world * args.steps / el
+    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d, seeded)",
+           "frames_per_s": value * T * L,
+           "config": {"workload": f"f1: EGNO rollout_fn, charged N=20, T=10, traj_len={L} (100 frames + per-frame "
+                                  f"energy), B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world,
+                      "n_balls": N, "num_timesteps": T, "traj_len": L,
+                      "parallelism": f"batch-sharded replicas x{world} (no collective)"}}
+    layer = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
+    if layer:
+        avg = float(np.mean(layer))
+        flop = 2.0 * (T * B * N * (N - 1) * MAC_PER_EDGE + T * B * N * MAC_PER_NODE)
+        ach = flop / (avg * 1e-3) / 1e12
+        res["roofline"] = {"kernel": "egnn_layer_kernel<EGNO>", "bound": "mfma", "achieved": ach,
+                           "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
+                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
+                           "frac_of_fp32_mfma_peak": ach / FP32_PEAK_TFLOPS,
+                           "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
+                           "launches_timed": len(layer),
+                           "layer_kernel_share": float(np.sum(layer)) / (el / args.steps * 1e3)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import harness as oh
+        p = {k: t.detach().cpu().numpy() for k, t in model.state_dict().items()}
+        Bc = 8
+        r, c = oh.full_edges(Bc, N)
+        cut = lambda t, w: t[: Bc * w].detach().cpu().numpy()  # noqa: E731
+        t_c = t_all[:Bc].cpu().numpy()
+        done, t0 = 0, time.perf_counter()
+        while True:
+            ref, _, _ = oh.egno_rollout(p, cut(nodes, N), cut(x, N), r, c, cut(v, N), cut(eao, N * (N - 1)),
+                                        cut(ea, N * (N - 1)), cut(lm, N), N, L, Bc, cut(q.reshape(-1), N), T=T,
+                                        t_out=t_c)
+            done += 1
+            if time.perf_counter() - t0 > 10.0 or done >= 5:
+                break
+        cel = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": Bc * done / cel, "unit": "trajectories/s", "cores": int(_host_cores()),
+                               "kind": "port", "sample": f"oracle/harness.py egno_rollout (numpy fp32 + f64 energy), "
+                               f"B={Bc} of the same batch, traj_len={L}, {done} calls in {cel:.1f} s"}
+        got = out[0][:T].reshape(T, B, N, 3)[:, :Bc].reshape(-1, 3).double().cpu().numpy()
+        want = ref[:T]
+        res["parity"] = {"first_segment_pos_maxnorm_rel_vs_oracle": float(np.abs(got - want.reshape(-1, 3)).max()
+                                                                           / np.abs(want).max()),
+                         "samples_checked": Bc}
+    return res
+
+
+# ChargedParticlesSim (synthetic_sim.py:244-260) per ordered pair and step, float64, as the kernel
+# evaluates it: x_i.x_j (5), |x_i|^2 + |x_j|^2 - 2 x_i.x_j (3), s q_i q_j / (l2 sqrt(l2)) (5),
+# F += fs (x_i - x_j) (9)
+FLOP_PER_PAIR_CHARGED = 22
+FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, AMD spec (not in the microarch guide)
+
+
+def run_sim_charged(args, world, rank, dev):
+    """ChargedParticlesSim.sample_trajectory (synthetic_sim.py:220-296) as
+    generate_dataset.py's documented charged N=20 run (its header, :10: --length 20000,
+    --sample-freq 100; 3000 training simulations): S trajectories integrated in one launch from
+    initial states already in HBM. A trajectory is one 20000-step simulation (199 saved frames)."""
+    import no_node_comparison_amd as pkg
+    from no_node_comparison_amd import _lib
+    from no_node_comparison_amd.sharding import max_over_ranks, shard_range
+    S = args.batch if args.batch != 512 else 3000
+    N, Tn, freq = 20, 20000, 100
+    sim = pkg.sim.ChargedParticlesSim(n_balls=N, vel_norm=0.5)
+    np.random.seed(43 + rank)
+    draws = [sim._draw(Tn // freq - 1, [0.5, 0.0, 0.5]) for _ in range(S)]
+    q = torch.tensor(np.stack([d[0] for d in draws]).reshape(S, N), dtype=torch.float64, device=dev)
+    l0 = torch.tensor(np.stack([d[1] for d in draws]), dtype=torch.float64, device=dev)
+    v0 = torch.tensor(np.stack([d[2] for d in draws]), dtype=torch.float64, device=dev)
+    call = lambda: sim.integrate(q, l0, v0, Tn, freq)  # noqa: E731
+    for _ in range(args.warmup):
+        out = call()
+    barrier_sync(world, dev)
+    if args.kernel_events:
+        _lib.profile_begin(args.steps + 8)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = call()
+    barrier_sync(world, dev)
+    el = time.perf_counter() - t0
+    records = _lib.profile_end() if args.kernel_events else []
+    el = max_over_ranks(el, dev)
+    value = S * world * args.steps / el
+    res = {"metric": "simulated N-body trajectories/s (charged, N=20, 20000 leapfrog steps)", "value": value,
+           "unit": "trajectories/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic initial states (the reference's draws, np seed 43 + rank)",
+           "config": {"workload": f"f3: ChargedParticlesSim N={N}, length {Tn}, sample_freq {freq}, S={S} per GPU",
+                      "sims_per_gpu": S, "n_balls": N, "length": Tn, "sample_freq": freq,
+                      "parallelism": f"independent simulations x{world}"}}
+    sims = [ms for kind, ms in records if kind == _lib.PROF_SIM_CHARGED]
+    if sims:
+        avg = float(np.mean(sims))
+        flop = float(FLOP_PER_PAIR_CHARGED) * S * N * (N - 1) * Tn
+        ach = flop / (avg * 1e-3) / 1e12
+        res["roofline"] = {"kernel": "sim_charged_kernel", "bound": "valu_fp64", "achieved": ach,
+                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
+                           "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
+                           "launches_timed": len(sims)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import sim as osim
+        done, t0 = 0, time.perf_counter()
+        while True:
+            qi, li, vi = draws[done]
+            L_ref, _ = osim.charged_trajectory(li, vi, qi, Tn, freq)
+            done += 1
+            if time.perf_counter() - t0 > 10.0 or done >= min(S, 20):
+                break
+        cel = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": done / cel, "unit": "trajectories/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/sim.py charged_trajectory (numpy f64, per simulation like the "
+                               f"reference), {done} of the same simulations in {cel:.1f} s"}
+        got = out[0][done - 1].cpu().numpy()
+        k = 10    # the first 10 saved frames (1000 steps): chaotic divergence grows after that
+        res["parity"] = {"first_frames_maxabs_vs_oracle": float(np.abs(got[:k] - L_ref[:k]).max()),
+                         "frames_checked": k}
+    return res
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -331,8 +504,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=512, help="samples per GPU")
-    ap.add_argument("--workload", default="egno", choices=["egno", "segno", "segno_gravity", "egno_train"],
-                    help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4")
+    ap.add_argument("--workload", default="egno",
+                    choices=["egno", "segno", "segno_gravity", "egno_train", "egno_rollout", "sim_charged"],
+                    help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4; "
+                         "egno_rollout = SURVEY row f1; sim_charged = row f3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", dest="kernel_events", action="store_false")
     args = ap.parse_args()
@@ -343,6 +518,10 @@ def main():
         res = run_egno(args, world, rank, dev)
     elif args.workload == "egno_train":
         res = run_egno_train(args, world, rank, dev)
+    elif args.workload == "egno_rollout":
+        res = run_egno_rollout(args, world, rank, dev)
+    elif args.workload == "sim_charged":
+        res = run_sim_charged(args, world, rank, dev)
     else:
         res = run_segno(args, world, rank, dev, gravity=args.workload == "segno_gravity")
     if rank == 0:

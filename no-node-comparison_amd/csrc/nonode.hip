@@ -110,6 +110,10 @@ struct ProfState {
   int* kind = nullptr;
 } g_prof;
 
+// record kinds: 0 / 1 egnn_layer_kernel<EGNO / SEGNO>, 2 / 3 tconv_kernel (later / first layer),
+// 4 / 5 sim_charged_kernel / sim_gravity_kernel
+constexpr int PROF_SIM_CHARGED = 4, PROF_SIM_GRAVITY = 5;
+
 struct ProfScope {
   int slot = -1;
   hipStream_t s;

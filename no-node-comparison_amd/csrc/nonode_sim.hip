@@ -191,6 +191,7 @@ int nonode_sim_charged(int S, int N, int T, int sample_freq, double dt, double m
   const int G = sim_group(N);
   SimChargedArgs a{S, G, N, T, sample_freq, T / sample_freq - 1, dt, max_F, strength, loc0, vel0, charges, loc_out,
                    vel_out};
+  ProfScope prof(PROF_SIM_CHARGED, (hipStream_t)stream);
   hipLaunchKernelGGL(sim_charged_kernel, dim3((S + G - 1) / G), dim3(sim_block(N)), 0, (hipStream_t)stream, a);
   return check_launch("sim_charged_kernel");
 }
@@ -205,6 +206,7 @@ int nonode_sim_gravity(int S, int N, int T, int sample_freq, double dt, double G
   const int Gs = sim_group(N);
   SimGravityArgs a{S, Gs, N, T, sample_freq, T / sample_freq, dt, G, softening * softening, pos0, vel0, mass,
                    pos_out, vel_out, force_out};
+  ProfScope prof(PROF_SIM_GRAVITY, (hipStream_t)stream);
   hipLaunchKernelGGL(sim_gravity_kernel, dim3((S + Gs - 1) / Gs), dim3(sim_block(N)), 0, (hipStream_t)stream, a);
   return check_launch("sim_gravity_kernel");
 }

@@ -75,12 +75,8 @@ class ChargedParticlesSim:
         q, l0, v0 = np.stack(q), np.stack(l0), np.stack(v0)
         dev = torch.device(device) if device is not None else _default_device()
         _lib.require_device(torch.empty(0, device=dev))
-        loc_d = torch.empty(S, T_save, 3, n, dtype=torch.float64, device=dev)
-        vel_d = torch.empty_like(loc_d)
         ql, ld, vd = _dev_f64(q.reshape(S, n), dev), _dev_f64(l0, dev), _dev_f64(v0, dev)
-        _lib.check(_lib.lib().nonode_sim_charged(S, n, T, sample_freq, self._delta_T, self._max_F,
-                                                 float(self.interaction_strength), _lib.ptr(ld), _lib.ptr(vd),
-                                                 _lib.ptr(ql), _lib.ptr(loc_d), _lib.ptr(vel_d), _lib.stream_of(ld)))
+        loc_d, vel_d = self.integrate(ql, ld, vd, T, sample_freq)
         if self.noise_var:
             loc_d += _dev_f64(np.stack([a for a, _ in noise]), dev) * self.noise_var
             vel_d += _dev_f64(np.stack([b for _, b in noise]), dev) * self.noise_var
@@ -88,6 +84,20 @@ class ChargedParticlesSim:
         if not as_numpy:
             return loc_d, vel_d, edges, q
         return loc_d.cpu().numpy(), vel_d.cpu().numpy(), edges, q
+
+    def integrate(self, q, loc0, vel0, T, sample_freq):
+        """The time integration of synthetic_sim.py:241-296 for S trajectories already on the GPU:
+        q [S, N], loc0 / vel0 [S, 3, N] float64 (after _clamp) -> loc, vel [S, T_save, 3, N], one
+        launch."""
+        _lib.require_device(q, loc0, vel0)
+        S, n = q.shape
+        T_save = T // sample_freq - 1
+        loc_d = torch.empty(S, T_save, 3, n, dtype=torch.float64, device=q.device)
+        vel_d = torch.empty_like(loc_d)
+        _lib.check(_lib.lib().nonode_sim_charged(S, n, T, sample_freq, self._delta_T, self._max_F,
+                                                 float(self.interaction_strength), _lib.ptr(loc0), _lib.ptr(vel0),
+                                                 _lib.ptr(q), _lib.ptr(loc_d), _lib.ptr(vel_d), _lib.stream_of(q)))
+        return loc_d, vel_d
 
     def sample_trajectory(self, T=10000, sample_freq=10, charge_prob=(1. / 2, 0, 1. / 2)):
         """synthetic_sim.py:220-296: loc, vel [T_save, 3, N], edges [N, N], charges [N, 1]."""
