@@ -32,6 +32,9 @@ typedef float f8 __attribute__((ext_vector_type(8)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
+#ifndef NONODE_STAGGER
+#define NONODE_STAGGER 1   // pair loop: unit B's VALU stages placed beside unit A's MFMA blocks
+#endif
 #ifndef NONODE_REG_FRAGS
 #define NONODE_REG_FRAGS 1
 #endif
@@ -356,7 +359,17 @@ __device__ __forceinline__ void load_vp(f4 (&d)[4], const float* vp, int g) {
 }
 // SiLU of the 16 ECL values, with the add / multiply as packed f32 ops (one wave per SIMD issues
 // a v_pk_* at the cost of a plain VALU op)
+#ifndef NONODE_PK_SILU
+#define NONODE_PK_SILU 1
+#endif
 __device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
+  if (!NONODE_PK_SILU) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a[mt][q] = silu(a[mt][q]);
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -704,13 +717,19 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         // pre-activation of edge (r, k): P_r + Q_s + W1[:, scalars] [|r|^2, e_rs] on MFMA
         // this lane's scalar edge inputs of unit k (feature 4*kf + g; feature 0 = |r|^2 is computed):
         // one unconditional, clamped global load per k-step, issued a pair ahead of its use
-        auto fetch_ef = [&](int k, float (&ev)[KF]) __attribute__((always_inline)) {
-          int j = n + k;
-          j = (j >= N) ? j - N : j;
-          const int jj = (j < n) ? j : j - 1;             // reference edge order (i, j != i)
-          const float* efp = p.ef + (ebase + jj) * p.ne;
+        // sender j = (n + k) mod N sits at jj = j (j < n) or j - 1 (j > n) in the reference edge order
+        // (i, j != i): jj * ne = n ne + k ne - (n + k >= N ? N ne : ne), k ne wave-uniform
+        const float* ef_seg = p.ef + ebase * p.ne;
+        int ef_lane[KF];
 #pragma unroll
-          for (int kf = 0; kf < KF; ++kf) ev[kf] = (NONODE_ABLATE && (p.debug & 8)) ? 0.5f : efp[min(max(4 * kf + g - 1, 0), p.ne - 1)];
+        for (int kf = 0; kf < KF; ++kf) ef_lane[kf] = n * p.ne + min(max(4 * kf + g - 1, 0), p.ne - 1);
+        const int ne_wrap = N * p.ne;
+        auto fetch_ef = [&](int k, float (&ev)[KF]) __attribute__((always_inline)) {
+          const int sub = (n + k >= N) ? ne_wrap : p.ne;
+          const int kne = k * p.ne;
+#pragma unroll
+          for (int kf = 0; kf < KF; ++kf)
+            ev[kf] = (NONODE_ABLATE && (p.debug & 8)) ? 0.5f : ef_seg[ef_lane[kf] + kne - sub];
         };
         // pre-activation of edge (r, k): P_r + Q_s + W1[:, scalars] [|r|^2, e_rs] on MFMA
         auto head = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
@@ -825,12 +844,64 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             const h8* wc1l = wc1h + foff;
             f4 a0[4], a1[4], m0[4], m1[4];
             float r00, r01, r02, r10, r11, r12;
+            float f00, f01, f02, f10, f11, f12;
+            f4 pm[4];
+            float gmax;
+#if NONODE_STAGGER
+            // The two units run half a stage apart, so every MFMA block of one unit has the other
+            // unit's VALU stage (gathers, SiLU, fp16 split) beside it in program order:
+            //   W2(A) | head+SiLU(B) ;  W2(B) | SiLU(m_A) ;  Wc1(A) | SiLU(m_B) ;  Wc1(B) | coord(A)
+            // (one wave per SIMD has no other wave to fill the matrix-pipe shadow).
+            {
+              H16Frags fw2, fwc1;
+              head2(k, e0, a0, r00, r01, r02);
+              STAMP(0);
+              silu_ecl(a0);
+              gmax = amax_ecl(a0);
+              h8 xh0[2], xl0[2], xh1[2], xl1[2];
+              h16_split(a0, xh0, xl0);
+              load_h16frags(fw2, w2l, lane);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) m0[mt] = rB2[mt];
+              if (!RV) load_vp(m0, vB2, g);
+              mfma_h16r(m0, fw2, xh0, xl0);                       // W2(A)
+              head2(k + 1, e1, a1, r10, r11, r12);                // | head + SiLU + split (B)
+              silu_ecl(a1);
+              gmax = fmaxf(gmax, amax_ecl(a1));
+              h16_split(a1, xh1, xl1);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) m1[mt] = rB2[mt];
+              if (!RV) load_vp(m1, vB2, g);
+              mfma_h16r(m1, fw2, xh1, xl1);                       // W2(B)
+              load_h16frags(fwc1, wc1l, lane);
+              silu_ecl(m0);                                       // | SiLU + split (m_A)
+              gmax = fmaxf(gmax, amax_ecl(m0));
+              h16_split(m0, xh0, xl0);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) a0[mt] = rBC1[mt];
+              if (!RV) load_vp(a0, vBC1, g);
+              mfma_h16r(a0, fwc1, xh0, xl0);                      // Wc1(A)
+              silu_ecl(m1);                                       // | SiLU + split (m_B)
+              gmax = fmaxf(gmax, amax_ecl(m1));
+              h16_split(m1, xh1, xl1);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) {
+                pm[mt] = m0[mt] + m1[mt];
+                a1[mt] = rBC1[mt];
+              }
+              if (!RV) load_vp(a1, vBC1, g);
+              mfma_h16r(a1, fwc1, xh1, xl1);                      // Wc1(B)
+              edge_f(a0, r00, r01, r02, f00, f01, f02);           // | coord MLP (A)
+              STAMP(2);
+              edge_f(a1, r10, r11, r12, f10, f11, f12);
+            }
+#else
             head2(k, e0, a0, r00, r01, r02);
             head2(k + 1, e1, a1, r10, r11, r12);
             STAMP(0);
             silu_ecl(a0);
             silu_ecl(a1);
-            float gmax = fmaxf(amax_ecl(a0), amax_ecl(a1));
+            gmax = fmaxf(amax_ecl(a0), amax_ecl(a1));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; }
             if (!RV) { load_vp(m0, vB2, g); load_vp(m1, vB2, g); }
@@ -844,7 +915,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             silu_ecl(m0);
             silu_ecl(m1);
             gmax = fmaxf(gmax, fmaxf(amax_ecl(m0), amax_ecl(m1)));
-            f4 pm[4];
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
               pm[mt] = m0[mt] + m1[mt];
@@ -859,9 +929,9 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               mfma_h16x2(a0, a1, wc1l, mh0, ml0, mh1, ml1, lane);  // coord hidden: SiLU(Wc1 m + bc1)
             }
             STAMP(2);
-            float f00, f01, f02, f10, f11, f12;
             edge_f(a0, r00, r01, r02, f00, f01, f02);
             edge_f(a1, r10, r11, r12, f10, f11, f12);
+#endif
             if (__builtin_expect(__any(gmax > H16_LIMIT), 0)) {
               f4 x0[4], x1[4];
               exact_unit(k, e0, x0, f00, f01, f02);

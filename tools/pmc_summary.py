@@ -40,3 +40,7 @@ for k, dd in res.items():
         if c in out:
             line += f" | {c} {out[c]:.3g}"
     print(line)
+    if "-v" in sys.argv:
+        wc = out.get("SQ_WAVE_CYCLES")
+        for c in sorted(out):
+            print(f"    {c:32s} {out[c]:14.4g}" + (f"  ({out[c] / wc:.1%} of wave cycles)" if wc and c.startswith(("SQ_WAIT", "SQ_ACTIVE")) else ""))
