@@ -43,7 +43,11 @@ enum : int {
 };
 enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
 constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2
-constexpr int BBLOB_FLOATS = BOFF_SCAL + 64;
+// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the four 64x64 edge matrices: the edge
+// backward's forward recompute (W2, Wc1) and its transposed products (W2^T, Wc1^T) run fp16x3
+constexpr int BOFF_H16 = BOFF_SCAL + 64;
+enum : int { BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_COUNT };
+constexpr int BBLOB_FLOATS = BOFF_H16 + BH_COUNT * 4096;
 
 // frag of W^T: value W^T[row][col] = W[col][row0 + row] (W row stride ld)
 __device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, int row0, int d) {
@@ -53,10 +57,25 @@ __device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, 
   dst[d] = W[col * ld + row0 + row];
 }
 
+// pack_h16 of W^T: W^T[row][col] = W[col][row] (W row stride ld)
+__device__ __forceinline__ void pack_h16_t(_Float16* dst, const float* W, int d, int ld) {
+  const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s = d >> 12;
+  const int row = 16 * mo + (lane & 15);
+  const int col = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
+  const float w = W[col * ld + row];
+  const _Float16 h = (_Float16)w;
+  dst[d] = hl == 0 ? h : (_Float16)(w - (float)h);
+}
+
 __global__ void pack_bwd_kernel(PackArgs a) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
   float* B = a.blob;
+  _Float16* H = reinterpret_cast<_Float16*>(B + BOFF_H16);
   switch (blockIdx.y) {
+    case 16: pack_h16(H + BH_W2 * 8192, a.w2, d); break;
+    case 17: pack_h16(H + BH_WC1 * 8192, a.cw1, d); break;
+    case 18: pack_h16_t(H + BH_W2T * 8192, a.w2, d, 64); break;
+    case 19: pack_h16_t(H + BH_WC1T * 8192, a.cw1, d, 64); break;
     case 0: if (d < 4096) pack_frag(B + BOFF_WA, a.w1, a.ld1, a.colA, 4, d, 1.f); break;
     case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
     case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
@@ -124,6 +143,66 @@ __device__ __forceinline__ void mul_dsilu(f4 (&gz)[4], const f4 (&z)[4]) {
 __device__ __forceinline__ void zero4(f4 (&a)[4]) {
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) a[mt] = f4{0.f, 0.f, 0.f, 0.f};
+}
+// a = SiLU(z) keeping the sigmoid s for the reverse pass (one exp + one rcp per value, not two)
+__device__ __forceinline__ void silu_keep(const f4 (&z)[4], f4 (&s)[4], f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s[mt][q] = sigm(z[mt][q]);
+      a[mt][q] = z[mt][q] * s[mt][q];
+    }
+}
+// g *= silu'(z) from the kept sigmoid
+__device__ __forceinline__ void mul_dsilu_s(f4 (&gz)[4], const f4 (&z)[4], const f4 (&s)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gz[mt][q] *= s[mt][q] * fmaf(z[mt][q], 1.f - s[mt][q], 1.f);
+}
+
+// ---- fp16x3 products of the edge backward ----------------------------------------------------
+// Activations are O(1) and take the forward's fp16x3 split (guarded by H16_LIMIT). Gradients have
+// no fixed scale (they carry the loss normalisation, ~1e-7 here), so they are scaled by powers of
+// two before the split: exact, and it keeps hi and lo out of the fp16 subnormal range.
+// 2^(12 - e) for m = f 2^e (f in [0.5, 1)): m times it lies in [2^11, 2^12)
+__device__ __forceinline__ float p2scale(float m) {
+  int ex = __builtin_amdgcn_frexp_expf(m);
+  ex = ex < -100 ? -100 : (ex > 100 ? 100 : ex);
+  return __builtin_ldexpf(1.f, 12 - ex);
+}
+// max over the 4 lane groups (the 64 channels of column e)
+__device__ __forceinline__ float col_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// out += W x for a gradient column set x: each column scaled to [2^11, 2^12) before the split, the
+// product scaled back (per lane: lane (e, g) holds column e)
+__device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane) {
+  const float sc = p2scale(col_max(amax_ecl(x)));
+  const float inv = 1.f / sc;   // exact (power of two)
+  f4 xs[4], acc[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { xs[mt] = x[mt] * sc; acc[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
+  h8 xh[2], xl[2];
+  h16_split(xs, xh, xl);
+  mfma_h16(acc, wh, xh, xl, lane);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) out[mt] += acc[mt] * inv;
+}
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void h4_split(f4 v, h4& hi, h4& lo) {
+  hi = __builtin_convertvector(v, h4);
+  const auto hw = __builtin_bit_cast(u2, hi);
+  const f4 r = {resid_lo(hw[0], v[0]), resid_hi(hw[0], v[1]), resid_lo(hw[1], v[2]), resid_hi(hw[1], v[3])};
+  lo = __builtin_convertvector(r, h4);
+}
+__device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
 }
 
 // ---- training-forward helpers -----------------------------------------------------------------
@@ -290,37 +369,84 @@ struct EdgeBwdArgs {
 // read-add-write (the 16 receivers and the 16 senders of one unit are distinct, and one wave's
 // units run in order), and the four tables are added at the end of the chunk: LDS float atomics
 // (ds_add_f32, 38 per unit) had cost more than the whole rest of the pass.
+constexpr int EB_VSTAGE = BOFF_SCAL + 64 - BOFF_FEAT;   // feature k-steps + vectors + scalars
+constexpr int EB_HSTAGE = 2 * 4096;   // + EB_VSTAGE in PASS 0 (PASS 1 at ct = 1 has no room)
 size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
   const int s_max = ((16 * ct - 1) / N + 2) * N;
   if (s_max_out) *s_max_out = s_max;
   // sP, sGM [ct*16][ROWP]; sQ [s_max][ROWP]; sX [s_max][4]; sGF [ct*16][4]; 4 x tile;
   // PASS 1: 4 x (sGA [ct*16][ROWP], sGB [s_max][ROWP], sGX [s_max][4])
-  return (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
+  // + two 64x64 fp16 hi/lo fragment sets staged once (EB_HSTAGE floats)
+  return EB_HSTAGE + (pass ? 0 : EB_VSTAGE) + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
          4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (size_t)s_max * (ROWP + 4)) : 0);
 }
 
 // acc[ot][it] += sum over the unit's 16 edges of G[e][16 ot + .] (x) A[e][16 it + .]; lane (e, g)
 // of acc[ot][it][q] holds dW[16 ot + 4 g + q][16 it + e]. bsum[t] += G summed over the lane's four
 // edges 4g..4g+3 at channel 16 t + e (the bias gradient, finished by group_sum).
-__device__ __forceinline__ void wgrad_unit(f4 (&acc)[4][4], float (&bsum)[4], const f4 (&G)[4], const f4 (&A)[4],
-                                           float* tile, int g, int e) {
+// fp16x3 on v_mfma_f32_16x16x16_f16 (K = the unit's 16 edges: lane (e', g) supplies edges
+// 4g .. 4g+3 of channel 16 t + e' after the LDS transpose). acc and bsum are kept in
+// units of 1/sc: sc is a wave-uniform running power-of-two scale for G, lowered (and acc, bsum
+// rescaled, exactly) when a unit's G is larger than any before it, so G sc stays below 2^12.
+// exact: A beyond the fp16 range (a diverged rollout) -> the f32 MFMA form for this unit.
+__device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], float& sc, const f4 (&G)[4],
+                                          const f4 (&A)[4], float* tile, int g, int e, bool exact) {
+  float m = col_max(amax_ecl(G));
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const float mu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m)));
+  if (mu > 0.f) {
+    const float su = p2scale(mu);
+    if (su < sc) {
+      const float r = su / sc;
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot) {
+        bsum[ot] *= r;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) acc[ot][it] *= r;
+      }
+      sc = su;
+    }
+  }
   float* tG = tile;
   float* tA = tile + 16 * ROWT;
-  store_ecl(tG + e * ROWT, G, g);
+  f4 Gs[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) Gs[mt] = G[mt] * sc;
+  store_ecl(tG + e * ROWT, Gs, g);
   store_ecl(tA + e * ROWT, A, g);
-  __builtin_amdgcn_wave_barrier();   // one wave writes and reads its own tile: LDS keeps wave order
+  __builtin_amdgcn_wave_barrier();
+  float gv[4][4], av[4][4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const int row = (4 * g + ks) * ROWT + e;
-    float gv[4], av[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) { gv[t] = tG[row + 16 * t]; av[t] = tA[row + 16 * t]; bsum[t] += gv[t]; }
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
-#pragma unroll
-      for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ot], av[it], acc[ot][it]);
+    for (int t = 0; t < 4; ++t) { gv[ks][t] = tG[row + 16 * t]; av[ks][t] = tA[row + 16 * t]; bsum[t] += gv[ks][t]; }
   }
   __builtin_amdgcn_wave_barrier();
+  if (__builtin_expect(exact, 0)) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+        for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ks][ot], av[ks][it], acc[ot][it]);
+    return;
+  }
+  h4 gh[4], gl[4], ah[4], al[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    h4_split(f4{gv[0][t], gv[1][t], gv[2][t], gv[3][t]}, gh[t], gl[t]);
+    h4_split(f4{av[0][t], av[1][t], av[2][t], av[3][t]}, ah[t], al[t]);
+  }
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      acc[ot][it] = mfma16k16(gl[ot], ah[it], acc[ot][it]);
+      acc[ot][it] = mfma16k16(gh[ot], al[it], acc[ot][it]);
+      acc[ot][it] = mfma16k16(gh[ot], ah[it], acc[ot][it]);
+    }
 }
 
 // acc[ot] += sum over the unit's edges of G[e][16 ot + .] (x) fe[e][.]: lane (e, g) of acc[ot][q]
@@ -372,7 +498,9 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
   const int rows = p.ct * 16;
-  float* sP = smem;
+  // LDS-staged fragments: PASS 0 the forward W2, Wc1 (used twice per unit there), PASS 1 W2^T, Wc1^T
+  float* sH = smem;
+  float* sP = smem + EB_HSTAGE + (PASS ? 0 : EB_VSTAGE);
   float* sGM = sP + rows * ROWP;
   float* sQ = sGM + rows * ROWP;
   float* sX = sQ + p.s_max * ROWP;
@@ -388,8 +516,19 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   const float bc2 = bb[BOFF_SCAL + 0];
   const float* wW2 = bb + BOFF_W2;
   const float* wWc1 = bb + BOFF_WC1;
-  const float* wWc1T = bb + BOFF_WC1T;
-  const float* wW2T = bb + BOFF_W2T;
+  {
+    const f4* src = reinterpret_cast<const f4*>(bb + BOFF_H16 + (PASS == 0 ? BH_W2 : BH_W2T) * 4096);
+    for (int i = tid; i < 2 * 1024; i += NW * 64) reinterpret_cast<f4*>(sH)[i] = src[i];
+    const f4* vsrc = reinterpret_cast<const f4*>(bb + BOFF_FEAT);
+    if (PASS == 0)
+      for (int i = tid; i < EB_VSTAGE / 4; i += NW * 64) reinterpret_cast<f4*>(sH + 8192)[i] = vsrc[i];
+  }
+  const float* sV = PASS == 0 ? sH + 8192 : bb + BOFF_FEAT;   // bb + BOFF_FEAT .. BOFF_SCAL + 64
+  const h8* hW2 = PASS == 0 ? reinterpret_cast<const h8*>(sH) : reinterpret_cast<const h8*>(bb + BOFF_H16 + BH_W2 * 4096);
+  const h8* hWc1 = PASS == 0 ? reinterpret_cast<const h8*>(sH + 4096) : reinterpret_cast<const h8*>(bb + BOFF_H16 + BH_WC1 * 4096);
+  const h8* hW2T = reinterpret_cast<const h8*>(sH);
+  const h8* hWc1T = reinterpret_cast<const h8*>(sH + 4096);
+  float scW = 0x1p112f;   // running scale of the accW / sB sums (wgrad_h16)
   f4 accW[4][4];   // PASS 0: dWc1, PASS 1: dW2
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -495,39 +634,49 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
 #pragma unroll
       for (int kf = 0; kf < 2; ++kf) {
         if (kf * 4 < NF) {
-          const f4 wf = *reinterpret_cast<const f4*>(bb + BOFF_FEAT + kf * 256 + lane * 4);
+          const f4 wf = *reinterpret_cast<const f4*>(sV + kf * 256 + lane * 4);
 #pragma unroll
           for (int mo = 0; mo < 4; ++mo) z1[mo] = mfma(wf[mo], ev[kf], z1[mo]);
         }
       }
-      f4 a[4], z2[4], m[4], z3[4], c1[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt];
-      silu_true(a);
-      load_vp(z2, bb + BOFF_VEC + BV_B2 * 64, g);
-      mfma_dense<4>(z2, wW2, a, lane);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt];
-      silu_true(m);
-      load_vp(z3, bb + BOFF_VEC + BV_BC1 * 64, g);
-      mfma_dense<4>(z3, wWc1, m, lane);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) c1[mt] = z3[mt];
-      silu_true(c1);
-      const float c = dot_vp(c1, bb + BOFF_VEC + BV_WC2 * 64, g) + bc2;
+      // a = SiLU(z1); z2 = W2 a + b2; m = SiLU(z2); z3 = Wc1 m + bc1; c1 = SiLU(z3) (fp16x3 on the
+      // matrix cores, exact f32 MFMAs for a unit whose activations leave the fp16 range)
+      f4 sg1[4], a[4], z2[4], sg2[4], m[4], z3[4], sg3[4], c1[4];
+      silu_keep(z1, sg1, a);
+      const bool bigA = __any(amax_ecl(a) > H16_LIMIT);
+      load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
+      if (__builtin_expect(bigA, 0)) {
+        mfma_dense<4>(z2, wW2, a, lane);
+      } else {
+        h8 xh[2], xl[2];
+        h16_split(a, xh, xl);
+        mfma_h16(z2, hW2, xh, xl, lane);
+      }
+      silu_keep(z2, sg2, m);
+      const bool bigM = __any(amax_ecl(m) > H16_LIMIT);
+      load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
+      if (__builtin_expect(bigM, 0)) {
+        mfma_dense<4>(z3, wWc1, m, lane);
+      } else {
+        h8 xh[2], xl[2];
+        h16_split(m, xh, xl);
+        mfma_h16(z3, hWc1, xh, xl, lane);
+      }
+      silu_keep(z3, sg3, c1);
+      const float c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
       // reverse: f = r c
       const float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
       const float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
       float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
       // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
       f4 gz3[4];
-      load_vp(gz3, bb + BOFF_VEC + BV_WC2 * 64, g);
+      load_vp(gz3, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) gz3[mt] *= gc;
-      mul_dsilu(gz3, z3);
+      mul_dsilu_s(gz3, z3, sg3);
       // dWc1 += gz3 (x) m ; dwc2 += gc c1 ; dbc1 += gz3 ; dbc2 += gc
       if (PASS == 0) {
-        wgrad_unit(accW, sB, gz3, m, tile, g, e);
+        wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * c1[mt];
         sGC += gc;
@@ -537,18 +686,18 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       f4 gz2[4];
       load_ecl(gz2, sGM + rl * ROWP, g);
       if (!rvalid) zero4(gz2);
-      if (!(p.dbg & 32)) mfma_dense<4>(gz2, wWc1T, gz3, lane);
-      mul_dsilu(gz2, z2);                       // m = SiLU(z2)
+      if (!(p.dbg & 32)) mm64_cs(gz2, hWc1T, gz3, lane);
+      mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
       // dW2 += gz2 (x) a ; db2 += gz2
-      if (!(p.dbg & 4)) wgrad_unit(accW, sB, gz2, a, tile, g, e);
+      if (!(p.dbg & 4)) wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA);
       f4 gz1[4];
       zero4(gz1);
-      if (!(p.dbg & 64)) mfma_dense<4>(gz1, wW2T, gz2, lane);
-      mul_dsilu(gz1, z1);                       // a = SiLU(z1)
+      if (!(p.dbg & 64)) mm64_cs(gz1, hW2T, gz2, lane);
+      mul_dsilu_s(gz1, z1, sg1);                 // a = SiLU(z1)
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
       if (!(p.dbg & 8)) wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
       // s = |r|^2 input column
-      const float gs = dot_vp(gz1, bb + BOFF_VEC + BV_WS * 64, g);
+      const float gs = dot_vp(gz1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64, g);
       gr0 = fmaf(2.f * gs, r0, gr0);
       gr1 = fmaf(2.f * gs, r1, gr1);
       gr2 = fmaf(2.f * gs, r2, gr2);
@@ -602,15 +751,16 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   __syncthreads();   // the last chunk's tables are dead: reuse the LDS
   float* wp = smem + wave * EW_STRIDE;
   const int wo = PASS == 0 ? EW_WC1 : EW_W2;
+  const float inv_sc = 1.f / scW;   // exact (power of two)
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
     for (int it = 0; it < 4; ++it)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = accW[ot][it][q];
+      for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = accW[ot][it][q] * inv_sc;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const float bs = group_sum(sB[t]);
+    const float bs = group_sum(sB[t]) * inv_sc;
     if (g == 0) wp[wo + (16 * t + e) * 65 + 64] = bs;
   }
   if (PASS == 1) {
@@ -1186,7 +1336,7 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
   a.ne = n_edge_feat;
   a.blob = bblob;
-  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 16), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 20), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_bwd_kernel");
 }
 
