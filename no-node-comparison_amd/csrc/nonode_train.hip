@@ -179,6 +179,17 @@ __device__ __forceinline__ float col_max(float v) {
   const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
+// max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors; no LDS round trip)
+template <int C>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_max16(float m) {
+  m = fmaxf(m, dppf<0xB1>(m));    // quad_perm [1, 0, 3, 2]
+  m = fmaxf(m, dppf<0x4E>(m));    // quad_perm [2, 3, 0, 1]
+  m = fmaxf(m, dppf<0x141>(m));   // row_half_mirror
+  return fmaxf(m, dppf<0x140>(m));  // row_mirror
+}
 // out += W x for a gradient column set x: each column scaled to [2^11, 2^12) before the split, the
 // product scaled back (per lane: lane (e, g) holds column e)
 __device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane) {
@@ -391,9 +402,7 @@ size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
 // exact: A beyond the fp16 range (a diverged rollout) -> the f32 MFMA form for this unit.
 __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], float& sc, const f4 (&G)[4],
                                           const f4 (&A)[4], float* tile, int g, int e, bool exact) {
-  float m = col_max(amax_ecl(G));
-#pragma unroll
-  for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const float m = row_max16(col_max(amax_ecl(G)));
   const float mu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m)));
   if (mu > 0.f) {
     const float su = p2scale(mu);
@@ -416,37 +425,46 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
   store_ecl(tG + e * ROWT, Gs, g);
   store_ecl(tA + e * ROWT, A, g);
   __builtin_amdgcn_wave_barrier();
-  float gv[4][4], av[4][4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int row = (4 * g + ks) * ROWT + e;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) { gv[ks][t] = tG[row + 16 * t]; av[ks][t] = tA[row + 16 * t]; bsum[t] += gv[ks][t]; }
-  }
-  __builtin_amdgcn_wave_barrier();
   if (__builtin_expect(exact, 0)) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 4; ++ks) {
+      const int row = (4 * g + ks) * ROWT + e;
+      float gv[4], av[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { gv[t] = tG[row + 16 * t]; av[t] = tA[row + 16 * t]; bsum[t] += gv[t]; }
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
-        for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ks][ot], av[ks][it], acc[ot][it]);
+        for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ot], av[it], acc[ot][it]);
+    }
+    __builtin_amdgcn_wave_barrier();
     return;
   }
-  h4 gh[4], gl[4], ah[4], al[4];
+  // A columns once (16 VGPRs of halves), G streamed one output tile at a time
+  h4 ah[4], al[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    h4_split(f4{gv[0][t], gv[1][t], gv[2][t], gv[3][t]}, gh[t], gl[t]);
-    h4_split(f4{av[0][t], av[1][t], av[2][t], av[3][t]}, ah[t], al[t]);
+  for (int it = 0; it < 4; ++it) {
+    f4 v;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) v[ks] = tA[(4 * g + ks) * ROWT + e + 16 * it];
+    h4_split(v, ah[it], al[it]);
   }
 #pragma unroll
-  for (int ot = 0; ot < 4; ++ot)
+  for (int ot = 0; ot < 4; ++ot) {
+    f4 v;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) v[ks] = tG[(4 * g + ks) * ROWT + e + 16 * ot];
+    bsum[ot] += (v[0] + v[1]) + (v[2] + v[3]);
+    h4 gh, gl;
+    h4_split(v, gh, gl);
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
-      acc[ot][it] = mfma16k16(gl[ot], ah[it], acc[ot][it]);
-      acc[ot][it] = mfma16k16(gh[ot], al[it], acc[ot][it]);
-      acc[ot][it] = mfma16k16(gh[ot], ah[it], acc[ot][it]);
+      acc[ot][it] = mfma16k16(gl, ah[it], acc[ot][it]);
+      acc[ot][it] = mfma16k16(gh, al[it], acc[ot][it]);
+      acc[ot][it] = mfma16k16(gh, ah[it], acc[ot][it]);
     }
+  }
+  __builtin_amdgcn_wave_barrier();
 }
 
 // acc[ot] += sum over the unit's edges of G[e][16 ot + .] (x) fe[e][.]: lane (e, g) of acc[ot][q]
@@ -641,29 +659,43 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       }
       // a = SiLU(z1); z2 = W2 a + b2; m = SiLU(z2); z3 = Wc1 m + bc1; c1 = SiLU(z3) (fp16x3 on the
       // matrix cores, exact f32 MFMAs for a unit whose activations leave the fp16 range)
-      f4 sg1[4], a[4], z2[4], sg2[4], m[4], z3[4], sg3[4], c1[4];
-      silu_keep(z1, sg1, a);
-      const bool bigA = __any(amax_ecl(a) > H16_LIMIT);
-      load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
-      if (__builtin_expect(bigA, 0)) {
-        mfma_dense<4>(z2, wW2, a, lane);
-      } else {
-        h8 xh[2], xl[2];
-        h16_split(a, xh, xl);
-        mfma_h16(z2, hW2, xh, xl, lane);
+      // (a = z1 sg1 is not kept: recomputed for the dW2 gradient, which saves 16 registers)
+      f4 sg1[4], z2[4], sg2[4], z3[4], sg3[4];
+      bool bigA;
+      {
+        f4 a[4];
+        silu_keep(z1, sg1, a);
+        bigA = __any(amax_ecl(a) > H16_LIMIT);
+        load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
+        if (__builtin_expect(bigA, 0)) {
+          mfma_dense<4>(z2, wW2, a, lane);
+        } else {
+          h8 xh[2], xl[2];
+          h16_split(a, xh, xl);
+          mfma_h16(z2, hW2, xh, xl, lane);
+        }
       }
-      silu_keep(z2, sg2, m);
-      const bool bigM = __any(amax_ecl(m) > H16_LIMIT);
-      load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
-      if (__builtin_expect(bigM, 0)) {
-        mfma_dense<4>(z3, wWc1, m, lane);
-      } else {
-        h8 xh[2], xl[2];
-        h16_split(m, xh, xl);
-        mfma_h16(z3, hWc1, xh, xl, lane);
+      // (m = z2 sg2 and c1 = z3 sg3 are recomputed where needed again: register budget)
+      bool bigM;
+      {
+        f4 m[4];
+        silu_keep(z2, sg2, m);
+        bigM = __any(amax_ecl(m) > H16_LIMIT);
+        load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
+        if (__builtin_expect(bigM, 0)) {
+          mfma_dense<4>(z3, wWc1, m, lane);
+        } else {
+          h8 xh[2], xl[2];
+          h16_split(m, xh, xl);
+          mfma_h16(z3, hWc1, xh, xl, lane);
+        }
       }
-      silu_keep(z3, sg3, c1);
-      const float c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
+      float c;
+      {
+        f4 c1[4];
+        silu_keep(z3, sg3, c1);
+        c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
+      }
       // reverse: f = r c
       const float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
       const float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
@@ -676,9 +708,12 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       mul_dsilu_s(gz3, z3, sg3);
       // dWc1 += gz3 (x) m ; dwc2 += gc c1 ; dbc1 += gz3 ; dbc2 += gc
       if (PASS == 0) {
+        f4 m[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt] * sg2[mt];
         wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM);
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * c1[mt];
+        for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
         sGC += gc;
         continue;
       }
@@ -689,7 +724,12 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       if (!(p.dbg & 32)) mm64_cs(gz2, hWc1T, gz3, lane);
       mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
       // dW2 += gz2 (x) a ; db2 += gz2
-      if (!(p.dbg & 4)) wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA);
+      if (!(p.dbg & 4)) {
+        f4 a[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
+        wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA);
+      }
       f4 gz1[4];
       zero4(gz1);
       if (!(p.dbg & 64)) mm64_cs(gz1, hW2T, gz2, lane);
@@ -750,19 +790,21 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   // ---- D: weight-gradient partials: each wave's to LDS, then one per block (waves added in order) ----
   __syncthreads();   // the last chunk's tables are dead: reuse the LDS
   float* wp = smem + wave * EW_STRIDE;
-  const int wo = PASS == 0 ? EW_WC1 : EW_W2;
-  const float inv_sc = 1.f / scW;   // exact (power of two)
+  auto put = [&](const f4 (&acc)[4][4], const float (&sb)[4], float sc, int wo) {
+    const float inv_sc = 1.f / sc;   // exact (power of two)
 #pragma unroll
-  for (int ot = 0; ot < 4; ++ot)
+    for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
-    for (int it = 0; it < 4; ++it)
+      for (int it = 0; it < 4; ++it)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = accW[ot][it][q] * inv_sc;
+        for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = acc[ot][it][q] * inv_sc;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const float bs = group_sum(sB[t]) * inv_sc;
-    if (g == 0) wp[wo + (16 * t + e) * 65 + 64] = bs;
-  }
+    for (int t = 0; t < 4; ++t) {
+      const float bs = group_sum(sb[t]) * inv_sc;
+      if (g == 0) wp[wo + (16 * t + e) * 65 + 64] = bs;
+    }
+  };
+  put(accW, sB, scW, PASS == 0 ? EW_WC1 : EW_W2);
   if (PASS == 1) {
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot)
@@ -772,20 +814,21 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         if (e < NF) wp[EW_FEAT + ch * (NF + 1) + e] = accFe[ot][q];
         if (e == NF) wp[EW_FEAT + ch * (NF + 1) + NF] = 0.f;
       }
-    block_partial(smem, p.wpart + (size_t)blockIdx.x * EW_STRIDE, EW_W2, EW_WC1);
-    block_partial(smem, p.wpart + (size_t)blockIdx.x * EW_STRIDE, EW_FEAT, EW_FEAT + 64 * (NF + 1));
-    return;
   }
+  if (PASS == 0) {
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float wc2 = edge_sum16(sWC2[mt][q]);
-      if (e == 0) wp[EW_WC2 + 16 * mt + 4 * g + q] = wc2;
-    }
-  const float gcs = edge_sum16(sGC);   // every lane group holds the same gc per edge: take group 0
-  if (lane == 0) wp[EW_WC2 + 64] = gcs;
-  block_partial(smem, p.wpart + (size_t)blockIdx.x * EW_STRIDE, EW_WC1, EW_WC2 + 65);
+      for (int q = 0; q < 4; ++q) {
+        const float wc2 = edge_sum16(sWC2[mt][q]);
+        if (e == 0) wp[EW_WC2 + 16 * mt + 4 * g + q] = wc2;
+      }
+    const float gcs = edge_sum16(sGC);   // every lane group holds the same gc per edge: take group 0
+    if (lane == 0) wp[EW_WC2 + 64] = gcs;
+  }
+  float* dst = p.wpart + (size_t)blockIdx.x * EW_STRIDE;
+  block_partial(smem, dst, PASS == 0 ? EW_WC1 : EW_W2, PASS == 1 ? EW_WC1 : EW_WC2 + 65);
+  if (PASS == 1) block_partial(smem, dst, EW_FEAT, EW_FEAT + 64 * (NF + 1));
 }
 // per-pass chunk size (tiles per LDS chunk) and dynamic LDS bytes
 int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_max_out, size_t* lds_out) {
