@@ -32,8 +32,10 @@ typedef float f8 __attribute__((ext_vector_type(8)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
+// Pair loop with unit B's VALU stages placed beside unit A's MFMA blocks: 1 = SEGNO only (there
+// it fits the register file; for EGNO it spills and slows the guard path), 2 = both
 #ifndef NONODE_STAGGER
-#define NONODE_STAGGER 1   // pair loop: unit B's VALU stages placed beside unit A's MFMA blocks
+#define NONODE_STAGGER 1
 #endif
 #ifndef NONODE_REG_FRAGS
 #define NONODE_REG_FRAGS 1
@@ -847,7 +849,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             float f00, f01, f02, f10, f11, f12;
             f4 pm[4];
             float gmax;
-#if NONODE_STAGGER
+            if constexpr (NONODE_STAGGER == 2 || (NONODE_STAGGER == 1 && VARIANT == SEGNO)) {
             // The two units run half a stage apart, so every MFMA block of one unit has the other
             // unit's VALU stage (gathers, SiLU, fp16 split) beside it in program order:
             //   W2(A) | head+SiLU(B) ;  W2(B) | SiLU(m_A) ;  Wc1(A) | SiLU(m_B) ;  Wc1(B) | coord(A)
@@ -895,7 +897,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               STAMP(2);
               edge_f(a1, r10, r11, r12, f10, f11, f12);
             }
-#else
+            } else {
             head2(k, e0, a0, r00, r01, r02);
             head2(k + 1, e1, a1, r10, r11, r12);
             STAMP(0);
@@ -931,7 +933,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             STAMP(2);
             edge_f(a0, r00, r01, r02, f00, f01, f02);
             edge_f(a1, r10, r11, r12, f10, f11, f12);
-#endif
+            }
             if (__builtin_expect(__any(gmax > H16_LIMIT), 0)) {
               f4 x0[4], x1[4];
               exact_unit(k, e0, x0, f00, f01, f02);
