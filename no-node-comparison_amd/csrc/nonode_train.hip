@@ -1240,9 +1240,17 @@ __global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nbl
   const int NO = M * (N + 1);
   const int ol = threadIdx.x & 15, part = threadIdx.x >> 4;
   const int o = blockIdx.x * 16 + ol;
-  float s = 0.f;
-  if (o < NO)
-    for (int b = part; b < nblk; b += 16) s += partial[(size_t)b * pstride + o];
+  // eight independent partial sums per thread (a fixed tree: deterministic), so the loads of a
+  // thread are in flight together
+  float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (o < NO) {
+    int b = part;
+    for (; b + 7 * 16 < nblk; b += 8 * 16)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s8[u] += partial[(size_t)(b + 16 * u) * pstride + o];
+    for (int u = 0; b < nblk; b += 16, ++u) s8[u & 7] += partial[(size_t)b * pstride + o];
+  }
+  float s = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
   red[part][ol] = s;
   __syncthreads();
   if (part != 0 || o >= NO) return;
