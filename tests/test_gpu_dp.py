@@ -1,0 +1,82 @@
+"""Data-parallel EGNO training step on the HIP kernels (SURVEY §8 row e, C4's exchange step).
+
+Two ranks share cuda:0 (the gloo backend carries the collective, so no second GPU is needed): each
+runs the HIP training forward + backward on its half of the batch with the reference's loss
+(main_simulation_simple_no.py:273-280), every p.grad is a view into one FlatGrads buffer, and ONE
+all-reduce of that buffer (then / world) gives the step's gradients. They must equal the
+single-process whole-batch gradients of the same kernels to 1e-5 max-norm relative per tensor (the
+two runs only sum the same fp32 terms in a different order).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests.conftest import maxnorm_rel
+from tests.test_gpu_parity import _dev, _egno, _egno_case
+from tests.test_gpu_train import _loss_like_reference
+
+pytestmark = pytest.mark.gpu
+B, N, T = 8, 20, 10
+DPTOL = 1e-5
+
+
+def _inputs(lo, hi):
+    c = _egno_case(B, N, T, seed=11)
+    n0, n1 = lo * N, hi * N                       # node rows of samples lo .. hi-1
+    e0, e1 = lo * N * (N - 1), hi * N * (N - 1)   # edge rows (reference order: sample-major)
+    sub = dict(x=c["x"][n0:n1], h=c["h"][n0:n1], v=c["v"][n0:n1], loc_mean=c["loc_mean"][n0:n1],
+               edge_fea=c["edge_fea"][e0:e1], t_out=c["t_out"][lo:hi],
+               row=c["row"][e0:e1] - n0, col=c["col"][e0:e1] - n0)
+    target = np.random.default_rng(5).standard_normal((B, N, T, 3)).astype(np.float32)[lo:hi]
+    return {k: _dev(v) for k, v in sub.items()}, _dev(target)
+
+
+def _step_grads(lo, hi, allreduce):
+    from no_node_comparison_amd.sharding import FlatGrads
+    m = _egno(T=T, seed=3).train()
+    fg = FlatGrads(m.parameters())
+    inp, target = _inputs(lo, hi)
+    x, _, _ = m(inp["x"], inp["h"], [inp["row"], inp["col"]], inp["edge_fea"], v=inp["v"],
+                loc_mean=inp["loc_mean"], timesteps_out=inp["t_out"])
+    loss, _ = _loss_like_reference(x, target, T, hi - lo, N)
+    fg.zero_()
+    loss.backward()
+    if allreduce:
+        fg.allreduce_()
+    torch.cuda.synchronize()
+    return {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        per = B // world
+        g = _step_grads(rank * per, (rank + 1) * per, allreduce=True)
+        if rank == 0:
+            np.savez(out, **g)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_step_on_hip_kernels_equals_whole_batch(tmp_path):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "dp_grads.npz")
+    mp.start_processes(_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    dp = np.load(out)
+    whole = _step_grads(0, B, allreduce=False)
+    nonzero = 0
+    for k, ref in whole.items():
+        if np.abs(ref).max() == 0:   # the last layer's h update does not reach the position loss
+            assert np.abs(dp[k]).max() == 0, k
+            continue
+        nonzero += 1
+        assert maxnorm_rel(dp[k], ref) < DPTOL, (k, maxnorm_rel(dp[k], ref))
+    assert nonzero > 50
