@@ -43,7 +43,7 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
 constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
 constexpr int TMAX = 16;   // max trajectory length handled by tconv_kernel
-constexpr int MMAX = 4;    // max Fourier modes
+constexpr int MMAX = 9;    // max Fourier modes (T <= 16: at most T/2 + 1 = 9 rfft bins)
 
 // ---- packed layer blob (floats) --------------------------------------------------------------
 // Fragment matrices: W[64][I] used as the A operand of v_mfma_f32_16x16x4_f32 with the B operand
@@ -1137,10 +1137,12 @@ __global__ void tconv_pack_kernel(const float* w, int Mfull, int M, int T, float
 // One workgroup (4 waves) per tile of 16 columns (b, n). Wave w: DFT of input channels 16w..16w+15,
 // then the mixing MFMAs for output channels 16w..16w+15, then LeakyReLU + residual for those
 // channels over all T. Lanes hold (column e = lane & 15, channels 16w + 4g + q).
-template <bool FIRST>
+// MM: compile-time bound on the number of modes (M <= MM), so the mode loops, the LDS spectrum and
+// the register arrays are sized for the configuration at hand
+template <bool FIRST, int MM>
 __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
-  __shared__ __attribute__((aligned(16))) float sX[2 * MMAX - 1][16][ROWP];
-  __shared__ float sCos[MMAX * TMAX], sSin[MMAX * TMAX];
+  __shared__ __attribute__((aligned(16))) float sX[2 * MM - 1][16][ROWP];
+  __shared__ float sCos[MM * TMAX], sSin[MM * TMAX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int T = p.T, M = p.M, BN = p.BN;
   if (tid < M * T) {
@@ -1181,9 +1183,9 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
         vs[t] = p.v[row * 3 + d];
       }
     }
-    float yr[MMAX][2], yi[MMAX][2];
+    float yr[MM][2], yi[MM][2];
 #pragma unroll
-    for (int m = 0; m < MMAX; ++m) {
+    for (int m = 0; m < MM; ++m) {
       if (m < M) {
         float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f};
 #pragma unroll
@@ -1215,7 +1217,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       if (t < T) {
         float y0 = 0.f, y1 = 0.f;
 #pragma unroll
-        for (int m = 0; m < MMAX; ++m) {
+        for (int m = 0; m < MM; ++m) {
           if (m < M) {
             const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
             y0 += yr[m][0] * cs - yi[m][0] * sn;
@@ -1230,15 +1232,15 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   // ---- step 1: truncated DFT of this wave's input channels ----
   {
-    f4 Xr[MMAX], Xs[MMAX];
+    f4 Xr[MM], Xs[MM];
 #pragma unroll
-    for (int m = 0; m < MMAX; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
+    for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {
       if (t < T) {
         const f4 hv = hval(t);
 #pragma unroll
-        for (int m = 0; m < MMAX; ++m) {
+        for (int m = 0; m < MM; ++m) {
           if (m < M) {
             Xr[m] += hv * sCos[m * TMAX + t];
             if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
@@ -1248,7 +1250,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     }
     *reinterpret_cast<f4*>(&sX[0][e][ch]) = Xr[0];
 #pragma unroll
-    for (int m = 1; m < MMAX; ++m) {
+    for (int m = 1; m < MM; ++m) {
       if (m < M) {
         *reinterpret_cast<f4*>(&sX[2 * m - 1][e][ch]) = Xr[m];
         *reinterpret_cast<f4*>(&sX[2 * m][e][ch]) = Xs[m];
@@ -1257,7 +1259,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   __syncthreads();
   // ---- step 2: channel mixing on MFMA (output tile mo = wave) ----
-  f4 Yr[MMAX], Yi[MMAX];
+  f4 Yr[MM], Yi[MM];
   auto mix = [&](f4& acc, int mat, int vec) {
     f4 in[4];
     load_ecl(in, &sX[vec][e][0], g);
@@ -1272,7 +1274,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
   mix(Yr[0], 0, 0);
 #pragma unroll
-  for (int m = 1; m < MMAX; ++m) {
+  for (int m = 1; m < MM; ++m) {
     if (m < M) {
       const int mat = 1 + 3 * (m - 1);
       Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
@@ -1290,7 +1292,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       if (t < T) {
         f4 y = Yr[0];
 #pragma unroll
-        for (int m = 1; m < MMAX; ++m)
+        for (int m = 1; m < MM; ++m)
           if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
         f4 o = hval(t);
 #pragma unroll
@@ -1388,10 +1390,13 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
 int launch_tconv(bool first, const TconvArgs& a, hipStream_t stream) {
   const int grid = (a.BN + 15) / 16;
   ProfScope prof(first ? 3 : 2, stream);
-  if (first)
-    hipLaunchKernelGGL(tconv_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(tconv_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
+  auto go = [&](auto kt, auto kf) {
+    if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(256), 0, stream, a);
+    else hipLaunchKernelGGL(kf, dim3(grid), dim3(256), 0, stream, a);
+  };
+  if (a.M <= 2) go(tconv_kernel<true, 2>, tconv_kernel<false, 2>);
+  else if (a.M <= 4) go(tconv_kernel<true, 4>, tconv_kernel<false, 4>);
+  else go(tconv_kernel<true, MMAX>, tconv_kernel<false, MMAX>);
   return check_launch("tconv_kernel");
 }
 

@@ -21,6 +21,8 @@
 
 namespace {
 
+constexpr int MMAX_T = 4;   // training path: at most 4 Fourier modes (tconv_bwd_kernel<MM> registers)
+
 // ---- backward weight blob (unscaled f32 fragments, forward and transposed) --------------------
 enum : int {
   BOFF_WA = 0,          // edge W1 h_i columns                 (frag layout, KT=4)
@@ -1138,8 +1140,8 @@ __global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* 
     GO[0][t] = G[0][t] = gxo[row * 3 + d];
     GO[1][t] = G[1][t] = gvo[row * 3 + d];
   }
-  float* pp = part + (size_t)idx * (2 * 2 * MMAX * 2);
-  for (int k = 0; k < 2 * 2 * MMAX * 2; ++k) pp[k] = 0.f;
+  float* pp = part + (size_t)idx * (2 * 2 * MMAX_T * 2);
+  for (int k = 0; k < 2 * 2 * MMAX_T * 2; ++k) pp[k] = 0.f;
   for (int m = 0; m < M; ++m) {
     const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
     float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f}, gYr[2] = {0.f, 0.f}, gYi[2] = {0.f, 0.f};
@@ -1157,8 +1159,8 @@ __global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* 
         const float wr = w[((i * 2 + o) * Mfull + m) * 2 + 0], wi = w[((i * 2 + o) * Mfull + m) * 2 + 1];
         gxr += gYr[o] * wr + gYi[o] * wi;
         gxi += -gYr[o] * wi + gYi[o] * wr;
-        pp[((i * 2 + o) * MMAX + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
-        pp[((i * 2 + o) * MMAX + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
+        pp[((i * 2 + o) * MMAX_T + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
+        pp[((i * 2 + o) * MMAX_T + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
       }
       for (int t = 0; t < T; ++t) {
         const double ang = 2.0 * (double)m * (double)t / (double)T;
@@ -1358,7 +1360,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.wpart = take((size_t)EB_MAX_BLOCKS * EW_STRIDE);
   w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
-  w.xpart = take(BN * 3 * 2 * 2 * MMAX * 2);
+  w.xpart = take(BN * 3 * 2 * 2 * MMAX_T * 2);
   w.partial = take((size_t)(GEMM_MAX_WAVES + 4) * 64 * 65);
   w.floats = tot;
   return w;
@@ -1403,8 +1405,9 @@ int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, in
                               float* v_out, float* h_out, void* state, size_t state_bytes, void* workspace,
                               size_t workspace_bytes, void* stream) {
   if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || in_node < 0 || in_node > 8 || modes < 1 ||
-      modes > MMAX || time_emb_dim < 4 || time_emb_dim > 64 || (time_emb_dim & 1) || Bt <= 0 || (B * N) % Bt)
-    return fail(NONODE_EUNSUPPORTED, "egno_forward_train: B=%d N=%d T=%d", B, N, T);
+      modes > MMAX_T || time_emb_dim < 4 || time_emb_dim > 64 || (time_emb_dim & 1) || Bt <= 0 || (B * N) % Bt)
+    return fail(NONODE_EUNSUPPORTED, "egno_forward_train: B=%d N=%d T=%d modes=%d (training: modes <= %d)", B, N, T,
+                modes, MMAX_T);
   if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_blobs || !tconvx_w ||
       !x_out || !v_out || !h_out || !state || !workspace)
     return fail(NONODE_EINVAL, "egno_forward_train: null pointer");
@@ -1461,7 +1464,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
                          const void* state, const float* g_x, const float* g_v, const float* g_h,
                          const nonode_layer_grads* layer_grads, float* const* g_tconv, float* const* g_tconvx,
                          float* g_emb_w, float* g_emb_b, void* workspace, size_t workspace_bytes, void* stream) {
-  if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || modes < 1 || modes > MMAX || Bt <= 0 ||
+  if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || modes < 1 || modes > MMAX_T || Bt <= 0 ||
       n_edge_feat < 0 || n_edge_feat > 4)
     return fail(NONODE_EUNSUPPORTED, "egno_backward: B=%d N=%d T=%d", B, N, T);
   if (!loc_mean || !bblobs || !tconv_w || !tconvx_w || !state || !g_x || !layer_grads || !g_tconv || !g_tconvx ||
@@ -1553,7 +1556,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
       // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M stay zero)
       hipMemsetAsync(g_tconvx[l], 0, 2 * 2 * modes * 2 * sizeof(float), s);
       float* tmp = w.partial;
-      const int cnt = 2 * 2 * MMAX * 2;
+      const int cnt = 2 * 2 * MMAX_T * 2;
       const long long rows = (long long)BN * 3, slice = 256;
       const int nb = (int)((rows + slice - 1) / slice);
       hipLaunchKernelGGL(rows_reduce, dim3(nb), dim3(256), 0, s, w.xpart, rows, cnt, slice, tmp + 64);
@@ -1561,7 +1564,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
       hipLaunchKernelGGL(rows_reduce, dim3(1), dim3(256), 0, s, tmp + 64, (long long)nb, cnt, (long long)nb, tmp);
       if (int rc = check_launch("rows_reduce")) return rc;
       for (int io = 0; io < 4; ++io)
-        hipMemcpyAsync(g_tconvx[l] + io * modes * 2, tmp + io * MMAX * 2, M * 2 * sizeof(float),
+        hipMemcpyAsync(g_tconvx[l] + io * modes * 2, tmp + io * MMAX_T * 2, M * 2 * sizeof(float),
                        hipMemcpyDeviceToDevice, s);
     }
     // ---- TimeConv reverse: h of the layer's TimeConv input ----

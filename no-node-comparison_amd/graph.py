@@ -5,9 +5,15 @@ The reference materialises int64 edge lists per batch (EGNO/simulation/dataset_s
 The kernels index that pattern implicitly, so the boundary checks once per edge tensor that the
 caller's edge_index is exactly it, and raises ValueError otherwise.
 """
+from collections import OrderedDict
+
 import torch
 
-_checked = {}
+# validated edge tensors, keyed by address / version / shape. Each entry holds a reference to its
+# tensors, so their memory cannot be freed and reused by a different edge list while the entry
+# exists (a key built from addresses alone would then match a tensor it never checked).
+_checked = OrderedDict()
+_CACHE = 8
 
 
 def full_edges(B, N, device="cpu"):
@@ -42,14 +48,16 @@ def check_full_graph(edge_index, n_nodes):
         raise ValueError(f"edge_index with {E} edges is not a fully connected batch over {n_nodes} nodes")
     B = n_nodes // N
     key = (rows.data_ptr(), cols.data_ptr(), rows._version, cols._version, E, n_nodes, str(rows.device))
-    if key in _checked:
-        return _checked[key]
+    hit = _checked.get(key)
+    if hit is not None:
+        _checked.move_to_end(key)
+        return hit[0], hit[1]
     r, c = full_edges(B, N, rows.device)
     if not (torch.equal(rows.to(torch.int64), r) and torch.equal(cols.to(torch.int64), c)):
         raise ValueError("edge_index is not the dataset's fully connected edge list "
                          "(receiver i, sender j != i, ordered by sample, i, j); the MI355X kernels "
                          "index that pattern implicitly")
-    if len(_checked) > 64:
-        _checked.clear()
-    _checked[key] = (B, N)
+    _checked[key] = (B, N, rows, cols)
+    while len(_checked) > _CACHE:
+        _checked.popitem(last=False)
     return B, N

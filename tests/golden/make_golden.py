@@ -24,6 +24,8 @@ What each fixture pins (reference file:line):
                       through forward_step (the integrator the shadowed forward intends).
   segno_gravity.npz   forward_step at N=100, B=2, T=5 on GravitySim-style inputs
                       (synthetic_sim.py:360-404).
+  egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8 (5 spectral modes incl. the
+                      Nyquist bin; model_confs.yaml:12's alternative), seed-0 weights.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
                       torch.manual_seed(0) (RNG-consumption order of the constructors).
 """
@@ -332,7 +334,42 @@ def make_init():
     np.savez_compressed(os.path.join(HERE, "init_seed0.npz"), **fx)
 
 
+def make_egno_modes(B=2, N=5, T=8, modes=5):
+    """EGNO.forward with num_modes=5 at num_timesteps=8 (model_confs.yaml:12's alternative value):
+    M = min(T, modes) = 5 = T/2 + 1 spectral modes, so the Nyquist bin is mixed. Weights are the
+    seed-0 initialisation (the drop-in reproduces the constructor's RNG order); only inputs,
+    outputs and per-tensor weight sums (to confirm that initialisation) are stored."""
+    loc_all, vel_all, q = charged_trajectories(B, N)
+    start = 20
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start]))
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start]))
+    eao = edge_attr_o(q).reshape(-1, 1)
+    edges = full_edges(B, N)
+    loc_p, vel_p, edge_attr, nodes, loc_mean = egno_main.prepare_inputs(
+        loc, vel, eao, edges, N, 1, torch.tensor(q))
+    t_out = torch.arange(1, T + 1).repeat(B, 1)
+    torch.manual_seed(0)
+    model = EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True,
+                 num_modes=modes, num_timesteps=T, time_emb_dim=32)
+    model.eval()
+    with torch.no_grad():
+        x_out, v_out, h_out = model(loc_p, nodes, edges, edge_attr, v=vel_p, loc_mean=loc_mean,
+                                    timesteps_out=t_out)
+    fx = {f"wsum::{k}": np.array(float(v.double().sum())) for k, v in model.state_dict().items()}
+    fx.update({
+        "cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T), "cfg::modes": np.array(modes),
+        "in::x": _np(loc_p), "in::h": _np(nodes), "in::v": _np(vel_p),
+        "in::loc_mean": _np(loc_mean), "in::edge_attr": _np(edge_attr),
+        "in::row": _np(edges[0]), "in::col": _np(edges[1]), "in::t_out": _np(t_out),
+        "out::x": _np(x_out), "out::v": _np(v_out), "out::h": _np(h_out),
+    })
+    np.savez_compressed(os.path.join(HERE, "egno_m5.npz"), **fx)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["egno_m5"]:
+        make_egno_modes()
+        sys.exit(0)
     make_egno()
     make_segno()
     make_segno_gravity()

@@ -150,3 +150,14 @@ def test_harness_has_no_cpu_path():
                                    torch.tensor(fx["raw::edge_attr_o"]), edges, N, 1, torch.tensor(fx["raw::charges"]))
     with pytest.raises(pkg.NonodeError):
         pkg.harness.conserved_energy("charged", torch.zeros(B * N, 3), torch.zeros(B * N, 3), torch.ones(B * N), B)
+
+
+def test_edge_check_cache_is_not_fooled_by_reused_memory():
+    """A validated edge list is cached; a different list later allocated at the same address must
+    still be checked (the cache keeps its tensors alive, so addresses cannot be recycled)."""
+    from no_node_comparison_amd.graph import check_full_graph, full_edges
+    for _ in range(20):
+        r, c = full_edges(3, 5)
+        assert check_full_graph([r.clone(), c.clone()], 15) == (3, 5)
+        with pytest.raises(ValueError):
+            check_full_graph([c.clone(), r.clone()], 15)

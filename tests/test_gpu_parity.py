@@ -347,3 +347,18 @@ def test_native_library_is_what_ran():
     maps = open(f"/proc/{os.getpid()}/maps").read()
     assert "libnonode.so" in maps
     assert math.isfinite(1.0)
+
+
+def test_egno_five_modes_matches_reference_golden():
+    """num_modes=5, num_timesteps=8 (five spectral modes with the Nyquist bin: the MM=9 TimeConv
+    instantiation) against the reference's own forward; seed-0 weights as the reference's."""
+    fx = load_golden("egno_m5")
+    T, modes = int(fx["cfg::T"]), int(fx["cfg::modes"])
+    m = _egno(T=T, modes=modes, seed=0)
+    edges = [_dev(fx["in::row"]), _dev(fx["in::col"])]
+    with torch.no_grad():
+        x, v, h = m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
+                    loc_mean=_dev(fx["in::loc_mean"]), timesteps_out=_dev(fx["in::t_out"]))
+    assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
+    assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
+    assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL

@@ -171,3 +171,24 @@ def test_oracle_gradients_match_reference_golden():
             assert np.abs(g[k]).max() == 0, k
         else:
             assert maxnorm_rel(g[k], ref) < 2e-6, k
+
+
+def test_egno_five_modes_matches_reference():
+    """num_modes=5 at num_timesteps=8 (5 spectral modes including the Nyquist bin): the drop-in's
+    seed-0 initialisation reproduces the reference's weights (per-tensor sums) and the oracle
+    reproduces the reference's forward."""
+    import torch
+    import no_node_comparison_amd as pkg
+    fx = load_golden("egno_m5")
+    T, modes = int(fx["cfg::T"]), int(fx["cfg::modes"])
+    torch.manual_seed(0)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=modes,
+                 num_timesteps=T, time_emb_dim=32)
+    sd = {k: v.detach().numpy() for k, v in m.state_dict().items()}
+    for k, v in sd.items():
+        assert abs(float(v.astype(np.float64).sum()) - float(fx["wsum::" + k])) <= 1e-6 * max(1.0, abs(float(fx["wsum::" + k]))), k
+    x, v, h = oe.egno_forward({k: a.astype(np.float64) for k, a in sd.items()},
+                              **_egno_inputs(fx, np.float64), T=T)
+    assert maxnorm_rel(x, fx["out::x"]) < TOL32
+    assert maxnorm_rel(v, fx["out::v"]) < TOL32
+    assert maxnorm_rel(h, fx["out::h"]) < TOL32
