@@ -87,7 +87,7 @@ size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt);
  *   tconv_blobs[l] (host array) time_conv_modules.l.t_conv.weights1 packed by nonode_pack_tconv;
  *   tconvx_w[l](host array) time_conv_x_modules.l.t_conv.weights1 [2][2][modes][2];
  *   outputs x_out, v_out [T*B*N][3], h_out [T*B*N][64] (time-major, egno.py:89-96).
- * Limits: N >= 2, T <= 16, modes <= 4, time_emb_dim even <= 64, in_node <= 8.
+ * Limits: N >= 2, T <= 16, modes <= 9, time_emb_dim even <= 64, in_node <= 8.
  */
 int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
                         int time_emb_dim, int modes, int Bt,
@@ -98,6 +98,25 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
                         const float* const* tconvx_w,
                         float* x_out, float* v_out, float* h_out,
                         void* workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * EGNO.forward for num_inputs > 1 (EGNO/model/egno.py:44-96 multi-input branch): the same
+ * computation as nonode_egno_forward with the inputs already spread over the T frames the way
+ * repeat_elements_to_exact_shape (EGNO/utils.py:115-131) does it:
+ *   x, v, loc_mean [T*B*N][3]; h [T*B*N][in_node]; edge_fea [T*B*N*(N-1)][n_edge_feat] (frame-major);
+ *   t_in [Bt][T] (input time of each frame's input; NULL = single-input embedding), t_out [Bt][T];
+ *   emb_w [64][in_node + 2*time_emb_dim] (columns [h | temb(t_in) | temb(t_out)]) when t_in != NULL.
+ * Workspace: nonode_egno_workspace_bytes(B, N, T, Bt). Other arguments as nonode_egno_forward.
+ */
+int nonode_egno_forward_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                               int time_emb_dim, int modes, int Bt,
+                               const float* x, const float* h, const float* v, const float* loc_mean,
+                               const float* edge_fea, const float* t_in, const float* t_out,
+                               const float* emb_w, const float* emb_b,
+                               const float* const* blobs, const float* const* tconv_blobs,
+                               const float* const* tconvx_w,
+                               float* x_out, float* v_out, float* h_out,
+                               void* workspace, size_t workspace_bytes, void* stream);
 
 /* Workspace bytes nonode_segno_forward_step needs. */
 size_t nonode_segno_workspace_bytes(int B, int N);

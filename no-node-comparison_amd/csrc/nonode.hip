@@ -1110,6 +1110,10 @@ struct TconvArgs {
   float* h_out; float* x_out; float* v_out;
   // FIRST layer only: h0 = embedding([h_in, temb]) built on the fly (egno.py:63-76)
   const float* hin; int din; const float* emb_w; int emb_ld; const float* etab; int Bt;
+  // 1: multi-input form (egno.py:44-96 with num_inputs > 1): the first layer's x, v, h_in and every
+  // layer's loc_mean are per frame ([T*BN] rows, the inputs already spread over the T frames as
+  // repeat_elements_to_exact_shape does); 0: x, v, h_in, loc_mean are [BN] rows replicated over T
+  int frames;
 };
 
 // Packed mixing weights of one TimeConv (layer_no.py:80-126), as W^T fragments (f32 MFMA A operand)
@@ -1157,29 +1161,35 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   const int ch = 16 * wave + 4 * g;      // this lane's 4 channels: ch .. ch+3
   f4 base = {0.f, 0.f, 0.f, 0.f};
   const float* et = nullptr;
-  if (FIRST) {
+  // emb_w[:, :din] h_in of row r (the node-feature part of the embedding Linear)
+  auto hin_part = [&](size_t r) {
+    f4 b = {0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < p.din; ++k) {
-      const float hv = p.hin[(size_t)c * p.din + k];
+      const float hv = p.hin[r * p.din + k];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) base[q] = fmaf(p.emb_w[(ch + q) * p.emb_ld + k], hv, base[q]);
+      for (int q = 0; q < 4; ++q) b[q] = fmaf(p.emb_w[(ch + q) * p.emb_ld + k], hv, b[q]);
     }
+    return b;
+  };
+  if (FIRST) {
+    if (!p.frames) base = hin_part((size_t)c);
     et = p.etab + ((size_t)(c % p.Bt) * T) * 64 + ch;
   }
   auto hval = [&](int t) -> f4 {
-    if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + base;
+    if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + (p.frames ? hin_part((size_t)t * BN + c) : base);
     return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + c) * 64 + ch);
   };
   __syncthreads();
   // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
   if (wave == 3 && g < 3 && cvalid) {
     const int d = g;
-    const float lmv = p.lm[(size_t)c * 3 + d];
+    auto lm_at = [&](int t) { return p.lm[((p.frames ? (size_t)t * BN : 0) + c) * 3 + d]; };
     float xs[TMAX], vs[TMAX];
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {
       if (t < T) {
-        const size_t row = FIRST ? (size_t)c : ((size_t)t * BN + c);
-        xs[t] = p.x[row * 3 + d] - lmv;
+        const size_t row = (FIRST && !p.frames) ? (size_t)c : ((size_t)t * BN + c);
+        xs[t] = p.x[row * 3 + d] - lm_at(t);
         vs[t] = p.v[row * 3 + d];
       }
     }
@@ -1225,7 +1235,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
           }
         }
         const size_t row = (size_t)t * BN + c;
-        p.x_out[row * 3 + d] = xs[t] + y0 * invT + lmv;
+        p.x_out[row * 3 + d] = xs[t] + y0 * invT + lm_at(t);
         p.v_out[row * 3 + d] = vs[t] + y1 * invT;
       }
     }
@@ -1304,20 +1314,29 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 }
 
 // etab[b][t][o] = emb_b[o] + sum_k emb_w[o][din+k] * temb(t_out[b][t])[k]   (layer_no.py:8-17)
+// multi-input (t_in != null, egno.py:44-49, 77-79): emb_w columns are [h | temb(t_in) | temb(t_out)]
+// and t_in[b][t] is the input time of frame t's input
 __global__ void temb_kernel(int Bt, int T, int din, int dim, const float* t_out, const float* emb_w,
-                            int emb_ld, const float* emb_b, float* etab) {
+                            int emb_ld, const float* emb_b, float* etab, const float* t_in = nullptr) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= Bt * T * 64) return;
   const int o = idx & 63, bt = idx >> 6;
-  const float tv = t_out[bt];
   const int half = dim / 2;
   const float scale = (float)(log(10000.0) / (double)(half - 1));
   float acc = emb_b[o];
-  for (int k = 0; k < half; ++k) {
-    const float fk = expf((float)k * -scale);
-    const float arg = tv * fk;
-    acc = fmaf(emb_w[o * emb_ld + din + k], sinf(arg), acc);
-    acc = fmaf(emb_w[o * emb_ld + din + half + k], cosf(arg), acc);
+  auto add_emb = [&](float tv, int col0) {
+    for (int k = 0; k < half; ++k) {
+      const float fk = expf((float)k * -scale);
+      const float arg = tv * fk;
+      acc = fmaf(emb_w[o * emb_ld + col0 + k], sinf(arg), acc);
+      acc = fmaf(emb_w[o * emb_ld + col0 + half + k], cosf(arg), acc);
+    }
+  };
+  if (t_in) {
+    add_emb(t_in[bt], din);
+    add_emb(t_out[bt], din + dim);
+  } else {
+    add_emb(t_out[bt], din);
   }
   etab[idx] = acc;
 }
@@ -1494,10 +1513,15 @@ size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt) {
   return (n * 64 + n * 3 + (size_t)Bt * T * 64 + 64) * sizeof(float);
 }
 
-int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+}  // extern "C"
+
+namespace {
+// nonode_egno_forward / nonode_egno_forward_frames: frames = 1 takes per-frame x, h, v, loc_mean and
+// edge_fea (and t_in for the input-time embedding), frames = 0 the single input replicated over T
+int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
                         int time_emb_dim, int modes, int Bt,
                         const float* x, const float* h, const float* v, const float* loc_mean,
-                        const float* edge_fea, const float* t_out,
+                        const float* edge_fea, const float* t_in, const float* t_out,
                         const float* emb_w, const float* emb_b,
                         const float* const* blobs, const float* const* tconv_blobs,
                         const float* const* tconvx_w,
@@ -1521,17 +1545,17 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
   float* hB = (float*)workspace;
   float* xB = hB + n * 64;
   float* etab = xB + n * 3;
-  const int emb_ld = in_node + time_emb_dim;
+  const int emb_ld = in_node + (t_in ? 2 : 1) * time_emb_dim;
   {
     const int tot = Bt * T * 64;
     hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim,
-                       t_out, emb_w, emb_ld, emb_b, etab);
+                       t_out, emb_w, emb_ld, emb_b, etab, t_in);
     if (int rc = check_launch("temb_kernel")) return rc;
   }
   for (int l = 0; l < n_layers; ++l) {
     TconvArgs a{};
     a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
-    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l];
+    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l]; a.frames = frames;
     a.h_out = hB; a.x_out = xB; a.v_out = v_out;
     if (l == 0) {
       a.h = nullptr; a.x = x; a.v = v; a.lm = loc_mean;
@@ -1540,11 +1564,42 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
       a.h = h_out; a.x = x_out; a.v = v_out; a.lm = loc_mean;
     }
     if (int rc = launch_tconv(l == 0, a, s)) return rc;
-    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, B, hB, xB, v_out, edge_fea, blobs[l], 0.f, 1.f, 0,
+    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hB, xB, v_out, edge_fea, blobs[l], 0.f, 1.f, 0,
                                     h_out, x_out, nullptr, s))
       return rc;
   }
   return NONODE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                        int time_emb_dim, int modes, int Bt,
+                        const float* x, const float* h, const float* v, const float* loc_mean,
+                        const float* edge_fea, const float* t_out,
+                        const float* emb_w, const float* emb_b,
+                        const float* const* blobs, const float* const* tconv_blobs,
+                        const float* const* tconvx_w,
+                        float* x_out, float* v_out, float* h_out,
+                        void* workspace, size_t workspace_bytes, void* stream) {
+  return egno_forward_impl(0, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v, loc_mean,
+                           edge_fea, nullptr, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w, x_out, v_out, h_out,
+                           workspace, workspace_bytes, stream);
+}
+
+int nonode_egno_forward_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                               int time_emb_dim, int modes, int Bt,
+                               const float* x, const float* h, const float* v, const float* loc_mean,
+                               const float* edge_fea, const float* t_in, const float* t_out,
+                               const float* emb_w, const float* emb_b,
+                               const float* const* blobs, const float* const* tconv_blobs,
+                               const float* const* tconvx_w,
+                               float* x_out, float* v_out, float* h_out,
+                               void* workspace, size_t workspace_bytes, void* stream) {
+  return egno_forward_impl(1, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v, loc_mean,
+                           edge_fea, t_in, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w, x_out, v_out, h_out,
+                           workspace, workspace_bytes, stream);
 }
 
 size_t nonode_segno_workspace_bytes(int B, int N) {

@@ -77,8 +77,9 @@ class EGNO(nn.Module):
     """EGNO neural operator (egno.py:8-111) — drop-in, MI355X kernels underneath.
 
     Supported configuration (the one model_confs.yaml:1-17 and main.py:133-134 build):
-    num_inputs=1, with_v=True, flat=False, norm=False, use_time_conv=True, hidden_nf=64,
-    SiLU activation. Anything else raises NotImplementedError at construction.
+    with_v=True, flat=False, norm=False, use_time_conv=True, hidden_nf=64, SiLU activation, any
+    num_inputs (num_inputs > 1: inference only). Anything else raises NotImplementedError at
+    construction.
     """
 
     def __init__(self, n_layers, in_node_nf, in_edge_nf, hidden_nf, activation=nn.SiLU(), device='cpu',
@@ -86,7 +87,7 @@ class EGNO(nn.Module):
                  time_emb_dim=32, num_inputs=1, varDT=False, fix_out_size=False):
         super().__init__()
         unsupported = []
-        if num_inputs != 1:
+        if num_inputs < 1:
             unsupported.append(f"num_inputs={num_inputs}")
         if not with_v:
             unsupported.append("with_v=False")
@@ -120,7 +121,8 @@ class EGNO(nn.Module):
         # registration + RNG order of EGNN.__init__ (basic.py:193-205): layers list, embedding
         # Linear, then each layer; then the per-layer time convs (egno.py:28-33)
         self.layers = nn.ModuleList()
-        self.embedding = nn.Linear(in_node_nf + time_emb_dim, hidden_nf)
+        # egno.py:12-16: the multi-input model also embeds each frame's input time
+        self.embedding = nn.Linear(in_node_nf + (2 if num_inputs > 1 else 1) * time_emb_dim, hidden_nf)
         for _ in range(n_layers):
             self.layers.append(EGNNLayerParams(in_edge_nf, hidden_nf, with_v))
         self.time_conv_modules = nn.ModuleList()
@@ -188,6 +190,8 @@ class EGNO(nn.Module):
         if v is None or loc_mean is None:
             raise ValueError("EGNO.forward needs v and loc_mean (the time convolution stacks "
                              "x - loc_mean with v, egno.py:103-105)")
+        if self.num_inputs > 1:
+            return self._forward_multi(x, h, edge_index, edge_fea, v, loc_mean, timesteps_in, timesteps_out)
         _lib.require_device(x, h, v, loc_mean, edge_fea, self.embedding.weight)
         T = self.num_timesteps
         BN = h.shape[0]
@@ -206,6 +210,46 @@ class EGNO(nn.Module):
             return egno_forward_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N)
         return self._forward_kernels(x, h, edge_fea, v, loc_mean, timesteps_out, B, N)
 
+    def frame_inputs(self, T):
+        """Input index of each of the T frames: repeat_elements_to_exact_shape (EGNO/utils.py:115-131)
+        repeats each of the I inputs T // I times in order, then the last input T % I more times."""
+        I = self.num_inputs
+        k = T // I
+        return [min(t // k, I - 1) if k > 0 else I - 1 for t in range(T)]
+
+    def _forward_multi(self, x, h, edge_index, edge_fea, v, loc_mean, timesteps_in, timesteps_out):
+        """egno.py:37-111 with num_inputs = I > 1: x, v, loc_mean [I, BN, 3], h [I, BN, in_node_nf],
+        edge_fea [I, E, in_edge_nf] (prepare_inputs, main_simulation_simple_no.py:313-327),
+        timesteps_in [B, I], timesteps_out [B, T]. Frame t uses input frame_inputs(T)[t]
+        (egno.py:44-49, 80-96); its embedding adds the input time's embedding (egno.py:77-79)."""
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("EGNO training with num_inputs > 1 is not implemented on the MI355X kernels")
+        I, T = self.num_inputs, self.num_timesteps
+        if x.dim() != 3 or x.shape[0] != I or h.dim() != 3 or h.shape[0] != I:
+            raise ValueError(f"num_inputs={I}: x, v, loc_mean must be [{I}, BN, 3] and h [{I}, BN, F]")
+        if timesteps_in is None or timesteps_in.dim() != 2 or timesteps_in.shape[1] != I:
+            raise ValueError(f"num_inputs={I}: timesteps_in must be [B, {I}]")
+        _lib.require_device(x, h, v, loc_mean, edge_fea, timesteps_in, self.embedding.weight)
+        BN = h.shape[1]
+        if timesteps_out is None or timesteps_out.dim() != 2 or timesteps_out.shape[1] != T:
+            raise ValueError(f"timesteps_out must be [B, {T}]")
+        Bt = timesteps_out.shape[0]
+        if BN % Bt or timesteps_in.shape[0] != Bt:
+            raise ValueError("timesteps_in / timesteps_out rows must divide the node count (egno.py:66)")
+        B, N = check_full_graph(edge_index, BN)
+        E = B * N * (N - 1)
+        if edge_fea.dim() != 3 or edge_fea.shape != (I, E, self.in_edge_nf):
+            raise ValueError(f"edge_fea must be [{I}, {E}, {self.in_edge_nf}], got {tuple(edge_fea.shape)}")
+        fidx = torch.tensor(self.frame_inputs(T), device=x.device)
+        f32 = lambda t: t.detach().to(torch.float32)  # noqa: E731
+        per_frame = lambda t: f32(t)[fidx].reshape(T * t.shape[1], t.shape[2]).contiguous()  # noqa: E731
+        with torch.no_grad():
+            xf, hf, vf, lmf, eff = (per_frame(t) for t in (x, h, v, loc_mean, edge_fea))
+            t_in = f32(timesteps_in)[:, fidx].contiguous()
+            t_out = f32(timesteps_out).contiguous()
+            return self._launch_forward(_lib.lib().nonode_egno_forward_frames, B, N, xf, hf, vf, lmf, eff, t_out,
+                                        t_in=t_in)
+
     def _t_out_f32(self, t_out):
         """timesteps_out as f32 (cached per tensor/version: callers pass the same int64 tensor)."""
         if t_out.dtype == torch.float32 and t_out.is_contiguous():
@@ -220,10 +264,14 @@ class EGNO(nn.Module):
 
     @torch.no_grad()
     def _forward_kernels(self, x, h, edge_fea, v, loc_mean, t_out, B, N):
-        T = self.num_timesteps
         f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
         x, h, v, lm, ef = f32(x), f32(h), f32(v), f32(loc_mean), f32(edge_fea)
-        tt = self._t_out_f32(t_out)
+        return self._launch_forward(_lib.lib().nonode_egno_forward, B, N, x, h, v, lm, ef, self._t_out_f32(t_out))
+
+    def _launch_forward(self, entry, B, N, x, h, v, lm, ef, tt, t_in=None):
+        """nonode_egno_forward (single input) or nonode_egno_forward_frames (t_in given)."""
+        T = self.num_timesteps
+        f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
         blobs, tblobs = self._packed()
         dev = x.device
         n = T * B * N
@@ -239,9 +287,12 @@ class EGNO(nn.Module):
         tcw_p = P(*[tblobs[i].data_ptr() for i in range(self.n_layers)])
         tcx_p = P(*[t.data_ptr() for t in tcx])
         ew, eb = f32(self.embedding.weight), f32(self.embedding.bias)
-        _lib.check(L.nonode_egno_forward(
-            B, N, T, self.n_layers, self.in_node_nf, self.in_edge_nf, self.time_emb_dim, self.num_modes,
-            tt.shape[0], _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef), _lib.ptr(tt),
-            _lib.ptr(ew), _lib.ptr(eb), blob_p, tcw_p, tcx_p, _lib.ptr(x_out), _lib.ptr(v_out),
-            _lib.ptr(h_out), _lib.ptr(ws), ws_bytes, _lib.stream_of(x)))
+        tail = (_lib.ptr(ew), _lib.ptr(eb), blob_p, tcw_p, tcx_p, _lib.ptr(x_out), _lib.ptr(v_out),
+                _lib.ptr(h_out), _lib.ptr(ws), ws_bytes, _lib.stream_of(x))
+        head = (B, N, T, self.n_layers, self.in_node_nf, self.in_edge_nf, self.time_emb_dim, self.num_modes,
+                tt.shape[0], _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef))
+        if t_in is None:
+            _lib.check(entry(*head, _lib.ptr(tt), *tail))
+        else:
+            _lib.check(entry(*head, _lib.ptr(t_in), _lib.ptr(tt), *tail))
         return x_out, v_out, h_out

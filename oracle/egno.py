@@ -134,6 +134,51 @@ def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=
     return xx, vv, hh
 
 
+def frame_inputs(num_inputs, T):
+    """repeat_elements_to_exact_shape (EGNO/utils.py:115-131) as a frame -> input index map: each
+    input repeated T // I times in order, then the last input T % I more times."""
+    k = T // num_inputs
+    return np.array([min(t // k, num_inputs - 1) if k > 0 else num_inputs - 1 for t in range(T)])
+
+
+def egno_forward_multi(p, x, h, row, col, edge_fea, v, loc_mean, t_in, t_out, n_layers=4, T=10,
+                       hidden=64, time_emb_dim=32):
+    """EGNO.forward (egno.py:37-111) for num_inputs = I > 1.
+
+    x, v, loc_mean: [I, BN, 3]; h: [I, BN, in_node]; edge_fea: [I, E, in_edge]; t_in: [Bt, I];
+    t_out: [Bt, T]. Frame t reads input frame_inputs(I, T)[t] (egno.py:80-96); the embedding input
+    is [h, temb(t_in), temb(t_out)] (egno.py:44-49, 77-79), both embeddings broadcast as egno.py:66."""
+    dt = x.dtype
+    I, BN = h.shape[0], h.shape[1]
+    E = row.shape[0]
+    f = frame_inputs(I, T)
+
+    def spread(temb):   # [Bt, T, Ht] -> [T, BN, Ht] with the egno.py:66 broadcast
+        Bt = temb.shape[0]
+        return np.transpose(temb, (1, 0, 2))[:, None].repeat(BN // Bt, axis=1).reshape(T, BN, -1)
+
+    temb_in = spread(timestep_embedding(t_in[:, f], time_emb_dim, dtype=dt))
+    temb_out = spread(timestep_embedding(t_out, time_emb_dim, dtype=dt))
+    hh = np.concatenate([h[f], temb_in, temb_out], axis=-1)
+    hh = linear(hh.reshape(T * BN, -1), p, "embedding")
+    offs_e = (np.arange(T) * BN).repeat(E)
+    row_t = np.tile(row, T) + offs_e
+    col_t = np.tile(col, T) + offs_e
+    xx = x[f].reshape(T * BN, 3)
+    vv = v[f].reshape(T * BN, 3)
+    lm = loc_mean[f].reshape(T * BN, 3)
+    ef = edge_fea[f].reshape(T * E, -1)
+    for i in range(n_layers):
+        hh = time_conv(hh.reshape(T, BN, hidden), p[f"time_conv_modules.{i}.t_conv.weights1"])
+        hh = hh.reshape(T * BN, hidden)
+        X = np.stack([xx - lm, vv], axis=-1).reshape(T, BN, 3, 2)
+        X = time_conv_x(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
+        xx = X[..., 0].reshape(T * BN, 3) + lm
+        vv = X[..., 1].reshape(T * BN, 3)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv)
+    return xx, vv, hh
+
+
 def num_modes_for(num_timesteps, num_modes):
     """egno.py:26."""
     return min(num_timesteps, num_modes) if num_timesteps != 5 else min(num_modes, 3)

@@ -26,6 +26,7 @@ What each fixture pins (reference file:line):
                       (synthetic_sim.py:360-404).
   egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8 (5 spectral modes incl. the
                       Nyquist bin; model_confs.yaml:12's alternative), seed-0 weights.
+  egno_multi.npz      EGNO.forward with num_inputs=3 (multi-input branch, egno.py:44-96), seed-0 weights.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
                       torch.manual_seed(0) (RNG-consumption order of the constructors).
 """
@@ -366,9 +367,46 @@ def make_egno_modes(B=2, N=5, T=8, modes=5):
     np.savez_compressed(os.path.join(HERE, "egno_m5.npz"), **fx)
 
 
+def make_egno_multi(B=2, N=5, T=10, I=3):
+    """EGNO.forward with num_inputs=3 (main.py --num_inputs; _schedule.yaml:58 sweeps 2 and 3):
+    inputs are frames start-2 .. start of a reference trajectory through prepare_inputs'
+    multi-input branch (main_simulation_simple_no.py:313-327); timesteps_in / _out as run_epoch
+    adjusts them (in - max(in), out - max(in)). Seed-0 weights; inputs, outputs, weight sums."""
+    loc_all, vel_all, q = charged_trajectories(B, N)
+    start = 20
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start - I + 1:start + 1]))   # [B, I, N, 3]
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start - I + 1:start + 1]))
+    eao = edge_attr_o(q).reshape(-1, 1)
+    edges = full_edges(B, N)
+    loc_p, vel_p, edge_attr, nodes, loc_mean = egno_main.prepare_inputs(
+        loc, vel, eao, edges, N, I, torch.tensor(q))
+    t_in = torch.arange(-I + 1, 1).repeat(B, 1)                  # [B, I]
+    t_out = torch.arange(1, T + 1).repeat(B, 1)                  # [B, T]
+    torch.manual_seed(0)
+    model = EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True,
+                 num_modes=2, num_timesteps=T, time_emb_dim=32, num_inputs=I)
+    model.eval()
+    with torch.no_grad():
+        x_out, v_out, h_out = model(loc_p, nodes, edges, edge_attr, v=vel_p, loc_mean=loc_mean,
+                                    timesteps_in=t_in, timesteps_out=t_out)
+    fx = {f"wsum::{k}": np.array(float(v.double().sum())) for k, v in model.state_dict().items()}
+    fx.update({
+        "cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T), "cfg::I": np.array(I),
+        "in::x": _np(loc_p), "in::h": _np(nodes), "in::v": _np(vel_p),
+        "in::loc_mean": _np(loc_mean), "in::edge_attr": _np(edge_attr),
+        "in::row": _np(edges[0]), "in::col": _np(edges[1]),
+        "in::t_in": _np(t_in), "in::t_out": _np(t_out),
+        "out::x": _np(x_out), "out::v": _np(v_out), "out::h": _np(h_out),
+    })
+    np.savez_compressed(os.path.join(HERE, "egno_multi.npz"), **fx)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["egno_m5"]:
         make_egno_modes()
+        sys.exit(0)
+    if sys.argv[1:] == ["egno_multi"]:
+        make_egno_multi()
         sys.exit(0)
     make_egno()
     make_segno()

@@ -100,9 +100,11 @@ def test_reference_checkpoint_loads():
 
 def test_unsupported_configs_raise():
     with pytest.raises(NotImplementedError):
-        _egno_ctor(num_inputs=2)
+        _egno_ctor(num_inputs=0)
     with pytest.raises(NotImplementedError):
         _egno_ctor(hidden_nf=32)
+    # num_inputs > 1 is supported (inference): the embedding takes both time embeddings (egno.py:12-16)
+    assert _egno_ctor(num_inputs=3).embedding.weight.shape == (64, 2 + 2 * 32)
     with pytest.raises(NotImplementedError):
         pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, tanh=True)
     with pytest.raises(ValueError):

@@ -362,3 +362,25 @@ def test_egno_five_modes_matches_reference_golden():
     assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
     assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
     assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL
+
+
+def test_egno_multi_input_matches_reference_golden():
+    """num_inputs=3 (nonode_egno_forward_frames: per-frame inputs, input-time embedding) against the
+    reference's own forward; seed-0 weights as the reference's."""
+    fx = load_golden("egno_multi")
+    T, I = int(fx["cfg::T"]), int(fx["cfg::I"])
+    torch.manual_seed(0)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                 num_timesteps=T, time_emb_dim=32, num_inputs=I, device=DEV).eval()
+    edges = [_dev(fx["in::row"]), _dev(fx["in::col"])]
+    with torch.no_grad():
+        x, v, h = m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
+                    loc_mean=_dev(fx["in::loc_mean"]), timesteps_in=_dev(fx["in::t_in"]),
+                    timesteps_out=_dev(fx["in::t_out"]))
+    assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
+    assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
+    assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL
+    m.train()
+    with pytest.raises(NotImplementedError):
+        m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
+          loc_mean=_dev(fx["in::loc_mean"]), timesteps_in=_dev(fx["in::t_in"]), timesteps_out=_dev(fx["in::t_out"]))

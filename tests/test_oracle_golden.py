@@ -192,3 +192,27 @@ def test_egno_five_modes_matches_reference():
     assert maxnorm_rel(x, fx["out::x"]) < TOL32
     assert maxnorm_rel(v, fx["out::v"]) < TOL32
     assert maxnorm_rel(h, fx["out::h"]) < TOL32
+
+
+def test_egno_multi_input_matches_reference():
+    """num_inputs=3 (egno.py:44-96 multi-input branch): seed-0 initialisation of the drop-in equals
+    the reference's (per-tensor sums), and the oracle's multi-input forward reproduces the
+    reference's output."""
+    import torch
+    import no_node_comparison_amd as pkg
+    fx = load_golden("egno_multi")
+    T, I = int(fx["cfg::T"]), int(fx["cfg::I"])
+    torch.manual_seed(0)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                 num_timesteps=T, time_emb_dim=32, num_inputs=I)
+    sd = {k: v.detach().numpy() for k, v in m.state_dict().items()}
+    for k, v in sd.items():
+        want = float(fx["wsum::" + k])
+        assert abs(float(v.astype(np.float64).sum()) - want) <= 1e-6 * max(1.0, abs(want)), k
+    d = lambda k: fx[k].astype(np.float64)  # noqa: E731
+    x, v, h = oe.egno_forward_multi({k: a.astype(np.float64) for k, a in sd.items()}, d("in::x"), d("in::h"),
+                                    fx["in::row"], fx["in::col"], d("in::edge_attr"), d("in::v"),
+                                    d("in::loc_mean"), fx["in::t_in"], fx["in::t_out"], T=T)
+    assert maxnorm_rel(x, fx["out::x"]) < TOL32
+    assert maxnorm_rel(v, fx["out::v"]) < TOL32
+    assert maxnorm_rel(h, fx["out::h"]) < TOL32
