@@ -42,8 +42,8 @@ class GCLParams(nn.Module):
 class SEGNO(nn.Module):
     """SEGNO neural ODE (model.py:6-102) — drop-in, MI355X kernels underneath.
 
-    Supported: single input (x of shape [BN, 3]), SiLU, tanh=False, norm_diff=False,
-    hidden_nf=64, in_edge_nf <= 4. ``multiple_agg`` is accepted; num_inputs > 1 inputs raise.
+    Supported: SiLU, tanh=False, norm_diff=False, hidden_nf=64, in_edge_nf <= 4; single input
+    (x [BN, 3]) or several (x [BN, I, 3] with in_steps, multiple_agg 'sum' / 'attn').
     """
 
     def __init__(self, in_node_nf, in_edge_nf, hidden_nf, device='cpu', act_fn=nn.SiLU(), n_layers=4,
@@ -70,7 +70,7 @@ class SEGNO(nn.Module):
         self.multiple_agg = multiple_agg
         if multiple_agg == "attn":
             # InvariantTemporalAttention parameters (model.py:126-139), created first as in the
-            # reference so the RNG stream matches; the multi-input path itself is not implemented
+            # reference so the RNG stream matches
             self.enc_attn_net = nn.Module()
             self.enc_attn_net.attn_mlp = nn.Sequential(nn.Linear(hidden_nf + 1, hidden_nf), nn.Tanh(),
                                                        nn.Linear(hidden_nf, 1))
@@ -107,11 +107,45 @@ class SEGNO(nn.Module):
         """model.py:53-92 (single input). his [BN, in_node_nf], x, v [BN, 3], edges 2 x [E],
         edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T."""
         if x.dim() == 3:
-            raise NotImplementedError("SEGNO multi-input (num_inputs > 1) path is not implemented")
+            return self._forward_multi(his, x, edges, v, edge_attr, int(T), in_steps)
         if self.bug_compat:
             # the live reference forward returns its inputs (and the embedded h)
             return x, self._embed(his), v
         return self._run(his, None, x, edges, v, edge_attr, int(T))
+
+    def _forward_multi(self, his, x, edges, v, edge_attr, T, in_steps):
+        """model.py:53-92 with num_inputs = I > 1: his [BN, I, F], x, v [BN, I, 3], in_steps [I]
+        (input frame offsets, train_nbody.py:114). forward_step (the HIP integrator) runs
+        diff(in_steps) + [T] substeps in turn; after each but the last, the next input is folded in
+        by multiple_agg ('sum': added; 'attn': InvariantTemporalAttention weights over the pair,
+        model.py:104-139, a small torch MLP on the device). Returns the last forward_step's result;
+        bug_compat=True returns the state before it, as the reference does."""
+        if in_steps is None:
+            raise ValueError("SEGNO with several inputs needs in_steps (train_nbody.py:114)")
+        if his.dim() != 3 or v.dim() != 3 or his.shape[1] != x.shape[1] or v.shape[1] != x.shape[1]:
+            raise ValueError("his, x, v must be [BN, I, .] with the same I")
+        _lib.require_device(his, x, v, edge_attr, self.embedding.weight)
+        st = in_steps.tolist() if torch.is_tensor(in_steps) else list(in_steps)
+        steps = [int(b) - int(a) for a, b in zip(st[:-1], st[1:])] + [int(T)]
+        with torch.no_grad():
+            h = self._embed(his.to(torch.float32))
+            h_, x_, v_ = h[:, 0].contiguous(), x[:, 0].contiguous(), v[:, 0].contiguous()
+            for i, step in enumerate(steps):
+                xi, hi, vi = self._run(None, h_, x_, edges, v_, edge_attr, step)
+                if i < len(steps) - 1:
+                    if self.multiple_agg == "sum":
+                        h_, x_, v_ = h[:, i + 1] + hi, x[:, i + 1] + xi, v[:, i + 1] + vi
+                    elif self.multiple_agg == "attn":
+                        x_, v_, h_ = self._attn_combine(torch.stack([x[:, i + 1], xi], 1),
+                                                        torch.stack([v[:, i + 1], vi], 1),
+                                                        torch.stack([h[:, i + 1], hi], 1))
+            return (x_, h_, v_) if self.bug_compat else (xi, hi, vi)
+
+    def _attn_combine(self, loc_seq, vel_seq, his_seq):
+        """prepare_node_inputs (model.py:104-121) with InvariantTemporalAttention (model.py:126-139)."""
+        speed = vel_seq.float().norm(dim=-1, keepdim=True)
+        a = self.enc_attn_net.attn_mlp(torch.cat([speed, his_seq.float()], dim=-1)).softmax(dim=1)
+        return (a * loc_seq).sum(1), (a * vel_seq).sum(1), (a * his_seq).sum(1)
 
     def forward_step(self, h, x, edges, v, edge_attr, T=10):
         """model.py:95-102: T substeps of the shared layer from an already-embedded h."""

@@ -66,3 +66,34 @@ def forward(p, his, x, row, col, v, edge_attr, T=10, bug_compat=True, **kw):
         forward_step(p, h, x, row, col, v, edge_attr, T=T, **kw)
         return x, h, v
     return forward_step(p, h, x, row, col, v, edge_attr, T=T, **kw)
+
+
+def attn_combine(p, loc_seq, vel_seq, his_seq):
+    """prepare_node_inputs + InvariantTemporalAttention (model.py:104-139): softmax over the stacked
+    inputs of attn_mlp([|v|, h]) = Linear(Tanh(Linear(.))), then attention-weighted sums."""
+    speed = np.sqrt((vel_seq ** 2).sum(-1, keepdims=True))                      # (BN, K, 1)
+    feats = np.concatenate([speed, his_seq], axis=-1)
+    z = np.tanh(feats @ p["enc_attn_net.attn_mlp.0.weight"].T + p["enc_attn_net.attn_mlp.0.bias"])
+    a = z @ p["enc_attn_net.attn_mlp.2.weight"].T + p["enc_attn_net.attn_mlp.2.bias"]   # (BN, K, 1)
+    a = np.exp(a - a.max(axis=1, keepdims=True))
+    a = a / a.sum(axis=1, keepdims=True)
+    return (a * loc_seq).sum(1), (a * vel_seq).sum(1), (a * his_seq).sum(1)
+
+
+def forward_multi(p, his, x, row, col, v, edge_attr, in_steps, T=10, multiple_agg="attn", bug_compat=True, **kw):
+    """The live SEGNO.forward (model.py:53-92) with num_inputs > 1: his [BN, I, F], x, v [BN, I, 3],
+    in_steps [I]. forward_step runs diff(in_steps) + [T] substeps in turn, folding each next input
+    in ('sum' or 'attn'). The reference returns the state before the last forward_step
+    (bug_compat=True); bug_compat=False returns that last step's result."""
+    steps = list(np.diff(np.asarray(in_steps))) + [T]
+    h = his @ p["embedding.weight"].T + p["embedding.bias"]
+    h_, x_, v_ = h[:, 0], x[:, 0], v[:, 0]
+    for i, step in enumerate(steps):
+        xi, hi, vi = forward_step(p, h_, x_, row, col, v_, edge_attr, T=int(step), **kw)
+        if i < len(steps) - 1:
+            if multiple_agg == "sum":
+                h_, x_, v_ = h[:, i + 1] + hi, x[:, i + 1] + xi, v[:, i + 1] + vi
+            elif multiple_agg == "attn":
+                x_, v_, h_ = attn_combine(p, np.stack([x[:, i + 1], xi], 1), np.stack([v[:, i + 1], vi], 1),
+                                          np.stack([h[:, i + 1], hi], 1))
+    return (x_, h_, v_) if bug_compat else (xi, hi, vi)

@@ -27,6 +27,8 @@ What each fixture pins (reference file:line):
   egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8 (5 spectral modes incl. the
                       Nyquist bin; model_confs.yaml:12's alternative), seed-0 weights.
   egno_multi.npz      EGNO.forward with num_inputs=3 (multi-input branch, egno.py:44-96), seed-0 weights.
+  segno_multi.npz     SEGNO live forward with num_inputs=3, multiple_agg='attn' (model.py:53-92,
+                      104-139) and the discarded last forward_step.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
                       torch.manual_seed(0) (RNG-consumption order of the constructors).
 """
@@ -401,7 +403,48 @@ def make_egno_multi(B=2, N=5, T=10, I=3):
     np.savez_compressed(os.path.join(HERE, "egno_multi.npz"), **fx)
 
 
+def make_segno_multi(B=2, N=5, T=10, I=3):
+    """SEGNO with num_inputs=3, multiple_agg='attn' (main.py:111): the live forward (model.py:53-92)
+    on inputs taken as train_nbody.py:97-123 takes them (frames start-6, start-3, start; in_steps
+    = indices - start; edge_attr from the last frame). Stores the reference forward's output
+    (which stops before the last forward_step) and that last forward_step's
+    result from the returned state."""
+    loc_all, vel_all, q = charged_trajectories(B, N, seed=45)
+    start = 30
+    steps = [T // I] * (I - 1)
+    indices = np.flip(start - np.cumsum([0] + steps)).copy()
+    edges = full_edges(B, N)
+    rows, cols = edges
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, indices])).permute(0, 2, 1, 3).reshape(B * N, I, 3)
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, indices])).permute(0, 2, 1, 3).reshape(B * N, I, 3)
+    charges = torch.tensor(q).reshape(-1, 1)
+    prod = charges[rows] * charges[cols]
+    in_steps = torch.tensor(indices - start).int()
+    h = torch.sqrt(torch.sum(vel ** 2, dim=-1)).unsqueeze(-1)                       # (BN, I, 1)
+    loc_dist = torch.sum((loc[rows, -1, :] - loc[cols, -1, :]) ** 2, 1).unsqueeze(1)
+    edge_attr = torch.cat([prod, loc_dist], 1)
+    torch.manual_seed(0)
+    model = SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True,
+                  norm_diff=False, tanh=False, device="cpu", varDT=False, multiple_agg="attn")
+    model.eval()
+    with torch.no_grad():
+        fx_, fh_, fv_ = model(h, loc, edges, vel, edge_attr, T=T, in_steps=in_steps)
+        lx, lh, lv = model.forward_step(fh_, fx_, edges, fv_, edge_attr, T=T)
+    fx = dict(_sd(model))
+    fx.update({
+        "cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T), "cfg::I": np.array(I),
+        "in::x": _np(loc), "in::v": _np(vel), "in::his": _np(h), "in::edge_attr": _np(edge_attr),
+        "in::row": _np(rows), "in::col": _np(cols), "in::in_steps": _np(in_steps),
+        "fwd::x": _np(fx_), "fwd::h": _np(fh_), "fwd::v": _np(fv_),
+        "last::x": _np(lx), "last::h": _np(lh), "last::v": _np(lv),
+    })
+    np.savez_compressed(os.path.join(HERE, "segno_multi.npz"), **fx)
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["segno_multi"]:
+        make_segno_multi()
+        sys.exit(0)
     if sys.argv[1:] == ["egno_m5"]:
         make_egno_modes()
         sys.exit(0)

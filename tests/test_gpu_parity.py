@@ -384,3 +384,22 @@ def test_egno_multi_input_matches_reference_golden():
     with pytest.raises(NotImplementedError):
         m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
           loc_mean=_dev(fx["in::loc_mean"]), timesteps_in=_dev(fx["in::t_in"]), timesteps_out=_dev(fx["in::t_out"]))
+
+
+def test_segno_multi_input_attn_matches_reference_golden():
+    """SEGNO num_inputs=3, multiple_agg='attn': the HIP integrator per segment with the attention
+    fold between, against the reference (bug_compat) and its discarded last forward_step."""
+    fx = load_golden("segno_multi")
+    T = int(fx["cfg::T"])
+    edges = [_dev(fx["in::row"]), _dev(fx["in::col"])]
+    for bug, pre in ((True, "fwd"), (False, "last")):
+        torch.manual_seed(0)
+        m = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True, multiple_agg="attn",
+                      bug_compat=bug, device=DEV).eval()
+        m.load_state_dict({k: torch.tensor(v) for k, v in params_of(fx).items()})
+        with torch.no_grad():
+            x, h, v = m(_dev(fx["in::his"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(fx["in::edge_attr"]),
+                        T=T, in_steps=_dev(fx["in::in_steps"]))
+        assert maxnorm_rel(x.cpu(), fx[pre + "::x"]) < TOL
+        assert maxnorm_rel(h.cpu(), fx[pre + "::h"]) < TOL
+        assert maxnorm_rel(v.cpu(), fx[pre + "::v"]) < TOL

@@ -216,3 +216,20 @@ def test_egno_multi_input_matches_reference():
     assert maxnorm_rel(x, fx["out::x"]) < TOL32
     assert maxnorm_rel(v, fx["out::v"]) < TOL32
     assert maxnorm_rel(h, fx["out::h"]) < TOL32
+
+
+def test_segno_multi_input_attn_matches_reference():
+    """SEGNO live forward with num_inputs=3, multiple_agg='attn' (model.py:53-92, 104-139): the oracle
+    reproduces the reference's output (bug_compat: the state before the last forward_step) and the
+    last forward_step the reference discards."""
+    fx = load_golden("segno_multi")
+    p = {k: v.astype(np.float64) for k, v in params_of(fx).items()}
+    T = int(fx["cfg::T"])
+    d = lambda k: fx[k].astype(np.float64)  # noqa: E731
+    args = (p, d("in::his"), d("in::x"), fx["in::row"], fx["in::col"], d("in::v"), d("in::edge_attr"),
+            fx["in::in_steps"])
+    for bug, pre in ((True, "fwd"), (False, "last")):
+        x, h, v = osg.forward_multi(*args, T=T, multiple_agg="attn", bug_compat=bug, dense_mean=True)
+        assert maxnorm_rel(x, fx[pre + "::x"]) < TOL32
+        assert maxnorm_rel(h, fx[pre + "::h"]) < TOL32
+        assert maxnorm_rel(v, fx[pre + "::v"]) < TOL32
