@@ -227,6 +227,28 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
                          float* const* g_tconvx, float* g_emb_w, float* g_emb_b,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/*
+ * Multi-input (num_inputs > 1) training: nonode_egno_forward_train / nonode_egno_backward with the
+ * inputs per frame as in nonode_egno_forward_frames (x, h, v, loc_mean [T*B*N] rows, edge_fea
+ * [T*B*N*(N-1)] rows, t_in [Bt][T]). The state is sized by nonode_egno_train_state_bytes with
+ * time_emb_dim doubled when t_in is given; backward takes with_t_in to match.
+ */
+int nonode_egno_forward_train_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                                     int time_emb_dim, int modes, int Bt, const float* x, const float* h,
+                                     const float* v, const float* loc_mean, const float* edge_fea,
+                                     const float* t_in, const float* t_out, const float* emb_w, const float* emb_b,
+                                     const float* const* blobs, const float* const* tconv_blobs,
+                                     const float* const* tconvx_w, float* x_out, float* v_out, float* h_out,
+                                     void* state, size_t state_bytes, void* workspace, size_t workspace_bytes,
+                                     void* stream);
+int nonode_egno_backward_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                                int with_t_in, int modes, int Bt, const float* loc_mean, const float* edge_fea,
+                                const float* const* bblobs, const float* const* tconv_w,
+                                const float* const* tconvx_w, const void* state, const float* g_x, const float* g_v,
+                                const float* g_h, const nonode_layer_grads* layer_grads, float* const* g_tconv,
+                                float* const* g_tconvx, float* g_emb_w, float* g_emb_b, void* workspace,
+                                size_t workspace_bytes, void* stream);
+
 
 /* ---- rollout drivers (rollout_fn / prepare_inputs / energy on the GPU) ---- */
 

@@ -20,6 +20,7 @@ SYMBOLS = (
     "nonode_profile_end", "nonode_tconv_blob_floats", "nonode_pack_tconv",
     "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
     "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
+    "nonode_egno_forward_train_frames", "nonode_egno_backward_frames",
     "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
     "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout", "nonode_sim_charged", "nonode_sim_gravity",
     "nonode_gather_batch", "nonode_rollout_metrics",
@@ -88,6 +89,11 @@ def lib():
     L.nonode_egno_train_state_bytes.restype = _sz
     L.nonode_egno_forward_train.argtypes = ([_i] * 9 + [_vp] * 8 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
                                             + [_sz, _vp, _sz, _vp])
+    L.nonode_egno_forward_train_frames.argtypes = ([_i] * 9 + [_vp] * 9 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
+                                                   + [_sz, _vp, _sz, _vp])
+    L.nonode_egno_backward_frames.argtypes = ([_i] * 10 + [_vp] * 2 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
+                                              + [ctypes.POINTER(LayerGrads), ctypes.POINTER(_vp),
+                                                 ctypes.POINTER(_vp)] + [_vp] * 3 + [_sz, _vp])
     L.nonode_egno_backward_workspace_bytes.argtypes = [_i] * 4
     L.nonode_egno_backward_workspace_bytes.restype = _sz
     L.nonode_egno_backward.argtypes = ([_i] * 9 + [_vp] * 2 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4

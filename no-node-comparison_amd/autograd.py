@@ -18,11 +18,14 @@ def _f32(t):
 
 class EGNOTrain(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, model, x, h, edge_fea, v, loc_mean, t_out, B, N, *params):
+    def forward(ctx, model, x, h, edge_fea, v, loc_mean, t_out, t_in, B, N, *params):
+        # t_in is None for a single input; else the inputs are per frame (num_inputs > 1) and t_in
+        # [Bt, T] is each frame's input time (nonode_egno_forward_train_frames)
         L = _lib.lib()
         T = model.num_timesteps
         dev = x.device
         x, h, v, lm, ef, tt = _f32(x), _f32(h), _f32(v), _f32(loc_mean), _f32(edge_fea), _f32(t_out)
+        emb_cols = model.time_emb_dim * (1 if t_in is None else 2)
         Bt = tt.shape[0]
         blobs, tblobs = model._packed()
         n = T * B * N
@@ -31,18 +34,23 @@ class EGNOTrain(torch.autograd.Function):
         h_out = torch.empty(n, model.hidden_nf, device=dev)
         ws_bytes = L.nonode_egno_workspace_bytes(B, N, T, Bt)
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
-        st_bytes = L.nonode_egno_train_state_bytes(B, N, T, model.n_layers, model.in_node_nf, model.time_emb_dim)
+        st_bytes = L.nonode_egno_train_state_bytes(B, N, T, model.n_layers, model.in_node_nf, emb_cols)
         state = torch.empty((st_bytes + 3) // 4, dtype=torch.float32, device=dev)
         P = ctypes.c_void_p * model.n_layers
         tcx = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
         ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
-        _lib.check(L.nonode_egno_forward_train(
-            B, N, T, model.n_layers, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
-            _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef), _lib.ptr(tt), _lib.ptr(ew),
-            _lib.ptr(eb), P(*[blobs[i].data_ptr() for i in range(model.n_layers)]),
-            P(*[tblobs[i].data_ptr() for i in range(model.n_layers)]), P(*[t.data_ptr() for t in tcx]),
-            _lib.ptr(x_out), _lib.ptr(v_out), _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.ptr(ws), ws_bytes,
-            _lib.stream_of(x)))
+        head = (B, N, T, model.n_layers, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
+                _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef))
+        tail = (_lib.ptr(ew), _lib.ptr(eb), P(*[blobs[i].data_ptr() for i in range(model.n_layers)]),
+                P(*[tblobs[i].data_ptr() for i in range(model.n_layers)]), P(*[t.data_ptr() for t in tcx]),
+                _lib.ptr(x_out), _lib.ptr(v_out), _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.ptr(ws), ws_bytes,
+                _lib.stream_of(x))
+        if t_in is None:
+            _lib.check(L.nonode_egno_forward_train(*head, _lib.ptr(tt), *tail))
+        else:
+            ti = _f32(t_in)
+            _lib.check(L.nonode_egno_forward_train_frames(*head, _lib.ptr(ti), _lib.ptr(tt), *tail))
+        ctx.frames = t_in is not None
         ctx.model, ctx.B, ctx.N, ctx.Bt = model, B, N, Bt
         ctx.state, ctx.lm, ctx.ef = state, lm, ef
         ctx.n_params = len(params)
@@ -71,19 +79,24 @@ class EGNOTrain(torch.autograd.Function):
         gx = _f32(gx) if gx is not None else torch.zeros(T * B * N, 3, device=dev)
         gv = _f32(gv) if gv is not None else None
         gh = _f32(gh) if gh is not None else None
-        _lib.check(L.nonode_egno_backward(
-            B, N, T, nl, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
-            _lib.ptr(ctx.lm), _lib.ptr(ctx.ef), P(*[bblobs[i].data_ptr() for i in range(nl)]),
-            P(*[t.data_ptr() for t in tw]), P(*[t.data_ptr() for t in txw]), _lib.ptr(ctx.state),
-            _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh), lg, g_tc, g_tcx,
-            _lib.ptr(grads["embedding.weight"]), _lib.ptr(grads["embedding.bias"]), _lib.ptr(ws), ws_bytes,
-            _lib.stream_of(gx)))
+        head = (B, N, T, nl, model.in_node_nf, model.in_edge_nf, model.time_emb_dim)
+        tail = (model.num_modes, Bt,
+                _lib.ptr(ctx.lm), _lib.ptr(ctx.ef), P(*[bblobs[i].data_ptr() for i in range(nl)]),
+                P(*[t.data_ptr() for t in tw]), P(*[t.data_ptr() for t in txw]), _lib.ptr(ctx.state),
+                _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh), lg, g_tc, g_tcx,
+                _lib.ptr(grads["embedding.weight"]), _lib.ptr(grads["embedding.bias"]), _lib.ptr(ws), ws_bytes,
+                _lib.stream_of(gx))
+        if ctx.frames:
+            _lib.check(L.nonode_egno_backward_frames(*head, 1, *tail))
+        else:
+            _lib.check(L.nonode_egno_backward(*head, *tail))
         ctx.state = None
         out = [grads[name] for name, _ in model.named_parameters()]
-        return (None,) * 9 + tuple(out)
+        return (None,) * 10 + tuple(out)
 
 
-def egno_forward_train(model, x, h, edge_fea, v, loc_mean, t_out, B, N):
-    """EGNO forward that records the kernels' backward on the autograd tape."""
+def egno_forward_train(model, x, h, edge_fea, v, loc_mean, t_out, B, N, t_in=None):
+    """EGNO forward that records the kernels' backward on the autograd tape (t_in: per-frame
+    multi-input form, see EGNO._forward_multi)."""
     params = [p for _, p in model.named_parameters()]
-    return EGNOTrain.apply(model, x, h, edge_fea, v, loc_mean, t_out, B, N, *params)
+    return EGNOTrain.apply(model, x, h, edge_fea, v, loc_mean, t_out, t_in, B, N, *params)

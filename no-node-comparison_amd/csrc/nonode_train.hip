@@ -221,36 +221,44 @@ __device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
 // ---- training-forward helpers -----------------------------------------------------------------
 // h0[t*BN + c] = emb_w[:, :din] h_in[c] + etab[c % Bt][t]   (egno.py:63-76; same arithmetic as
 // tconv_kernel<true>), and x, v replicated over T (egno.py:89-96)
+// frames = 1 (num_inputs > 1): h_in, x, v are per frame ([T*BN] rows) instead of replicated
 __global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, const float* emb_w, int emb_ld,
-                          const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr) {
+                          const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr,
+                          int frames) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= BN * 64) return;
   const int o = idx & 63, c = idx >> 6;
-  float base = 0.f;
-  for (int k = 0; k < din; ++k) base = fmaf(emb_w[o * emb_ld + k], hin[(size_t)c * din + k], base);
+  auto hin_part = [&](size_t r) {
+    float b = 0.f;
+    for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[r * din + k], b);
+    return b;
+  };
+  const float base = frames ? 0.f : hin_part((size_t)c);
   const float* et = etab + (size_t)(c % Bt) * T * 64;
   for (int t = 0; t < T; ++t) {
     const size_t row = (size_t)t * BN + c;
-    h0[row * 64 + o] = et[t * 64 + o] + base;
-    if (o < 3) { xr[row * 3 + o] = x[(size_t)c * 3 + o]; vr[row * 3 + o] = v[(size_t)c * 3 + o]; }
+    const size_t src = frames ? row : (size_t)c;
+    h0[row * 64 + o] = et[t * 64 + o] + (frames ? hin_part(row) : base);
+    if (o < 3) { xr[row * 3 + o] = x[src * 3 + o]; vr[row * 3 + o] = v[src * 3 + o]; }
   }
 }
 
 // emb_in[t*BN + c] = [h_in[c], temb(t_out[c % Bt][t])]  (the embedding Linear's input rows)
+// rows [h_in | temb(t_out)], or [h_in | temb(t_in) | temb(t_out)] when t_in != null (egno.py:77-79)
 __global__ void emb_in_kernel(int BN, int T, int din, int dim, int Bt, const float* hin, const float* t_out,
-                              float* emb_in) {
+                              float* emb_in, const float* t_in, int frames) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  const int w = din + dim;
+  const int w = din + (t_in ? 2 : 1) * dim;
   if (idx >= BN * T * w) return;
   const int k = idx % w, row = idx / w;
   const int t = row / BN, c = row - t * BN;
   float val;
   if (k < din) {
-    val = hin[(size_t)c * din + k];
+    val = hin[(size_t)(frames ? row : c) * din + k];
   } else {
-    const int kk = k - din, half = dim / 2;
+    const int kq = k - din, which = kq / dim, kk = kq - which * dim, half = dim / 2;
     const float scale = (float)(log(10000.0) / (double)(half - 1));
-    const float tv = t_out[(size_t)(c % Bt) * T + t];
+    const float tv = ((t_in && which == 0) ? t_in : t_out)[(size_t)(c % Bt) * T + t];
     const int j = kk < half ? kk : kk - half;
     const float arg = tv * expf((float)j * -scale);
     val = kk < half ? sinf(arg) : cosf(arg);
@@ -1127,15 +1135,14 @@ int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
 // Writes gx, gv and per-thread weight-gradient terms part[(c*3+d)][i][o][m][2].
 __global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x, const float* v, const float* lm,
                                   const float* gxo, const float* gvo, const float* w, float* gx, float* gv,
-                                  float* part) {
+                                  float* part, int frames) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= BN * 3) return;
   const int c = idx / 3, d = idx - 3 * c;
   float X[2][TMAX], G[2][TMAX], GO[2][TMAX];
-  const float lmv = lm[(size_t)c * 3 + d];
   for (int t = 0; t < T; ++t) {
     const size_t row = (size_t)t * BN + c;
-    X[0][t] = x[row * 3 + d] - lmv;
+    X[0][t] = x[row * 3 + d] - lm[(frames ? row : (size_t)c) * 3 + d];
     X[1][t] = v[row * 3 + d];
     GO[0][t] = G[0][t] = gxo[row * 3 + d];
     GO[1][t] = G[1][t] = gvo[row * 3 + d];
@@ -1397,9 +1404,13 @@ size_t nonode_egno_train_state_bytes(int B, int N, int T, int n_layers, int in_n
   return train_state(nullptr, B, N, T, n_layers, in_node, time_emb_dim).floats * sizeof(float);
 }
 
-int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
-                              int modes, int Bt, const float* x, const float* h, const float* v,
-                              const float* loc_mean, const float* edge_fea, const float* t_out,
+}  // extern "C"
+
+namespace {
+// frames = 1: per-frame inputs (num_inputs > 1) and, with t_in, the input-time embedding columns
+int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                              int time_emb_dim, int modes, int Bt, const float* x, const float* h, const float* v,
+                              const float* loc_mean, const float* edge_fea, const float* t_in, const float* t_out,
                               const float* emb_w, const float* emb_b, const float* const* blobs,
                               const float* const* tconv_blobs, const float* const* tconvx_w, float* x_out,
                               float* v_out, float* h_out, void* state, size_t state_bytes, void* workspace,
@@ -1411,7 +1422,8 @@ int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, in
   if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_blobs || !tconvx_w ||
       !x_out || !v_out || !h_out || !state || !workspace)
     return fail(NONODE_EINVAL, "egno_forward_train: null pointer");
-  if (state_bytes < nonode_egno_train_state_bytes(B, N, T, n_layers, in_node, time_emb_dim))
+  const int emb_cols = (t_in ? 2 : 1) * time_emb_dim;   // time-embedding columns of the embedding Linear
+  if (state_bytes < nonode_egno_train_state_bytes(B, N, T, n_layers, in_node, emb_cols))
     return fail(NONODE_EINVAL, "egno_forward_train: state too small");
   if (workspace_bytes < nonode_egno_workspace_bytes(B, N, T, Bt))
     return fail(NONODE_EINVAL, "egno_forward_train: workspace too small");
@@ -1419,30 +1431,30 @@ int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, in
   const int BN = B * N;
   const size_t n = (size_t)BN * T;
   const int L = n_layers;
-  TrainState st = train_state(state, B, N, T, L, in_node, time_emb_dim);
+  TrainState st = train_state(state, B, N, T, L, in_node, emb_cols);
   float* etab = (float*)workspace + n * 64 + n * 3;
-  const int emb_ld = in_node + time_emb_dim;
+  const int emb_ld = in_node + emb_cols;
   {
     const int tot = Bt * T * 64;
     hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim, t_out,
-                       emb_w, emb_ld, emb_b, etab);
+                       emb_w, emb_ld, emb_b, etab, t_in);
     if (int rc = check_launch("temb_kernel")) return rc;
     hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
-                       etab, x, v, st.hs, st.xs, st.vs);
+                       etab, x, v, st.hs, st.xs, st.vs, frames);
     if (int rc = check_launch("h0_kernel")) return rc;
     const size_t tot2 = n * emb_ld;
     hipLaunchKernelGGL(emb_in_kernel, dim3((unsigned)((tot2 + 255) / 256)), dim3(256), 0, s, BN, T, in_node,
-                       time_emb_dim, Bt, h, t_out, st.emb_in);
+                       time_emb_dim, Bt, h, t_out, st.emb_in, t_in, frames);
     if (int rc = check_launch("emb_in_kernel")) return rc;
   }
   for (int l = 0; l < L; ++l) {
     TconvArgs a{};
     a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
-    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l];
+    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l]; a.frames = frames;
     a.h = st.hs + l * n * 64; a.x = st.xs + l * n * 3; a.v = st.vs + l * n * 3; a.lm = loc_mean;
     a.h_out = st.he + l * n * 64; a.x_out = st.xe + l * n * 3; a.v_out = st.ve + l * n * 3;
     if (int rc = launch_tconv(false, a, s)) return rc;
-    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, B, a.h_out, a.x_out, a.v_out, edge_fea, blobs[l], 0.f, 1.f,
+    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, a.h_out, a.x_out, a.v_out, edge_fea, blobs[l], 0.f, 1.f,
                                     0, st.hs + (l + 1) * n * 64, st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
                                     st.Ms + l * n * 64, st.Fs + l * n * 4))
       return rc;
@@ -1453,13 +1465,46 @@ int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, in
   hipMemcpyAsync(h_out, st.hs + L * n * 64, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
   return check_launch("egno_forward_train copies");
 }
+}  // namespace
+
+extern "C" {
+
+int nonode_egno_forward_train(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                              int modes, int Bt, const float* x, const float* h, const float* v,
+                              const float* loc_mean, const float* edge_fea, const float* t_out,
+                              const float* emb_w, const float* emb_b, const float* const* blobs,
+                              const float* const* tconv_blobs, const float* const* tconvx_w, float* x_out,
+                              float* v_out, float* h_out, void* state, size_t state_bytes, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+  return egno_forward_train_impl(0, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v,
+                                 loc_mean, edge_fea, nullptr, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w,
+                                 x_out, v_out, h_out, state, state_bytes, workspace, workspace_bytes, stream);
+}
+
+int nonode_egno_forward_train_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                                     int time_emb_dim, int modes, int Bt, const float* x, const float* h,
+                                     const float* v, const float* loc_mean, const float* edge_fea,
+                                     const float* t_in, const float* t_out, const float* emb_w, const float* emb_b,
+                                     const float* const* blobs, const float* const* tconv_blobs,
+                                     const float* const* tconvx_w, float* x_out, float* v_out, float* h_out,
+                                     void* state, size_t state_bytes, void* workspace, size_t workspace_bytes,
+                                     void* stream) {
+  return egno_forward_train_impl(1, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v,
+                                 loc_mean, edge_fea, t_in, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w,
+                                 x_out, v_out, h_out, state, state_bytes, workspace, workspace_bytes, stream);
+}
 
 size_t nonode_egno_backward_workspace_bytes(int B, int N, int T, int modes) {
   return bwd_ws(nullptr, B, N, T, effective_modes(T, modes)).floats * sizeof(float);
 }
 
-int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
-                         int modes, int Bt, const float* loc_mean, const float* edge_fea,
+}  // extern "C"
+
+namespace {
+// frames = 1: per-frame loc_mean / edge_fea (num_inputs > 1); emb_cols: time-embedding columns of
+// the embedding Linear (time_emb_dim, or 2 time_emb_dim with the input-time embedding)
+int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                         int time_emb_dim, int modes, int Bt, const float* loc_mean, const float* edge_fea,
                          const float* const* bblobs, const float* const* tconv_w, const float* const* tconvx_w,
                          const void* state, const float* g_x, const float* g_v, const float* g_h,
                          const nonode_layer_grads* layer_grads, float* const* g_tconv, float* const* g_tconvx,
@@ -1477,7 +1522,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
   const int BN = B * N, L = n_layers, ne = n_edge_feat;
   const size_t n = (size_t)BN * T;
   const long long E = (long long)n * (N - 1);
-  TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, time_emb_dim);
+  TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, emb_cols);
   BwdWs w = bwd_ws(workspace, B, N, T, M);
   Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
   // grads of the final outputs
@@ -1514,7 +1559,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
       EdgeBwdArgs ea;
       static const int ebdbg = getenv("NONODE_EBDBG") ? atoi(getenv("NONODE_EBDBG")) : 0;
       ea.dbg = ebdbg;
-      ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
+      ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = frames ? T * B : B; ea.ct = 0; ea.s_max = 0;
       ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
       ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
@@ -1550,7 +1595,7 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
     const int nxt = cur ^ 1;
     hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes,
                        st.xs + l * n * 3, st.vs + l * n * 3, loc_mean, w.gxe, w.gve, tconvx_w[l], w.gx[nxt],
-                       w.gv[nxt], w.xpart);
+                       w.gv[nxt], w.xpart, frames);
     if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
     {
       // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M stay zero)
@@ -1592,9 +1637,41 @@ int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_e
     gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
   }
   // ---- embedding Linear (egno.py:63-76): dW = sum_rows gh0 (x) [h_in, temb], db = sum gh0 ----
-  const int emb_ld = in_node + time_emb_dim;
-  if (int rc = gemm(gh, 64, 64, st.emb_in, emb_ld, emb_ld, (long long)n, g_emb_w, emb_ld, 0, g_emb_b)) return rc;
+  const int emb_ld = in_node + emb_cols;
+  // (in column blocks of <= 64: the multi-input embedding has in_node + 2 time_emb_dim inputs)
+  for (int c0 = 0; c0 < emb_ld; c0 += 64) {
+    const int nc = emb_ld - c0 < 64 ? emb_ld - c0 : 64;
+    if (int rc = gemm(gh, 64, 64, st.emb_in + c0, emb_ld, nc, (long long)n, g_emb_w, emb_ld, c0,
+                      c0 == 0 ? g_emb_b : nullptr))
+      return rc;
+  }
   return NONODE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int nonode_egno_backward(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                         int modes, int Bt, const float* loc_mean, const float* edge_fea,
+                         const float* const* bblobs, const float* const* tconv_w, const float* const* tconvx_w,
+                         const void* state, const float* g_x, const float* g_v, const float* g_h,
+                         const nonode_layer_grads* layer_grads, float* const* g_tconv, float* const* g_tconvx,
+                         float* g_emb_w, float* g_emb_b, void* workspace, size_t workspace_bytes, void* stream) {
+  return egno_backward_impl(0, time_emb_dim, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt,
+                            loc_mean, edge_fea, bblobs, tconv_w, tconvx_w, state, g_x, g_v, g_h, layer_grads, g_tconv,
+                            g_tconvx, g_emb_w, g_emb_b, workspace, workspace_bytes, stream);
+}
+
+int nonode_egno_backward_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat, int time_emb_dim,
+                                int with_t_in, int modes, int Bt, const float* loc_mean, const float* edge_fea,
+                                const float* const* bblobs, const float* const* tconv_w,
+                                const float* const* tconvx_w, const void* state, const float* g_x, const float* g_v,
+                                const float* g_h, const nonode_layer_grads* layer_grads, float* const* g_tconv,
+                                float* const* g_tconvx, float* g_emb_w, float* g_emb_b, void* workspace,
+                                size_t workspace_bytes, void* stream) {
+  return egno_backward_impl(1, (with_t_in ? 2 : 1) * time_emb_dim, B, N, T, n_layers, in_node, n_edge_feat,
+                            time_emb_dim, modes, Bt, loc_mean, edge_fea, bblobs, tconv_w, tconvx_w, state, g_x, g_v,
+                            g_h, layer_grads, g_tconv, g_tconvx, g_emb_w, g_emb_b, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

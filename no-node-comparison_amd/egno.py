@@ -78,8 +78,7 @@ class EGNO(nn.Module):
 
     Supported configuration (the one model_confs.yaml:1-17 and main.py:133-134 build):
     with_v=True, flat=False, norm=False, use_time_conv=True, hidden_nf=64, SiLU activation, any
-    num_inputs (num_inputs > 1: inference only). Anything else raises NotImplementedError at
-    construction.
+    num_inputs. Anything else raises NotImplementedError at construction.
     """
 
     def __init__(self, n_layers, in_node_nf, in_edge_nf, hidden_nf, activation=nn.SiLU(), device='cpu',
@@ -222,8 +221,6 @@ class EGNO(nn.Module):
         edge_fea [I, E, in_edge_nf] (prepare_inputs, main_simulation_simple_no.py:313-327),
         timesteps_in [B, I], timesteps_out [B, T]. Frame t uses input frame_inputs(T)[t]
         (egno.py:44-49, 80-96); its embedding adds the input time's embedding (egno.py:77-79)."""
-        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("EGNO training with num_inputs > 1 is not implemented on the MI355X kernels")
         I, T = self.num_inputs, self.num_timesteps
         if x.dim() != 3 or x.shape[0] != I or h.dim() != 3 or h.shape[0] != I:
             raise ValueError(f"num_inputs={I}: x, v, loc_mean must be [{I}, BN, 3] and h [{I}, BN, F]")
@@ -247,6 +244,10 @@ class EGNO(nn.Module):
             xf, hf, vf, lmf, eff = (per_frame(t) for t in (x, h, v, loc_mean, edge_fea))
             t_in = f32(timesteps_in)[:, fidx].contiguous()
             t_out = f32(timesteps_out).contiguous()
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            from .autograd import egno_forward_train
+            return egno_forward_train(self, xf, hf, eff, vf, lmf, t_out, B, N, t_in=t_in)
+        with torch.no_grad():
             return self._launch_forward(_lib.lib().nonode_egno_forward_frames, B, N, xf, hf, vf, lmf, eff, t_out,
                                         t_in=t_in)
 

@@ -26,7 +26,8 @@ What each fixture pins (reference file:line):
                       (synthetic_sim.py:360-404).
   egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8 (5 spectral modes incl. the
                       Nyquist bin; model_confs.yaml:12's alternative), seed-0 weights.
-  egno_multi.npz      EGNO.forward with num_inputs=3 (multi-input branch, egno.py:44-96), seed-0 weights.
+  egno_multi.npz      EGNO.forward with num_inputs=3 (multi-input branch, egno.py:44-96), seed-0 weights,
+                      and one training step's parameter gradients.
   segno_multi.npz     SEGNO live forward with num_inputs=3, multiple_agg='attn' (model.py:53-92,
                       104-139) and the discarded last forward_step.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
@@ -400,6 +401,20 @@ def make_egno_multi(B=2, N=5, T=10, I=3):
         "in::t_in": _np(t_in), "in::t_out": _np(t_out),
         "out::x": _np(x_out), "out::v": _np(v_out), "out::h": _np(h_out),
     })
+    # one training step's gradients through the multi-input model (main_simulation_simple_no.py:267-280)
+    model.train()
+    model.zero_grad()
+    loc_true = torch.tensor(loc_all[:, start + 1:start + 1 + T]).transpose(1, 2)  # [B, N, T, 3]
+    loc_pred, _, _ = model(loc_p, nodes, edges, edge_attr, v=vel_p, loc_mean=loc_mean,
+                           timesteps_in=t_in, timesteps_out=t_out)
+    loc_pred = loc_pred.reshape(T, -1, 3).transpose(0, 1)
+    loc_pred = _to_dense_batch(loc_pred, torch.arange(B).repeat_interleave(N))[0]
+    loss = torch.nn.MSELoss(reduction="none")(loc_pred, loc_true).mean((0, 1, 3)).mean()
+    loss.backward()
+    fx.update({"grad::" + k: (_np(p.grad) if p.grad is not None else np.zeros(tuple(p.shape), np.float32))
+               for k, p in model.named_parameters()})
+    fx["out::loss"] = _np(loss)
+    fx["in::loc_true"] = _np(loc_true)
     np.savez_compressed(os.path.join(HERE, "egno_multi.npz"), **fx)
 
 

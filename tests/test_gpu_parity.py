@@ -380,10 +380,6 @@ def test_egno_multi_input_matches_reference_golden():
     assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
     assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
     assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL
-    m.train()
-    with pytest.raises(NotImplementedError):
-        m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
-          loc_mean=_dev(fx["in::loc_mean"]), timesteps_in=_dev(fx["in::t_in"]), timesteps_out=_dev(fx["in::t_out"]))
 
 
 def test_segno_multi_input_attn_matches_reference_golden():

@@ -119,3 +119,28 @@ def test_egno_adam_step_runs_and_repacks():
 
 
 DEV_ = "cuda"
+
+
+def test_egno_multi_input_gradients_match_reference_golden():
+    """num_inputs=3 training step (nonode_egno_forward_train_frames / nonode_egno_backward_frames):
+    loss and every parameter gradient against the reference's autograd (tests/golden/egno_multi.npz)."""
+    fx = load_golden("egno_multi")
+    B, N, T, I = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"]), int(fx["cfg::I"])
+    torch.manual_seed(0)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                 num_timesteps=T, time_emb_dim=32, num_inputs=I, device=_dev(fx["in::x"]).device).train()
+    m.zero_grad(set_to_none=True)
+    x, _, _ = m(_dev(fx["in::x"]), _dev(fx["in::h"]), [_dev(fx["in::row"]), _dev(fx["in::col"])],
+                _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]), loc_mean=_dev(fx["in::loc_mean"]),
+                timesteps_in=_dev(fx["in::t_in"]), timesteps_out=_dev(fx["in::t_out"]))
+    loss, _ = _loss_like_reference(x, _dev(fx["in::loc_true"]), T, B, N)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(float(loss.detach()) - float(fx["out::loss"])) <= 1e-5 * abs(float(fx["out::loss"]))
+    for k, p in m.named_parameters():
+        ref = fx["grad::" + k]
+        got = p.grad.detach().cpu().numpy()
+        if np.abs(ref).max() == 0:
+            assert np.abs(got).max() <= 1e-6, k
+        else:
+            assert maxnorm_rel(got, ref) < GTOL, (k, maxnorm_rel(got, ref))
