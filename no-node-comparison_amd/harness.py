@@ -28,14 +28,14 @@ def get_edges(batch_size, n_nodes, device="cpu"):
 
 @torch.no_grad()
 def prepare_inputs(loc, vel, edge_attr_o, edges, n_nodes, num_inputs=1, charges=None, t_in=None):
-    """main_simulation_simple_no.py:311-339 for num_inputs == 1 (nonode_prepare_inputs).
+    """main_simulation_simple_no.py:311-339 (nonode_prepare_inputs; num_inputs > 1 per input slot).
 
     loc, vel: [B, N, 3] (one frame) or [F, B, N, 3] with ``t_in`` [B] choosing frame t_in-1 per
     sample (rollout_fn's loc_all[timesteps_in.T - 1]). edges must be the dataset's fully connected
     list (only its size is used: the kernel indexes pairs implicitly). Returns
     (loc [BN,3], vel [BN,3], edge_attr [E, n_eo+1], nodes [BN, 1(+1)], loc_mean [BN,3])."""
-    if num_inputs != 1:
-        raise NotImplementedError("prepare_inputs: num_inputs > 1")
+    if num_inputs > 1:
+        return _prepare_inputs_multi(loc, vel, edge_attr_o, edges, n_nodes, num_inputs, charges)
     _lib.require_device(loc, vel, edge_attr_o, charges)
     if loc.dim() == 3:
         loc, vel = loc.unsqueeze(0), vel.unsqueeze(0)
@@ -62,6 +62,54 @@ def prepare_inputs(loc, vel, edge_attr_o, edges, n_nodes, num_inputs=1, charges=
                                        n_eo, _lib.ptr(x), _lib.ptr(v), _lib.ptr(nodes), _lib.ptr(ea), _lib.ptr(lm),
                                        _lib.stream_of(loc)))
     return x, v, ea, nodes, lm
+
+
+def _prepare_inputs_multi(loc, vel, edge_attr_o, edges, n_nodes, num_inputs, charges):
+    """main_simulation_simple_no.py:313-327 (num_inputs = I > 1), literally: loc, vel are transposed
+    on their first two axes and reshaped to I slots of B*N rows ([B, I, N, 3] from the loader gives
+    one slot per input); each slot is featurised like a single input (per-graph mean, |v| (+ q),
+    [edge_attr_o, |x_i - x_j|^2]). Returns x, v, loc_mean [I, BN, 3], edge_attr [I, E, n_eo+1],
+    nodes [I, BN, 1(+1)]."""
+    I = num_inputs
+    lt = loc.transpose(0, 1).contiguous().reshape(I, -1, n_nodes, 3)
+    vt = vel.transpose(0, 1).contiguous().reshape(I, -1, n_nodes, 3)
+    outs = [prepare_inputs(lt[i], vt[i], edge_attr_o, edges, n_nodes, 1, charges) for i in range(I)]
+    x, v, ea, nodes, lm = (torch.stack([o[k] for o in outs]) for k in range(5))
+    return x, v, ea, nodes, lm
+
+
+@torch.no_grad()
+def egno_rollout_multi(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean, n_nodes, traj_len,
+                       batch_size, charges=None, num_steps=10, timesteps_in=None, timesteps_out=None,
+                       energy_dataset=None):
+    """rollout_fn (main_simulation_simple_no.py:342-384) for num_inputs > 1: per segment the HIP
+    forward, then the frames timesteps_in - 1 of each sample become the next inputs and go through
+    prepare_inputs exactly as the reference passes them ([I, B, N, 3], which prepare_inputs
+    transposes). Returns (loc_preds [traj_len*T, BN, 3], energies, energies_allsteps) like
+    egno_rollout."""
+    T = model.num_timesteps
+    B, N = batch_size, n_nodes
+    t_in = timesteps_in if timesteps_in.dim() == 2 else timesteps_in.unsqueeze(-1)
+    bidx = torch.arange(B, device=loc.device).unsqueeze(0).expand(t_in.shape[1], -1)
+    preds = torch.empty(traj_len * T, B * N, 3, device=loc.device)
+    en_all = []
+    for i in range(traj_len):
+        t_out = timesteps_out[:, i * T:(i + 1) * T] - i * T
+        x, v, _ = model(loc, nodes, edges, edge_attr, v=vel, loc_mean=loc_mean, timesteps_out=t_out,
+                        timesteps_in=t_in)
+        preds[i * T:(i + 1) * T] = x.reshape(T, B * N, 3)
+        loc_all, vel_all = x.view(T, B, N, 3), v.view(T, B, N, 3)
+        sel = (t_in.T - 1).long()
+        loc, vel = loc_all[sel, bidx], vel_all[sel, bidx]
+        loc, vel, edge_attr, nodes, loc_mean = prepare_inputs(loc, vel, edge_attr_o, edges, N, t_in.shape[1],
+                                                              charges)
+        if energy_dataset is not None:
+            en_all.append(conserved_energy(energy_dataset, loc_all.reshape(T, B * N, 3),
+                                           vel_all.reshape(T, B * N, 3), charges, B))
+    if energy_dataset is None:
+        return preds, None, None
+    en_all = torch.cat(en_all).unsqueeze(-1)
+    return preds, en_all[T - 1::T], en_all
 
 
 @torch.no_grad()
@@ -93,6 +141,10 @@ def egno_rollout(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean
     from .egno import EGNO
     if not isinstance(model, EGNO):
         raise TypeError("egno_rollout drives no_node_comparison_amd.EGNO (its packed weights)")
+    if model.num_inputs > 1:
+        return egno_rollout_multi(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean, n_nodes,
+                                  traj_len, batch_size, charges, num_steps, timesteps_in, timesteps_out,
+                                  energy_dataset)
     T = model.num_timesteps
     if num_steps != T:
         raise ValueError("rollout_fn reshapes each segment into num_steps == model.num_timesteps frames")

@@ -27,7 +27,8 @@ What each fixture pins (reference file:line):
   egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8 (5 spectral modes incl. the
                       Nyquist bin; model_confs.yaml:12's alternative), seed-0 weights.
   egno_multi.npz      EGNO.forward with num_inputs=3 (multi-input branch, egno.py:44-96), seed-0 weights,
-                      and one training step's parameter gradients.
+                      and one training step's parameter gradients; egno_multi_rollout.npz: its
+                      2-segment rollout_fn with energies.
   segno_multi.npz     SEGNO live forward with num_inputs=3, multiple_agg='attn' (model.py:53-92,
                       104-139) and the discarded last forward_step.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
@@ -416,6 +417,24 @@ def make_egno_multi(B=2, N=5, T=10, I=3):
     fx["out::loss"] = _np(loss)
     fx["in::loc_true"] = _np(loc_true)
     np.savez_compressed(os.path.join(HERE, "egno_multi.npz"), **fx)
+
+    # ---- multi-input rollout_fn (main_simulation_simple_no.py:342-384), 2 segments, energies ----
+    class _DS:
+        def energy_fun(self, loc, vel, edges, batch=None):
+            return ref_utils.conserved_energy_fun("charged", loc, vel, edges, batch=batch)
+
+    model.eval()
+    traj_len = 2
+    t_out_full = torch.arange(1, T * traj_len + 1).repeat(B, 1)
+    with torch.no_grad():
+        preds, energies, energies_all = egno_main.rollout_fn(
+            model, nodes, loc_p, edges, vel_p, eao, edge_attr, loc_mean, N, traj_len, B,
+            charges=torch.tensor(q), num_steps=T, timesteps_in=t_in.clone(), timesteps_out=t_out_full.clone(),
+            energy_fun=_DS().energy_fun)
+    np.savez_compressed(os.path.join(HERE, "egno_multi_rollout.npz"), **{
+        "cfg::traj_len": np.array(traj_len), "raw::edge_attr_o": _np(eao), "raw::charges": q,
+        "in::t_out": _np(t_out_full), "out::loc_preds": _np(preds), "out::energies": _np(energies),
+        "out::energies_all": _np(energies_all)})
 
 
 def make_segno_multi(B=2, N=5, T=10, I=3):

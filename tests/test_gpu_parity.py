@@ -399,3 +399,24 @@ def test_segno_multi_input_attn_matches_reference_golden():
         assert maxnorm_rel(x.cpu(), fx[pre + "::x"]) < TOL
         assert maxnorm_rel(h.cpu(), fx[pre + "::h"]) < TOL
         assert maxnorm_rel(v.cpu(), fx[pre + "::v"]) < TOL
+
+
+def test_egno_multi_input_rollout_matches_reference_golden():
+    """rollout_fn with num_inputs=3 (harness.egno_rollout -> egno_rollout_multi): each segment's last
+    frames become the next inputs through the multi-input prepare_inputs, as the reference does."""
+    fx = load_golden("egno_multi")
+    ro = load_golden("egno_multi_rollout")
+    B, N, T, I = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"]), int(fx["cfg::I"])
+    Lr = int(ro["cfg::traj_len"])
+    torch.manual_seed(0)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                 num_timesteps=T, time_emb_dim=32, num_inputs=I, device=DEV).eval()
+    edges = pkg.harness.get_edges(B, N, DEV)
+    preds, en, en_all = pkg.harness.egno_rollout(
+        m, _dev(fx["in::h"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(ro["raw::edge_attr_o"]),
+        _dev(fx["in::edge_attr"]), _dev(fx["in::loc_mean"]), N, Lr, B, charges=_dev(ro["raw::charges"]),
+        num_steps=T, timesteps_in=_dev(fx["in::t_in"]), timesteps_out=_dev(ro["in::t_out"]), energy_dataset="charged")
+    assert maxnorm_rel(preds[:T].cpu(), ro["out::loc_preds"][:T]) < TOL
+    assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < 1e-4
+    assert maxnorm_rel(en_all.cpu(), ro["out::energies_all"]) < 1e-4
+    assert maxnorm_rel(en.cpu(), ro["out::energies"]) < 1e-4
