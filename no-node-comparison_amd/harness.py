@@ -188,8 +188,9 @@ def egno_rollout(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean
 
 @torch.no_grad()
 def segno_rollout(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps=10, charges=None,
-                  energy_dataset=None, batch_size=None):
-    """rollout_fn (train_nbody.py:200-236), num_prev == 1, as one native call.
+                  energy_dataset=None, batch_size=None, in_steps=None):
+    """rollout_fn (train_nbody.py:200-236): num_prev == 1 as one native call; several previous
+    frames (loc, vel [BN, I, 3], in_steps) as a segment loop over SEGNO's multi-input forward.
 
     Returns (loc_preds [traj_len, BN, 3], energies [traj_len, B, 1] or None)."""
     from .graph import check_full_graph
@@ -198,6 +199,9 @@ def segno_rollout(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps
         raise TypeError("segno_rollout drives no_node_comparison_amd.SEGNO (its packed weights)")
     if model.bug_compat:
         raise ValueError("segno_rollout integrates (bug_compat=True would return the inputs every segment)")
+    if loc.dim() == 3:
+        return _segno_rollout_multi(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps, charges,
+                                    energy_dataset, in_steps)
     _lib.require_device(loc, h, vel, edge_attr, charges, model.embedding.weight)
     BN = loc.shape[0]
     B, N = check_full_graph(edge_index, BN)
@@ -224,3 +228,38 @@ def segno_rollout(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps
         float(model.coords_weight), int(bool(model.recurrent)), _lib.ptr(preds), _lib.ptr(en), _lib.ptr(ws), ws_bytes,
         _lib.stream_of(x)))
     return preds, (en.unsqueeze(-1) if en is not None else None)
+
+
+@torch.no_grad()
+def _segno_rollout_multi(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps, charges, energy_dataset,
+                         in_steps):
+    """train_nbody.py:200-236 with num_prev = I > 1: each segment's prediction is appended to the
+    window of the last I frames (the oldest dropped), |v| and the last frame's distances are
+    recomputed, and in_steps shifts by the segment's substeps (:221-233)."""
+    from .graph import check_full_graph
+    if in_steps is None:
+        raise ValueError("a multi-input SEGNO rollout needs in_steps (train_nbody.py:114)")
+    BN = loc.shape[0]
+    B, N = check_full_graph(edge_index, BN)
+    steps = list(num_steps) if isinstance(num_steps, (list, tuple)) else [int(num_steps)] * traj_len
+    if len(steps) != traj_len:
+        raise ValueError("num_steps should be a list of length traj_len")
+    rows, cols = (t.long() for t in edge_index)
+    q = _f32(charges).reshape(-1)
+    prod = (q[rows] * q[cols]).reshape(-1, 1)
+    preds = torch.empty(traj_len, BN, 3, device=loc.device)
+    en = []
+    loc, vel = _f32(loc), _f32(vel)
+    for i, T in enumerate(steps):
+        loc_p, _, vel_p = model(h, loc, edge_index, vel, edge_attr, T=T, in_steps=in_steps)
+        if energy_dataset is not None:
+            en.append(conserved_energy(energy_dataset, loc_p, vel_p, charges, B))
+        preds[i] = loc_p
+        loc = torch.cat((loc[:, 1:, :], loc_p.unsqueeze(1)), dim=1)
+        vel = torch.cat((vel[:, 1:, :], vel_p.unsqueeze(1)), dim=1)
+        h = torch.sqrt(torch.sum(vel ** 2, dim=-1)).unsqueeze(-1)
+        loc_dist = torch.sum((loc[rows, -1, :] - loc[cols, -1, :]) ** 2, 1).unsqueeze(1)
+        st = in_steps.tolist() if torch.is_tensor(in_steps) else list(in_steps)
+        in_steps = torch.tensor(st[1:] + [T], device=loc.device) - T
+        edge_attr = torch.cat([prod, loc_dist], 1)
+    return preds, (torch.stack(en).unsqueeze(-1) if en else None)

@@ -30,7 +30,8 @@ What each fixture pins (reference file:line):
                       and one training step's parameter gradients; egno_multi_rollout.npz: its
                       2-segment rollout_fn with energies.
   segno_multi.npz     SEGNO live forward with num_inputs=3, multiple_agg='attn' (model.py:53-92,
-                      104-139) and the discarded last forward_step.
+                      104-139) and the discarded last forward_step; segno_multi_rollout.npz: the
+                      2-segment num_prev = 3 rollout_fn through the integrator.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
                       torch.manual_seed(0) (RNG-consumption order of the constructors).
 """
@@ -473,6 +474,26 @@ def make_segno_multi(B=2, N=5, T=10, I=3):
         "last::x": _np(lx), "last::h": _np(lh), "last::v": _np(lv),
     })
     np.savez_compressed(os.path.join(HERE, "segno_multi.npz"), **fx)
+
+    # ---- multi-input rollout_fn (train_nbody.py:200-236, num_prev = 3), through a wrapper whose
+    # call runs the live forward and then the forward_step it discards (the integrator result) ----
+    class _Integrated(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
+            xo, ho, vo = self.m(his, x, edges, v, edge_attr, T=T, in_steps=in_steps)
+            return self.m.forward_step(ho, xo, edges, vo, edge_attr, T=T)
+
+    batch = torch.arange(B).repeat_interleave(N)
+    with torch.no_grad():
+        preds, energies = segno_train.rollout_fn(
+            _Integrated(model), h, loc, edges, vel, edge_attr, batch, 2, num_steps=[T, T // 2], num_prev=I,
+            charges=charges, energy_fun=lambda l, v, e, batch=None: ref_utils.conserved_energy_fun(
+                "charged", l, v, e, batch=batch), in_steps=in_steps.clone())
+    np.savez_compressed(os.path.join(HERE, "segno_multi_rollout.npz"), **{
+        "out::loc_preds": _np(preds), "out::energies": _np(energies), "raw::charges": _np(charges)})
 
 
 if __name__ == "__main__":

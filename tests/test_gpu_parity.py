@@ -420,3 +420,22 @@ def test_egno_multi_input_rollout_matches_reference_golden():
     assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < 1e-4
     assert maxnorm_rel(en_all.cpu(), ro["out::energies_all"]) < 1e-4
     assert maxnorm_rel(en.cpu(), ro["out::energies"]) < 1e-4
+
+
+def test_segno_multi_input_rollout_matches_reference_golden():
+    """rollout_fn with num_prev=3 (train_nbody.py:200-236) through the integrator, 2 segments of
+    10 and 5 substeps, with energies."""
+    fx = load_golden("segno_multi")
+    ro = load_golden("segno_multi_rollout")
+    T = int(fx["cfg::T"])
+    m = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True, multiple_agg="attn",
+                  device=DEV).eval()
+    m.load_state_dict({k: torch.tensor(v) for k, v in params_of(fx).items()})
+    edges = [_dev(fx["in::row"]), _dev(fx["in::col"])]
+    preds, en = pkg.harness.segno_rollout(m, _dev(fx["in::his"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]),
+                                          _dev(fx["in::edge_attr"]), 2, num_steps=[T, T // 2],
+                                          charges=_dev(ro["raw::charges"]), energy_dataset="charged",
+                                          in_steps=_dev(fx["in::in_steps"]))
+    assert maxnorm_rel(preds[0].cpu(), ro["out::loc_preds"][0]) < TOL
+    assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < 1e-4
+    assert maxnorm_rel(en.cpu(), ro["out::energies"]) < 1e-4
