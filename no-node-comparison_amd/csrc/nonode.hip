@@ -1138,9 +1138,11 @@ __global__ void tconv_pack_kernel(const float* w, int Mfull, int M, int T, float
   out[d] = sgn * cm / (float)T * w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
 }
 
-// One workgroup (4 waves) per tile of 16 columns (b, n). Wave w: DFT of input channels 16w..16w+15,
-// then the mixing MFMAs for output channels 16w..16w+15, then LeakyReLU + residual for those
-// channels over all T. Lanes hold (column e = lane & 15, channels 16w + 4g + q).
+// One workgroup (4 waves) per tile of 16 columns (b, n). Wave w: DFT over T of columns 4w..4w+3
+// (all 64 channels; each f4 access of the wave covers 4 whole rows), spectrum to LDS; then the
+// mixing MFMAs for output channels 16w..16w+15 of all 16 columns (lanes: column e = lane & 15,
+// channels 16w + 4g + q); the mixed spectrum goes back through LDS, and wave w finishes columns
+// 4w..4w+3: inverse DFT, LeakyReLU + residual (h kept in registers from the DFT), row stores.
 // MM: compile-time bound on the number of modes (M <= MM), so the mode loops, the LDS spectrum and
 // the register arrays are sized for the configuration at hand
 template <bool FIRST, int MM>
@@ -1155,10 +1157,17 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     sCos[m * TMAX + t] = (float)cospi(ang);
     sSin[m * TMAX + t] = (float)sinpi(ang);
   }
+  // x / v lanes and the mixing MFMAs: column e = lane & 15 of the tile
   const int col = blockIdx.x * 16 + e;
   const bool cvalid = col < BN;
   const int c = cvalid ? col : BN - 1;
-  const int ch = 16 * wave + 4 * g;      // this lane's 4 channels: ch .. ch+3
+  // h streaming (steps 1 and 3): wave w owns columns 4w .. 4w+3 of the tile, lane (cl = lane >> 4,
+  // cq = lane & 15) channels 4cq .. 4cq+3 of column 4w + cl, so one f4 load / store instruction of a
+  // wave moves 4 whole consecutive 256-byte rows (1 KB contiguous per frame)
+  const int ecol = 4 * wave + (lane >> 4), chs = 4 * (lane & 15);
+  const int scol = blockIdx.x * 16 + ecol;
+  const bool svalid = scol < BN;
+  const int sc = svalid ? scol : BN - 1;
   f4 base = {0.f, 0.f, 0.f, 0.f};
   const float* et = nullptr;
   // emb_w[:, :din] h_in of row r (the node-feature part of the embedding Linear)
@@ -1167,31 +1176,33 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     for (int k = 0; k < p.din; ++k) {
       const float hv = p.hin[r * p.din + k];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = fmaf(p.emb_w[(ch + q) * p.emb_ld + k], hv, b[q]);
+      for (int q = 0; q < 4; ++q) b[q] = fmaf(p.emb_w[(chs + q) * p.emb_ld + k], hv, b[q]);
     }
     return b;
   };
   if (FIRST) {
-    if (!p.frames) base = hin_part((size_t)c);
-    et = p.etab + ((size_t)(c % p.Bt) * T) * 64 + ch;
+    if (!p.frames) base = hin_part((size_t)sc);
+    et = p.etab + ((size_t)(sc % p.Bt) * T) * 64 + chs;
   }
   auto hval = [&](int t) -> f4 {
-    if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + (p.frames ? hin_part((size_t)t * BN + c) : base);
-    return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + c) * 64 + ch);
+    if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + (p.frames ? hin_part((size_t)t * BN + sc) : base);
+    return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs);
   };
   __syncthreads();
   // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
   if (wave == 3 && g < 3 && cvalid) {
     const int d = g;
     auto lm_at = [&](int t) { return p.lm[((p.frames ? (size_t)t * BN : 0) + c) * 3 + d]; };
-    float xs[TMAX], vs[TMAX];
+    float xs[TMAX], vs[TMAX], lms[TMAX];
+    // loads are unconditional (frame index clamped to T - 1): a load under `if (t < T)` becomes a
+    // branch whose join waits for every outstanding load, i.e. one HBM latency per frame
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {
-      if (t < T) {
-        const size_t row = (FIRST && !p.frames) ? (size_t)c : ((size_t)t * BN + c);
-        xs[t] = p.x[row * 3 + d] - lm_at(t);
-        vs[t] = p.v[row * 3 + d];
-      }
+      const int tc = t < T ? t : T - 1;
+      const size_t row = (FIRST && !p.frames) ? (size_t)c : ((size_t)tc * BN + c);
+      lms[t] = lm_at(tc);
+      xs[t] = p.x[row * 3 + d] - lms[t];
+      vs[t] = p.v[row * 3 + d];
     }
     float yr[MM][2], yi[MM][2];
 #pragma unroll
@@ -1235,12 +1246,17 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
           }
         }
         const size_t row = (size_t)t * BN + c;
-        p.x_out[row * 3 + d] = xs[t] + y0 * invT + lm_at(t);
+        p.x_out[row * 3 + d] = xs[t] + y0 * invT + lms[t];
         p.v_out[row * 3 + d] = vs[t] + y1 * invT;
       }
     }
   }
   // ---- step 1: truncated DFT of this wave's input channels ----
+  // every frame's h is loaded once, up front and unconditionally (clamped frame index, see the x / v
+  // loads above), and kept in registers for the residual of step 3
+  f4 hvs[TMAX];
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) hvs[t] = hval(t < T ? t : T - 1);
   {
     f4 Xr[MM], Xs[MM];
 #pragma unroll
@@ -1248,7 +1264,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {
       if (t < T) {
-        const f4 hv = hval(t);
+        const f4 hv = hvs[t];
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
           if (m < M) {
@@ -1258,12 +1274,12 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
         }
       }
     }
-    *reinterpret_cast<f4*>(&sX[0][e][ch]) = Xr[0];
+    *reinterpret_cast<f4*>(&sX[0][ecol][chs]) = Xr[0];
 #pragma unroll
     for (int m = 1; m < MM; ++m) {
       if (m < M) {
-        *reinterpret_cast<f4*>(&sX[2 * m - 1][e][ch]) = Xr[m];
-        *reinterpret_cast<f4*>(&sX[2 * m][e][ch]) = Xs[m];
+        *reinterpret_cast<f4*>(&sX[2 * m - 1][ecol][chs]) = Xr[m];
+        *reinterpret_cast<f4*>(&sX[2 * m][ecol][chs]) = Xs[m];
       }
     }
   }
@@ -1295,8 +1311,31 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       mix(Yi[m], mat + 2, 2 * m);       // -A^T Xs
     }
   }
-  // ---- step 3: y[t] (output channels ch..ch+3 of column e), LeakyReLU(0.01), residual ----
-  if (cvalid) {
+  // ---- the spectrum Y back through LDS into the streaming layout (sX is free once every wave's
+  // mixing has read it) ----
+  __syncthreads();
+  {
+    const int chm = 16 * wave + 4 * g;   // MFMA output channels of column e
+    *reinterpret_cast<f4*>(&sX[0][e][chm]) = Yr[0];
+#pragma unroll
+    for (int m = 1; m < MM; ++m) {
+      if (m < M) {
+        *reinterpret_cast<f4*>(&sX[2 * m - 1][e][chm]) = Yr[m];
+        *reinterpret_cast<f4*>(&sX[2 * m][e][chm]) = Yi[m];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- step 3: y[t] (channels chs..chs+3 of column ecol), LeakyReLU(0.01), residual ----
+  if (svalid) {
+    Yr[0] = *reinterpret_cast<const f4*>(&sX[0][ecol][chs]);
+#pragma unroll
+    for (int m = 1; m < MM; ++m) {
+      if (m < M) {
+        Yr[m] = *reinterpret_cast<const f4*>(&sX[2 * m - 1][ecol][chs]);
+        Yi[m] = *reinterpret_cast<const f4*>(&sX[2 * m][ecol][chs]);
+      }
+    }
 #pragma unroll
     for (int t = 0; t < TMAX; ++t) {
       if (t < T) {
@@ -1304,10 +1343,10 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 #pragma unroll
         for (int m = 1; m < MM; ++m)
           if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
-        f4 o = hval(t);
+        f4 o = hvs[t];
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
-        *reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + c) * 64 + 16 * wave + 4 * g) = o;
+        *reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs) = o;
       }
     }
   }

@@ -1188,6 +1188,11 @@ __global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* 
 // straight into v_mfma_f32_16x16x4_f32: lane (l & 15, l >> 4) supplies G[k0 + (l>>4)][16 ti + (l&15)]
 // as the A operand and A[k0 + (l>>4)][16 tj + (l&15)] as the B operand, so K runs along the lane
 // groups and the 64 x 64 result stays in 16 accumulator tiles. HBM-bound (one pass over G and A).
+// V4 (M = N = 64, row strides and bases 16-byte aligned): lane il holds channels 4 il .. 4 il + 3 of
+// its row as ONE float4 per operand (16 lanes = one 256-byte row), i.e. MFMA index 16 t + il stands
+// for channel 4 il + t; the epilogue maps the accumulator back.
+constexpr int GEMM_UNR = 8;
+template <bool V4>
 __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__ G, int ldg, int M,
                                                        const float* __restrict__ A, int lda, int N, long long K,
                                                        long long kslice, float* partial) {
@@ -1200,21 +1205,74 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
   float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-  for (long long k = k0; k < k1; k += 4) {
-    const long long row = k + kr;
-    const bool ok = row < k1;
-    float gv[4], av[4];
+  if constexpr (V4) {
+    // software-pipelined: the next trip's GEMM_UNR row groups are in flight while this trip's MFMAs
+    // run (kslice is a multiple of 4 GEMM_UNR here, so only the grid's last wave has a ragged trip)
+    constexpr int S = 4 * GEMM_UNR;   // rows per trip
+    float4 g0[GEMM_UNR], a0[GEMM_UNR], g1[GEMM_UNR], a1[GEMM_UNR];   // ping-pong buffers: no copies
+    auto fetch = [&](float4 (&gb)[GEMM_UNR], float4 (&ab)[GEMM_UNR], long long k) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int cg = 16 * t + il;
-      gv[t] = (ok && cg < M) ? G[row * ldg + cg] : 0.f;
-      av[t] = (ok && cg < N) ? A[row * lda + cg] : 0.f;
-      bsum[t] += gv[t];
+      for (int u = 0; u < GEMM_UNR; ++u) {
+        // unconditional loads from a clamped row (a conditional load becomes a branch with a
+        // vmcnt(0) wait inside it); rows past k1 are zeroed at use
+        const long long row = k + 4 * u + kr, rc = row < k1 ? row : k1 - 1;
+        gb[u] = reinterpret_cast<const float4*>(G + rc * ldg)[il];
+        ab[u] = reinterpret_cast<const float4*>(A + rc * lda)[il];
+      }
+    };
+    auto compute = [&](const float4 (&gb)[GEMM_UNR], const float4 (&ab)[GEMM_UNR], long long k) {
+#pragma unroll
+      for (int u = 0; u < GEMM_UNR; ++u) {
+        const bool ok = k + 4 * u + kr < k1;
+        const float gv[4] = {ok ? gb[u].x : 0.f, ok ? gb[u].y : 0.f, ok ? gb[u].z : 0.f, ok ? gb[u].w : 0.f};
+        const float av[4] = {ok ? ab[u].x : 0.f, ok ? ab[u].y : 0.f, ok ? ab[u].z : 0.f, ok ? ab[u].w : 0.f};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bsum[t] += gv[t];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[a], av[b], acc[a][b]);
+      }
+    };
+    // the next trip's rows are in flight while this trip's MFMAs run (kslice is a multiple of S
+    // here, so only the grid's last wave has a ragged trip)
+    // (fetches are unconditional, clamped rows past k1: a conditional fetch makes the wait counter
+    // merge at the join fall back to vmcnt(0))
+    if (k0 < k1) {
+      fetch(g0, a0, k0);
+      for (long long k = k0; k < k1; k += 2 * S) {
+        fetch(g1, a1, k + S);
+        compute(g0, a0, k);
+        fetch(g0, a0, k + 2 * S);
+        compute(g1, a1, k + S);
+      }
+    }
+  } else {
+  // GEMM_UNR groups of 4 rows per trip: every group's loads are issued before the first MFMA, so a
+  // wave (one per SIMD at the capped grid) keeps GEMM_UNR row groups of HBM latency in flight
+  for (long long k = k0; k < k1; k += 4 * GEMM_UNR) {
+    float gv[GEMM_UNR][4], av[GEMM_UNR][4];
+#pragma unroll
+    for (int u = 0; u < GEMM_UNR; ++u) {
+      const long long row = k + 4 * u + kr;
+      const bool ok = row < k1;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int cg = 16 * t + il;
+        gv[u][t] = (ok && cg < M) ? G[row * ldg + cg] : 0.f;
+        av[u][t] = (ok && cg < N) ? A[row * lda + cg] : 0.f;
+      }
     }
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+    for (int u = 0; u < GEMM_UNR; ++u) {
 #pragma unroll
-      for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[a], av[b], acc[a][b]);
+      for (int t = 0; t < 4; ++t) bsum[t] += gv[u][t];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[u][a], av[u][b], acc[a][b]);
+    }
+  }
   }
   // the block's four wave partials are added through LDS in wave order: one partial per block
   __shared__ float red[4][64 * 65];
@@ -1227,11 +1285,13 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
     for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int i = 16 * a + 4 * kr + q, jj = 16 * b + il;   // accumulator: C[4(l>>4)+q][l&15]
+        // accumulator: C[4(l>>4)+q][l&15]; V4 index 16 t + r is channel 4 r + t
+        const int i = V4 ? 4 * (4 * kr + q) + a : 16 * a + 4 * kr + q, jj = V4 ? 4 * il + b : 16 * b + il;
         if (i < M && jj < N) out[i * (N + 1) + jj] = acc[a][b][q];
       }
     const float bs = group_sum(bsum[a]);
-    if (kr == 0 && 16 * a + il < M) out[(16 * a + il) * (N + 1) + N] = bs;
+    const int ib = V4 ? 4 * il + a : 16 * a + il;
+    if (kr == 0 && ib < M) out[ib * (N + 1) + N] = bs;
   }
   __syncthreads();
   float* dst = partial + (size_t)blockIdx.x * NO;
@@ -1308,13 +1368,20 @@ struct Gemm {
     if (K <= 0) return NONODE_OK;
     long long waves = (K + 31) / 32;                   // >= 32 rows per wave
     if (waves > max_waves) waves = max_waves;
+    const bool v4 = M == 64 && N == 64 && ldg % 4 == 0 && lda % 4 == 0 && ((uintptr_t)G & 15) == 0 &&
+                    ((uintptr_t)A & 15) == 0;
     long long kslice = (K + waves - 1) / waves;
-    kslice = (kslice + 3) & ~3LL;
+    kslice = v4 ? (kslice + 4 * GEMM_UNR - 1) / (4 * GEMM_UNR) * (4 * GEMM_UNR) : (kslice + 3) & ~3LL;
     waves = (K + kslice - 1) / kslice;
     const int nblk = (int)((waves + 3) / 4);
     const int nparts = nblk;   // one partial per block
     const int NO = M * (N + 1);
-    hipLaunchKernelGGL(gemm_tn_partial, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice, partial);
+    if (v4)
+      hipLaunchKernelGGL(gemm_tn_partial<true>, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice,
+                         partial);
+    else
+      hipLaunchKernelGGL(gemm_tn_partial<false>, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice,
+                         partial);
     if (int rc = check_launch("gemm_tn_partial")) return rc;
     hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, partial, nparts, M, N, dst, ld, col0,
                        cs, bias, accumulate, scale, split, col1, (long long)NO);
