@@ -1145,7 +1145,9 @@ __global__ void tconv_pack_kernel(const float* w, int Mfull, int M, int T, float
 // 4w..4w+3: inverse DFT, LeakyReLU + residual (h kept in registers from the DFT), row stores.
 // MM: compile-time bound on the number of modes (M <= MM), so the mode loops, the LDS spectrum and
 // the register arrays are sized for the configuration at hand
-template <bool FIRST, int MM>
+// TB: compile-time bound on the frame count (T <= TB), so the per-frame register arrays and the
+// unconditional (clamped) loads cover only the frames a configuration can have (TB = 10 for T <= 10)
+template <bool FIRST, int MM, int TB>
 __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   __shared__ __attribute__((aligned(16))) float sX[2 * MM - 1][16][ROWP];
   __shared__ float sCos[MM * TMAX], sSin[MM * TMAX];
@@ -1193,11 +1195,11 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   if (wave == 3 && g < 3 && cvalid) {
     const int d = g;
     auto lm_at = [&](int t) { return p.lm[((p.frames ? (size_t)t * BN : 0) + c) * 3 + d]; };
-    float xs[TMAX], vs[TMAX], lms[TMAX];
+    float xs[TB], vs[TB], lms[TB];
     // loads are unconditional (frame index clamped to T - 1): a load under `if (t < T)` becomes a
     // branch whose join waits for every outstanding load, i.e. one HBM latency per frame
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) {
+    for (int t = 0; t < TB; ++t) {
       const int tc = t < T ? t : T - 1;
       const size_t row = (FIRST && !p.frames) ? (size_t)c : ((size_t)tc * BN + c);
       lms[t] = lm_at(tc);
@@ -1210,7 +1212,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       if (m < M) {
         float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f};
 #pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
+        for (int t = 0; t < TB; ++t) {
           if (t < T) {
             const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
             Xr[0] = fmaf(xs[t], cs, Xr[0]); Xi[0] = fmaf(-xs[t], sn, Xi[0]);
@@ -1234,7 +1236,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     }
     const float invT = 1.0f / (float)T;
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) {
+    for (int t = 0; t < TB; ++t) {
       if (t < T) {
         float y0 = 0.f, y1 = 0.f;
 #pragma unroll
@@ -1253,16 +1255,17 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   // ---- step 1: truncated DFT of this wave's input channels ----
   // every frame's h is loaded once, up front and unconditionally (clamped frame index, see the x / v
-  // loads above), and kept in registers for the residual of step 3
-  f4 hvs[TMAX];
+  // loads above), and kept in registers for the residual of step 3. (Issuing these loads before
+  // wave 3's x / v work measured 1 us slower per launch.)
+  f4 hvs[TB];
 #pragma unroll
-  for (int t = 0; t < TMAX; ++t) hvs[t] = hval(t < T ? t : T - 1);
+  for (int t = 0; t < TB; ++t) hvs[t] = hval(t < T ? t : T - 1);
   {
     f4 Xr[MM], Xs[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) {
+    for (int t = 0; t < TB; ++t) {
       if (t < T) {
         const f4 hv = hvs[t];
 #pragma unroll
@@ -1337,7 +1340,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       }
     }
 #pragma unroll
-    for (int t = 0; t < TMAX; ++t) {
+    for (int t = 0; t < TB; ++t) {
       if (t < T) {
         f4 y = Yr[0];
 #pragma unroll
@@ -1355,29 +1358,38 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 // etab[b][t][o] = emb_b[o] + sum_k emb_w[o][din+k] * temb(t_out[b][t])[k]   (layer_no.py:8-17)
 // multi-input (t_in != null, egno.py:44-49, 77-79): emb_w columns are [h | temb(t_in) | temb(t_out)]
 // and t_in[b][t] is the input time of frame t's input
-__global__ void temb_kernel(int Bt, int T, int din, int dim, const float* t_out, const float* emb_w,
-                            int emb_ld, const float* emb_b, float* etab, const float* t_in = nullptr) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= Bt * T * 64) return;
-  const int o = idx & 63, bt = idx >> 6;
+__global__ __launch_bounds__(256) void temb_kernel(int Bt, int T, int din, int dim, const float* t_out,
+                                                   const float* emb_w, int emb_ld, const float* emb_b,
+                                                   float* etab, const float* t_in = nullptr) {
+  // a 256-thread block owns 4 (b, t) rows x 64 outputs; each row's sin / cos table (<= 2 * 64
+  // values, dim <= 64 is checked by the host) is computed once into LDS instead of once per output
+  __shared__ float trig[4][128];
+  const int row = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int bt = blockIdx.x * 4 + row;
+  const bool live = bt < Bt * T;
   const int half = dim / 2;
+  const int ncol = (t_in ? 2 : 1) * dim;
   const float scale = (float)(log(10000.0) / (double)(half - 1));
-  float acc = emb_b[o];
-  auto add_emb = [&](float tv, int col0) {
-    for (int k = 0; k < half; ++k) {
-      const float fk = expf((float)k * -scale);
+  if (live) {
+    for (int c = lane; c < ncol; c += 64) {
+      const int seg = c / dim, k = c % dim;           // seg 0: t_in (if given) else t_out
+      const float tv = (t_in && seg == 0) ? t_in[bt] : t_out[bt];
+      const float fk = expf((float)(k % half) * -scale);
       const float arg = tv * fk;
-      acc = fmaf(emb_w[o * emb_ld + col0 + k], sinf(arg), acc);
-      acc = fmaf(emb_w[o * emb_ld + col0 + half + k], cosf(arg), acc);
+      trig[row][c] = k < half ? sinf(arg) : cosf(arg);
     }
-  };
-  if (t_in) {
-    add_emb(t_in[bt], din);
-    add_emb(t_out[bt], din + dim);
-  } else {
-    add_emb(t_out[bt], din);
   }
-  etab[idx] = acc;
+  __syncthreads();
+  if (!live) return;
+  const int o = lane;
+  float acc = emb_b[o];
+  const float* w = emb_w + o * emb_ld + din;
+  for (int seg = 0; seg < ncol / dim; ++seg)
+    for (int k = 0; k < half; ++k) {
+      acc = fmaf(w[seg * dim + k], trig[row][seg * dim + k], acc);
+      acc = fmaf(w[seg * dim + half + k], trig[row][seg * dim + half + k], acc);
+    }
+  etab[(size_t)bt * 64 + o] = acc;
 }
 
 // out[n][o] = b[o] + sum_k W[o][k] in[n][k]   (SEGNO embedding, model.py:73)
@@ -1452,9 +1464,15 @@ int launch_tconv(bool first, const TconvArgs& a, hipStream_t stream) {
     if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(256), 0, stream, a);
     else hipLaunchKernelGGL(kf, dim3(grid), dim3(256), 0, stream, a);
   };
-  if (a.M <= 2) go(tconv_kernel<true, 2>, tconv_kernel<false, 2>);
-  else if (a.M <= 4) go(tconv_kernel<true, 4>, tconv_kernel<false, 4>);
-  else go(tconv_kernel<true, MMAX>, tconv_kernel<false, MMAX>);
+  if (a.T <= 10) {
+    if (a.M <= 2) go(tconv_kernel<true, 2, 10>, tconv_kernel<false, 2, 10>);
+    else if (a.M <= 4) go(tconv_kernel<true, 4, 10>, tconv_kernel<false, 4, 10>);
+    else go(tconv_kernel<true, MMAX, 10>, tconv_kernel<false, MMAX, 10>);
+  } else {
+    if (a.M <= 2) go(tconv_kernel<true, 2, TMAX>, tconv_kernel<false, 2, TMAX>);
+    else if (a.M <= 4) go(tconv_kernel<true, 4, TMAX>, tconv_kernel<false, 4, TMAX>);
+    else go(tconv_kernel<true, MMAX, TMAX>, tconv_kernel<false, MMAX, TMAX>);
+  }
   return check_launch("tconv_kernel");
 }
 
