@@ -203,10 +203,28 @@ def _egno_case(B, N, T=10, seed=0):
 
 
 @pytest.mark.parametrize("B,N,T", [(1, 2, 10), (3, 5, 10), (7, 20, 10), (2, 20, 5), (5, 13, 4), (2, 40, 10),
-                                   (1, 100, 2)])
+                                   (1, 100, 2), (3, 7, 16), (2, 9, 13), (4, 6, 11)])
 def test_egno_matches_oracle_across_shapes(B, N, T):
     m = _egno(T=T, seed=B * 100 + N)
     case = _egno_case(B, N, T, seed=N)
+    p = _sd_np(m)
+    xr, vr, hr = oe.egno_forward(p, **{k: (v.astype(np.float64) if k not in ("row", "col", "t_out") else v)
+                                       for k, v in case.items()}, T=T)
+    with torch.no_grad():
+        x, v, h = m(_dev(case["x"]), _dev(case["h"]), [_dev(case["row"]), _dev(case["col"])], _dev(case["edge_fea"]),
+                    v=_dev(case["v"]), loc_mean=_dev(case["loc_mean"]), timesteps_out=_dev(case["t_out"]))
+    assert maxnorm_rel(x.cpu(), xr) < TOL
+    assert maxnorm_rel(v.cpu(), vr) < TOL
+    assert maxnorm_rel(h.cpu(), hr) < TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,modes", [(16, 9), (12, 4), (10, 5), (7, 4)])
+def test_egno_mode_and_frame_bounds_match_oracle(T, modes):
+    """Every tconv_kernel build (mode bound 2 / 4 / 9 x frame bound 10 / 16) against the oracle."""
+    B, N = 3, 6
+    m = _egno(T=T, modes=modes, seed=T * 10 + modes)
+    case = _egno_case(B, N, T, seed=modes)
     p = _sd_np(m)
     xr, vr, hr = oe.egno_forward(p, **{k: (v.astype(np.float64) if k not in ("row", "col", "t_out") else v)
                                        for k, v in case.items()}, T=T)
