@@ -66,18 +66,31 @@ def setup_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NONODE_DIST_BACKEND=gloo rehearses the multi-rank bench on a box with fewer GPUs than ranks
+    # (ranks then share GPUs round-robin); the default on a GPU node is RCCL ("nccl"), one GPU per rank
+    gpu = torch.cuda.is_available()
+    if gpu:
+        local = local % torch.cuda.device_count()
     if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if torch.cuda.is_available():
+        backend = os.environ.get("NONODE_DIST_BACKEND") or ("nccl" if gpu else "gloo")
+        if gpu:
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
-    dev = torch.device(f"cuda:{local}" if torch.cuda.is_available() else "cpu")
+    dev = torch.device(f"cuda:{local}" if gpu else "cpu")
     return world, rank, dev
+
+
+def _barrier(dev):
+    # NCCL (RCCL) barrier on this rank's own GPU, not a guessed one
+    if dev.type == "cuda" and dist.get_backend() == "nccl":
+        dist.barrier(device_ids=[dev.index])
+    else:
+        dist.barrier()
 
 
 def barrier_sync(world, dev):
     if world > 1:
-        dist.barrier()
+        _barrier(dev)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
 
@@ -527,7 +540,7 @@ def main():
     if rank == 0:
         print(json.dumps(res))
     if world > 1:
-        dist.barrier()
+        _barrier(dev)
         dist.destroy_process_group()
 
 
