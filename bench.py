@@ -95,6 +95,23 @@ def barrier_sync(world, dev):
         torch.cuda.synchronize(dev)
 
 
+def _prewarm(call, args, dev):
+    """Untimed calls of the same step for at least --prewarm-ms of wall time, before the W warmup
+    steps: an idle GPU ramps its clocks during them (on a fresh MI355X box the first ~10 ms of C3
+    ran at half speed). Reported as "prewarm_ms" in the JSON line."""
+    if args.prewarm_ms <= 0:
+        return
+    from no_node_comparison_amd.sharding import max_over_ranks
+    t0 = time.perf_counter()
+    while True:
+        call()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        # every rank stops after the same call (a training step holds a collective)
+        if max_over_ranks((time.perf_counter() - t0) * 1e3, dev) >= args.prewarm_ms:
+            break
+
+
 def build_egno_case(B, N, T, seed, dev, world=1, rank=0):
     import no_node_comparison_amd as pkg
     loc, vel, q = rank_batch(B, world, rank, N, seed)
@@ -146,6 +163,7 @@ def run_egno(args, world, rank, dev):
     call = lambda: model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],  # noqa: E731
                          loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
     with torch.no_grad():
+        _prewarm(call, args, dev)
         for _ in range(args.warmup):
             out = call()
         barrier_sync(world, dev)
@@ -252,6 +270,7 @@ def run_segno(args, world, rank, dev, gravity=False):
 
     from no_node_comparison_amd import _lib
     with torch.no_grad():
+        _prewarm(call, args, dev)
         for _ in range(args.warmup):
             call()
         barrier_sync(world, dev)
@@ -318,6 +337,7 @@ def run_egno_train(args, world, rank, dev):
         opt.step()
         return loss
 
+    _prewarm(step, args, dev)
     for _ in range(args.warmup):
         step()
     barrier_sync(world, dev)
@@ -367,6 +387,7 @@ def run_egno_rollout(args, world, rank, dev):
     call = lambda: pkg.harness.egno_rollout(model, nodes, x, edges, v, eao, ea, lm, N, L, B,  # noqa: E731
                                             charges=q.reshape(-1), num_steps=T, timesteps_out=t_all,
                                             energy_dataset="charged")
+    _prewarm(call, args, dev)
     for _ in range(args.warmup):
         out = call()
     barrier_sync(world, dev)
@@ -452,6 +473,7 @@ def run_sim_charged(args, world, rank, dev):
     l0 = torch.tensor(np.stack([d[1] for d in draws]), dtype=torch.float64, device=dev)
     v0 = torch.tensor(np.stack([d[2] for d in draws]), dtype=torch.float64, device=dev)
     call = lambda: sim.integrate(q, l0, v0, Tn, freq)  # noqa: E731
+    _prewarm(call, args, dev)
     for _ in range(args.warmup):
         out = call()
     barrier_sync(world, dev)
@@ -522,6 +544,8 @@ def main():
                     help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4; "
                          "egno_rollout = SURVEY row f1; sim_charged = row f3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--prewarm-ms", type=float, default=300.0,
+                    help="untimed clock-ramp calls (wall ms) before the W warmup steps")
     ap.add_argument("--no-kernel-events", dest="kernel_events", action="store_false")
     args = ap.parse_args()
     world, rank, dev = setup_dist()
@@ -538,6 +562,7 @@ def main():
     else:
         res = run_segno(args, world, rank, dev, gravity=args.workload == "segno_gravity")
     if rank == 0:
+        res["prewarm_ms"] = args.prewarm_ms
         print(json.dumps(res))
     if world > 1:
         _barrier(dev)
