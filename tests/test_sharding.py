@@ -168,3 +168,26 @@ def _dp_grads(rank, world, total):
 
 def test_dp_allreduce_equals_whole_batch_gradients_gloo_ws2():
     _run(2, _dp_grads, 4)
+
+
+def _prewarm_agreement(rank, world, out_dir):
+    """bench._prewarm: ranks of different speed stop after the same number of calls (a training
+    step holds a collective, so unequal counts would deadlock the timed loop)."""
+    import time
+    import types
+    import bench
+    calls = []
+
+    def call():
+        calls.append(1)
+        time.sleep(0.002 * (rank + 1))   # rank 1 is twice as slow as rank 0
+
+    bench._prewarm(call, types.SimpleNamespace(prewarm_ms=40.0), torch.device("cpu"))
+    with open(os.path.join(out_dir, f"r{rank}"), "w") as f:
+        f.write(str(len(calls)))
+
+
+def test_bench_prewarm_stops_all_ranks_together(tmp_path):
+    _run(2, _prewarm_agreement, str(tmp_path))
+    counts = [int(open(tmp_path / f"r{r}").read()) for r in range(2)]
+    assert counts[0] == counts[1] > 1
