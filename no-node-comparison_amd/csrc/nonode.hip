@@ -37,6 +37,10 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 #ifndef NONODE_STAGGER
 #define NONODE_STAGGER 1
 #endif
+// tconv_kernel h stream cache policy: bit 0 = nontemporal loads, bit 1 = nontemporal stores
+#ifndef NONODE_TC_NT
+#define NONODE_TC_NT 0
+#endif
 #ifndef NONODE_REG_FRAGS
 #define NONODE_REG_FRAGS 1
 #endif
@@ -1188,7 +1192,11 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   auto hval = [&](int t) -> f4 {
     if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + (p.frames ? hin_part((size_t)t * BN + sc) : base);
+#if NONODE_TC_NT & 1
+    return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs));
+#else
     return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs);
+#endif
   };
   __syncthreads();
   // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
@@ -1349,7 +1357,11 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
         f4 o = hvs[t];
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
+#if NONODE_TC_NT & 2
+        __builtin_nontemporal_store(o, reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs));
+#else
         *reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs) = o;
+#endif
       }
     }
   }
