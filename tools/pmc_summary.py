@@ -13,7 +13,7 @@ for f in glob.glob(f"{d}/pmc_*/run_counter_collection.csv"):
         if "egnn_layer" in n:
             key = "layer" + ("<SEGNO>" if "Li1E" in n or "<1," in n else "")
         elif "tconv" in n:
-            key = "tconv_first" if "<true>" in n else "tconv"
+            key = "tconv_first" if ("<true>" in n or "<true," in n) else "tconv"
         else:
             continue
         res[key].setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
@@ -22,7 +22,7 @@ for row in csv.DictReader(open(f"{d}/trace/run_kernel_stats.csv")):
     stats[row["Name"]] = float(row["AverageNs"])
 for k, dd in res.items():
     out = {c: statistics.mean(v) for c, v in dd.items()}
-    ns = [v for n, v in stats.items() if ("egnn_layer" in n if k.startswith("layer") else ("tconv" in n and (("<true>" in n) == (k == "tconv_first"))))]
+    ns = [v for n, v in stats.items() if ("egnn_layer" in n if k.startswith("layer") else ("tconv" in n and ((("<true>" in n) or ("<true," in n)) == (k == "tconv_first"))))]
     ns = ns[0] if ns else None
     line = f"{k}: avg {ns/1e3 if ns else 0:.1f} us"
     if "GRBM_GUI_ACTIVE" in out and ns:

@@ -21,7 +21,7 @@ def kernel_key(name):
         variant = "SEGNO" if (m and m.group(1) == "1") or "ILi1E" in name else "EGNO"
         return f"egnn_layer_kernel<{variant}>"
     if "tconv_kernel" in name:
-        return "tconv_kernel<first>" if ("<true>" in name or "ILb1E" in name) else "tconv_kernel"
+        return "tconv_kernel<first>" if ("<true>" in name or "<true," in name or "ILb1E" in name) else "tconv_kernel"
     for k in ("temb_kernel", "embed_kernel"):
         if k in name:
             return k
