@@ -558,6 +558,10 @@ struct LayerArgs {
   int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections,
                // 8 no edge-feature loads, 16 SiLU -> clamp, 32 skip the per-edge fp16 MFMAs
   float inv_deg, dt, cw;
+  // XCD-aware chunk order (EGNO forward): workgroup k runs graph chunk chunk_of[k], chosen so that
+  // k % 8 (its XCD) owns the same 1/8 of the columns as the TimeConv tiles on that XCD
+  int use_perm;
+  unsigned short chunk_of[256];
 };
 
 size_t layer_lds_floats(int ct, int N, int* s_max_out) {
@@ -600,8 +604,9 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
   const float* vWC2_ = sV + 512 + V_WC2 * 64;
 
   const int G = gridDim.x;
-  const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;         // first receiver
-  const int nend = (int)(((long long)(blockIdx.x + 1) * p.n_graphs) / G) * N;  // one past the last
+  const int cb = p.use_perm ? (int)p.chunk_of[blockIdx.x] : (int)blockIdx.x;
+  const int nb = (int)(((long long)cb * p.n_graphs) / G) * N;         // first receiver
+  const int nend = (int)(((long long)(cb + 1) * p.n_graphs) / G) * N;  // one past the last
   __syncthreads();
 
   const int ntw = (nend - nb + 15) >> 4;
@@ -1118,6 +1123,7 @@ struct TconvArgs {
   // layer's loc_mean are per frame ([T*BN] rows, the inputs already spread over the T frames as
   // repeat_elements_to_exact_shape does); 0: x, v, h_in, loc_mean are [BN] rows replicated over T
   int frames;
+  int xcd;   // 1: workgroup k runs tile (k % 8) * ceil(tiles / 8) + k / 8 (XCD-aware order)
 };
 
 // Packed mixing weights of one TimeConv (layer_no.py:80-126), as W^T fragments (f32 MFMA A operand)
@@ -1157,6 +1163,9 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   __shared__ float sCos[MM * TMAX], sSin[MM * TMAX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int T = p.T, M = p.M, BN = p.BN;
+  const int ntiles = (BN + 15) / 16, tpx = (ntiles + 7) / 8;
+  const int tile = p.xcd ? (int)(blockIdx.x % 8) * tpx + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (tile >= ntiles) return;   // whole workgroup, before any barrier
   if (tid < M * T) {
     const int m = tid / T, t = tid - (tid / T) * T;
     const double ang = 2.0 * (double)m * (double)t / (double)T;
@@ -1164,14 +1173,14 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     sSin[m * TMAX + t] = (float)sinpi(ang);
   }
   // x / v lanes and the mixing MFMAs: column e = lane & 15 of the tile
-  const int col = blockIdx.x * 16 + e;
+  const int col = tile * 16 + e;
   const bool cvalid = col < BN;
   const int c = cvalid ? col : BN - 1;
   // h streaming (steps 1 and 3): wave w owns columns 4w .. 4w+3 of the tile, lane (cl = lane >> 4,
   // cq = lane & 15) channels 4cq .. 4cq+3 of column 4w + cl, so one f4 load / store instruction of a
   // wave moves 4 whole consecutive 256-byte rows (1 KB contiguous per frame)
   const int ecol = 4 * wave + (lane >> 4), chs = 4 * (lane & 15);
-  const int scol = blockIdx.x * 16 + ecol;
+  const int scol = tile * 16 + ecol;
   const bool svalid = scol < BN;
   const int sc = svalid ? scol : BN - 1;
   f4 base = {0.f, 0.f, 0.f, 0.f};
@@ -1416,6 +1425,11 @@ __global__ void embed_kernel(int n_nodes, int din, const float* in, const float*
 }
 
 // ---- host-side launchers ----------------------------------------------------------------------
+// NONODE_XCD=0 turns off the XCD-aware tile / chunk order of the EGNO forward
+bool xcd_on() {
+  static const int on = getenv("NONODE_XCD") ? atoi(getenv("NONODE_XCD")) : 1;
+  return on != 0;
+}
 template <int VARIANT, int NW, bool PAIR>
 void launch_cfg(int kf, int G, size_t lds, hipStream_t stream, const LayerArgs& a) {
   static std::once_flag once;
@@ -1432,7 +1446,8 @@ template <int VARIANT>
 int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const float* x,
                  const float* v, const float* ef, const float* blob, float dt, float cw, int recurrent,
                  float* h_out, float* x_out, float* v_out, hipStream_t stream, int steps = 1,
-                 float* const* pp = nullptr, float* m_out = nullptr, float* f_out = nullptr) {
+                 float* const* pp = nullptr, float* m_out = nullptr, float* f_out = nullptr,
+                 int xcd_cols = 0) {
   const int n_total = n_graphs * N;
   const int cus = num_cus();
   const int G = n_graphs < cus ? n_graphs : cus;
@@ -1460,6 +1475,23 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   static const int cfg = getenv("NONODE_CFG") ? atoi(getenv("NONODE_CFG")) : 1;
   a.debug = dbg;
   a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
+  a.use_perm = 0;
+  if (xcd_cols > 0 && G % 8 == 0 && G <= 256 && xcd_on()) {
+    // chunk c starts at column (first receiver row mod xcd_cols); its XCD block is that column's
+    // eighth. Fill each XCD's G/8 slots (k = x, x + 8, ...) from its block, overflow anywhere.
+    int slot_fill[8] = {0};
+    int left[256], nleft = 0;
+    for (int k = 0; k < G; ++k) a.chunk_of[k] = 0xffff;
+    for (int c = 0; c < G; ++c) {
+      const long long row0 = (((long long)c * n_graphs) / G) * N;
+      const int x = (int)((row0 % xcd_cols) * 8 / xcd_cols);
+      if (slot_fill[x] < G / 8) a.chunk_of[x + 8 * slot_fill[x]++] = (unsigned short)c;
+      else left[nleft++] = c;
+    }
+    for (int k = 0, i = 0; k < G; ++k)
+      if (a.chunk_of[k] == 0xffff) a.chunk_of[k] = (unsigned short)left[i++];
+    a.use_perm = 1;
+  }
   ProfScope prof(VARIANT, stream);
   if (ne == 0) { a.ef = blob; a.ne = 1; a.ef_mod = 1; }   // dummy gather target; feature weights are 0
   const int kf = a.ne <= 3 ? 1 : 2;
@@ -1469,8 +1501,11 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   return check_launch("egnn_layer_kernel");
 }
 
-int launch_tconv(bool first, const TconvArgs& a, hipStream_t stream) {
-  const int grid = (a.BN + 15) / 16;
+int launch_tconv(bool first, const TconvArgs& a_in, hipStream_t stream) {
+  TconvArgs a = a_in;
+  const int ntiles = (a.BN + 15) / 16;
+  a.xcd = xcd_on() && ntiles >= 64;
+  const int grid = a.xcd ? 8 * ((ntiles + 7) / 8) : ntiles;
   ProfScope prof(first ? 3 : 2, stream);
   auto go = [&](auto kt, auto kf) {
     if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(256), 0, stream, a);
@@ -1634,7 +1669,7 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
     }
     if (int rc = launch_tconv(l == 0, a, s)) return rc;
     if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hB, xB, v_out, edge_fea, blobs[l], 0.f, 1.f, 0,
-                                    h_out, x_out, nullptr, s))
+                                    h_out, x_out, nullptr, s, 1, nullptr, nullptr, nullptr, BN))
       return rc;
   }
   return NONODE_OK;
