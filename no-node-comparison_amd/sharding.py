@@ -70,7 +70,7 @@ def gather_samples(local, total):
 class FlatGrads:
     """Data-parallel gradient exchange with ONE collective per step.
 
-    Every parameter's .grad is a view into one contiguous fp32 buffer, so autograd accumulates
+    Every parameter's .grad is a view into one contiguous buffer (fp32 for the models), so autograd accumulates
     straight into it and the step needs a single all-reduce (sum) of the flat buffer (0.81 MB
     for EGNO) followed by a division by the world size: with equal shards this is the gradient of
     the global mean loss. With world size 1 (or no process group) it is a no-op."""
@@ -78,17 +78,52 @@ class FlatGrads:
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
         n = sum(p.numel() for p in self.params)
-        dev = self.params[0].device
-        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+        dev, dt = self.params[0].device, self.params[0].dtype
+        if any(p.dtype != dt or p.device != dev for p in self.params):
+            raise ValueError("FlatGrads needs every parameter on one device with one dtype")
+        self.flat = torch.zeros(n, dtype=dt, device=dev)
+        self.views = []
         off = 0
         for p in self.params:
-            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            self.views.append(self.flat[off:off + p.numel()].view_as(p))
             off += p.numel()
+        self._bind()
+
+    def _bind(self):
+        for p, v in zip(self.params, self.views):
+            p.grad = v
 
     def zero_(self):
         self.flat.zero_()
+        self._bind()
+
+    def gather_(self):
+        """Bring every p.grad back into the flat buffer. The reference loop calls
+        optimizer.zero_grad() each step (main_simulation_simple_no.py:224), which in torch 2.x sets
+        p.grad = None, so the next backward allocates fresh local tensors instead of accumulating
+        into the views. Those (or a None, i.e. zero) are copied into the buffer and the views are
+        re-bound, so the all-reduce always reduces the gradients the optimizer will step on."""
+        stale = [i for i, (p, v) in enumerate(zip(self.params, self.views))
+                 if p.grad is None or p.grad.data_ptr() != v.data_ptr()]
+        if not stale:
+            return self.flat
+        if len(stale) == len(self.params):
+            # the usual case after zero_grad(): one concatenation into the buffer
+            parts = [(p.grad if p.grad is not None else torch.zeros_like(v)).reshape(-1)
+                     for p, v in zip(self.params, self.views)]
+            torch.cat(parts, out=self.flat)
+        else:
+            for i in stale:
+                p, v = self.params[i], self.views[i]
+                if p.grad is None:
+                    v.zero_()
+                else:
+                    v.copy_(p.grad)
+        self._bind()
+        return self.flat
 
     def allreduce_(self):
+        self.gather_()
         if not _initialized() or dist.get_world_size() == 1:
             return self.flat
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)

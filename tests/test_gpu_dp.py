@@ -44,7 +44,9 @@ def _step_grads(lo, hi, allreduce):
     x, _, _ = m(inp["x"], inp["h"], [inp["row"], inp["col"]], inp["edge_fea"], v=inp["v"],
                 loc_mean=inp["loc_mean"], timesteps_out=inp["t_out"])
     loss, _ = _loss_like_reference(x, target, T, hi - lo, N)
-    fg.zero_()
+    # the reference loop's order (main_simulation_simple_no.py:224,278-280): zero_grad() sets every
+    # p.grad to None (dropping the FlatGrads views); allreduce_() must gather them back
+    torch.optim.Adam(m.parameters(), lr=1e-4).zero_grad()
     loss.backward()
     if allreduce:
         fg.allreduce_()

@@ -170,6 +170,47 @@ def test_dp_allreduce_equals_whole_batch_gradients_gloo_ws2():
     _run(2, _dp_grads, 4)
 
 
+def _reference_loop_order(rank, world, total, set_to_none):
+    """The reference training loop's order (main_simulation_simple_no.py:224,278-280):
+    optimizer.zero_grad(); loss.backward(); [one all-reduce]; optimizer.step(). zero_grad() drops
+    the FlatGrads views (set_to_none=True is torch 2.x's default); the all-reduce must still reduce
+    the gradients the optimizer steps on, for several steps in a row."""
+    from no_node_comparison_amd.sharding import FlatGrads
+    torch.manual_seed(0)
+    data = torch.randn(total, 6)
+    target = torch.randn(total, 2)
+
+    def make():
+        torch.manual_seed(1)
+        return torch.nn.Sequential(torch.nn.Linear(6, 16), torch.nn.SiLU(), torch.nn.Linear(16, 2)).double()
+
+    lo, hi = shard_range(total, world, rank)
+    m = make()
+    fg = FlatGrads(m.parameters())
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    ref = make()
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-2)
+    for step in range(3):
+        opt.zero_grad(set_to_none=set_to_none)
+        loss = torch.nn.functional.mse_loss(m(data[lo:hi].double()), target[lo:hi].double())
+        loss.backward()
+        fg.allreduce_()
+        ropt.zero_grad()
+        torch.nn.functional.mse_loss(ref(data.double()), target.double()).backward()
+        for (k, p), q in zip(m.named_parameters(), ref.parameters()):
+            assert p.grad.data_ptr() == fg.views[[id(x) for x in fg.params].index(id(p))].data_ptr()
+            assert maxnorm_rel(p.grad.numpy(), q.grad.numpy()) < 1e-12, (step, k)
+        opt.step()
+        ropt.step()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert maxnorm_rel(p.detach().numpy(), q.detach().numpy()) < 1e-12
+
+
+@pytest.mark.parametrize("set_to_none", [True, False])
+def test_flatgrads_under_reference_zero_grad_gloo_ws2(set_to_none):
+    _run(2, _reference_loop_order, 8, set_to_none)
+
+
 def _prewarm_agreement(rank, world, out_dir):
     """bench._prewarm: ranks of different speed stop after the same number of calls (a training
     step holds a collective, so unequal counts would deadlock the timed loop)."""
