@@ -106,6 +106,7 @@ class SEGNO(nn.Module):
     def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
         """model.py:53-92 (single input). his [BN, in_node_nf], x, v [BN, 3], edges 2 x [E],
         edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T."""
+        self._check_trainable()
         if x.dim() == 3:
             return self._forward_multi(his, x, edges, v, edge_attr, int(T), in_steps)
         if self.bug_compat:
@@ -149,10 +150,21 @@ class SEGNO(nn.Module):
 
     def forward_step(self, h, x, edges, v, edge_attr, T=10):
         """model.py:95-102: T substeps of the shared layer from an already-embedded h."""
+        self._check_trainable()
         self.module.n_layers = T
         self.n_layers = T
         out = self._run(None, h, x, edges, v, edge_attr, int(T))
         return out
+
+    def _check_trainable(self):
+        """The fused integrator has no reverse pass yet: in train mode with gradients enabled the
+        outputs could not carry a gradient, so say so instead of returning detached tensors (the
+        reference fails later, at train_nbody.py:178, with "does not require grad")."""
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) \
+                and not self.bug_compat:
+            raise RuntimeError("SEGNO (MI355X kernels): training through the fused integrator "
+                               "(train_nbody.py:168-179) is not implemented; call model.eval() or run "
+                               "under torch.no_grad() for inference")
 
     def _embed(self, his):
         _lib.require_device(his, self.embedding.weight)

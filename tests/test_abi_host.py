@@ -111,6 +111,18 @@ def test_unsupported_configs_raise():
         pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, multiple_agg="max")
 
 
+def test_segno_train_mode_raises_clearly():
+    """Until the fused integrator has a reverse pass, train mode with grad enabled must not return
+    silently detached outputs (train_nbody.py:168-179 would fail later with a generic message)."""
+    m = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True).train()
+    z = torch.zeros(20, 3)
+    with pytest.raises(RuntimeError, match="not implemented"):
+        m(torch.zeros(20, 1), z, pkg.graph.full_edges(1, 20), z, torch.zeros(380, 2), T=10)
+    with pytest.raises(pkg.NonodeError, match="no CPU path"):   # eval mode gets as far as the device check
+        with torch.no_grad():
+            m(torch.zeros(20, 1), z, pkg.graph.full_edges(1, 20), z, torch.zeros(380, 2), T=10)
+
+
 def test_no_cpu_fallback():
     fx = load_golden("egno_fwd")
     m = _egno_ctor()
