@@ -1,17 +1,26 @@
 """Benchmark of the EGNO / SEGNO trajectory-rollout hot path on MI355X.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` — one process per GPU (launched
-by torch.distributed.run for N > 1), W untimed steps, then exactly K timed steps bracketed by a
-barrier + synchronize, max over ranks; rank 0 prints ONE JSON line.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` — one process per GPU, W untimed
+steps, then exactly K timed steps bracketed by a barrier + synchronize, max over ranks; rank 0 prints
+ONE JSON line. For N > 1 the driver starts the ranks with torch.distributed.run; started without it
+(WORLD_SIZE unset), ``--gpus N`` launches torch.distributed.run itself as a child process before
+anything touches the GPU, and every rank checks that the world it joined has exactly N ranks.
 
 A "step" is one pass of the hot path over one batch of synthetic input. Default workload
 (BASELINE.json configs[1], "C2"): EGNO 4 layers, charged N=20, T=10, B=512 per GPU, fp32 — one
 model call producing T=10 frames for all B trajectories. Ranks are independent replicas on their
 own batch shard (the path shards by sample; inference has no collective), so scaling is weak.
+``--global-batch G`` fixes the total batch instead (G / N per GPU, "scaling": "strong"), e.g. the
+C4 training config: ``--workload egno_train --global-batch 4096``.
+
+The CPU baseline is oracle/torch_ref.py — the reference's own torch operators, op by op, on the
+host cores — and the HIP outputs are checked against it on the same batch.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "N-body trajectories/s (B×T, N=20 rollout) + pos-MSE vs ref, 1/2/4/8 MI355X"
+DTYPE = "fp32 (fp16x3 split-MFMA, fp32 accumulate, f32 guard)"
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = f32-input MFMA peak (spec)
 FP16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (spec)
 # The layer kernel delivers fp32-accurate 64x64 products as fp16x3 split MFMAs (W_lo x_hi + W_hi x_lo +
@@ -31,7 +41,7 @@ FP16_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (s
 FP16X3_PEAK_TFLOPS = FP16_PEAK_TFLOPS / 3.0
 HBM_PEAK_GBS = 8000.0
 
-# Algorithmic work of one egnn_layer_kernel launch (DESIGN.md §4, SURVEY §8d decomposed count):
+# Algorithmic work of one egnn_layer_kernel launch (DESIGN.md §3.1, SURVEY §8d decomposed count):
 #   per edge: 8448 MAC (W2 64x64 + Wc1 64x64 + w_s/W_e/w_c2 vectors)
 #   per node: 24640 MAC (P, Q projections 2x64x64, node_v 64x64+64, node MLP 128x64+64x64)
 MAC_PER_EDGE = 8448
@@ -39,45 +49,58 @@ MAC_PER_NODE = 24640
 # SEGNO_GCL (gcl.py:71-119): per edge W2 + Wc1 + vectors as EGNO; per node P, Q + node MLP (no phi_v)
 MAC_PER_EDGE_SEGNO = 8448
 MAC_PER_NODE_SEGNO = 20480
+# Edge backward (edge_bwd_kernel pass 0 + pass 1): the reverse of the two per-edge
+# 64x64 Linears W2 and Wc1 — data gradient (64x64) and weight gradient (64x64) each — plus the
+# vector terms (w_c2, the scalar input columns). The forward recompute is not counted.
+MAC_PER_EDGE_BWD = 4 * 4096 + 4 * 64
+# Algorithmic HBM bytes of the reference formulation's edge aggregation at C2: messages
+# [e, 64 + 3] read + node sums [n, 64 + 3] written, fp32, per layer
+AGG_BYTES = lambda e, n: (e + n) * 67 * 4  # noqa: E731
 
 
-def synthetic_charged(B, N, seed):
-    """SURVEY §8d generator: positions ~ N(0, sigma^2), sigma = (N/5)^(1/3); unit direction x 0.5
-    velocities; charges +-1 with p = 1/2."""
-    g = torch.Generator().manual_seed(seed)
-    sigma = (N / 5.0) ** (1.0 / 3.0)
-    loc = torch.randn(B, N, 3, generator=g) * sigma
-    vel = torch.randn(B, N, 3, generator=g)
-    vel = vel / vel.norm(dim=-1, keepdim=True) * 0.5
-    q = (torch.randint(0, 2, (B, N, 1), generator=g) * 2 - 1).float()
-    return loc, vel, q
+# ---------------------------------------------------------------------------------------------------
+# launch / distributed setup
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
 
-def rank_batch(B_per, world, rank, N, seed):
-    """This rank's shard of the global synthetic batch of B_per * world samples (weak scaling: the
-    per-GPU batch is fixed). Concatenating every rank's shard gives the global batch."""
-    from no_node_comparison_amd.sharding import shard_range
-    loc, vel, q = synthetic_charged(B_per * world, N, seed)
-    lo, hi = shard_range(B_per * world, world, rank)
-    return loc[lo:hi], vel[lo:hi], q[lo:hi]
+def maybe_launch(args):
+    """--gpus N > 1 outside torch.distributed.run: run N ranks as a child torch.distributed.run
+    (one process per GPU) and exit with its status. Called before anything initialises the GPU."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.stdout.flush()
+    sys.exit(subprocess.call(cmd, env=env))
 
 
-def setup_dist():
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but the process group has {world} ranks")
+    gpu = torch.cuda.is_available()
     # NONODE_DIST_BACKEND=gloo rehearses the multi-rank bench on a box with fewer GPUs than ranks
     # (ranks then share GPUs round-robin); the default on a GPU node is RCCL ("nccl"), one GPU per rank
-    gpu = torch.cuda.is_available()
+    backend = os.environ.get("NONODE_DIST_BACKEND") or ("nccl" if gpu else "gloo")
     if gpu:
-        local = local % torch.cuda.device_count()
+        ndev = torch.cuda.device_count()
+        if backend == "nccl" and world > ndev:
+            raise SystemExit(f"bench: {world} RCCL ranks but only {ndev} visible GPUs")
+        local = local % ndev
+        torch.cuda.set_device(local)
     if world > 1:
-        backend = os.environ.get("NONODE_DIST_BACKEND") or ("nccl" if gpu else "gloo")
-        if gpu:
-            torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench: joined a world of {dist.get_world_size()}, expected {args.gpus}")
     dev = torch.device(f"cuda:{local}" if gpu else "cpu")
-    return world, rank, dev
+    return world, rank, dev, (backend if world > 1 else None)
 
 
 def _barrier(dev):
@@ -93,6 +116,32 @@ def barrier_sync(world, dev):
         _barrier(dev)
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
+
+
+def batch_plan(args, world, rank, per_gpu_default):
+    """Weak scaling (default): B per GPU fixed (--batch, else the workload's default). Strong
+    scaling (--global-batch G): G samples in total, shard_range(G, world, rank) on this rank."""
+    from no_node_comparison_amd.sharding import shard_range
+    if args.global_batch:
+        G = args.global_batch
+        lo, hi = shard_range(G, world, rank)
+        return dict(B_global=G, B=hi - lo, lo=lo, hi=hi, scaling="strong")
+    B = args.batch or per_gpu_default
+    return dict(B_global=B * world, B=B, lo=B * rank, hi=B * (rank + 1), scaling="weak")
+
+
+def check_launch(args, world, rank, dev, backend):
+    """--check-launch: report every rank's (rank, local rank, device) without running a workload
+    (the CPU test of the launcher)."""
+    me = torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0")), dev.index if dev.index is not None else -1])
+    if world > 1:
+        me = me.to(dev) if backend == "nccl" else me
+        parts = [torch.zeros_like(me) for _ in range(world)]
+        dist.all_gather(parts, me)
+        ranks = [p.cpu().tolist() for p in parts]
+    else:
+        ranks = [me.tolist()]
+    return {"check_launch": True, "world_size": world, "backend": backend, "ranks": ranks, "n_gpus": world}
 
 
 def _prewarm(call, args, dev):
@@ -112,54 +161,138 @@ def _prewarm(call, args, dev):
             break
 
 
-def build_egno_case(B, N, T, seed, dev, world=1, rank=0):
+def device_info(dev):
+    """What the run ran on: CU count (the layer kernels size their grid by it), arch, clocks and
+    partition modes (rocm-smi, best effort) — to tell box-to-box variance from code changes."""
+    if dev.type != "cuda":
+        return None
+    p = torch.cuda.get_device_properties(dev)
+    info = {"name": p.name, "arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
+            "hbm_gib": round(p.total_memory / 2 ** 30, 1)}
+    try:
+        r = subprocess.run(["rocm-smi", "--showclocks", "--showcomputepartition", "--showmemorypartition",
+                            "--showpower", "--json"], capture_output=True, text=True, timeout=20)
+        d = json.loads(r.stdout)
+        card = next(iter(v for k, v in d.items() if k.startswith("card")), {})
+        keep = ("sclk", "mclk", "fclk", "partition", "power")
+        info["smi"] = {k: v for k, v in card.items() if any(s in k.lower() for s in keep)}
+    except Exception as e:   # noqa: BLE001 - informational only
+        info["smi"] = f"unavailable ({type(e).__name__})"
+    return info
+
+
+# ---------------------------------------------------------------------------------------------------
+# synthetic inputs (SURVEY §8d)
+def synthetic_charged(B, N, seed):
+    """SURVEY §8d generator: positions ~ N(0, sigma^2), sigma = (N/5)^(1/3); unit direction x 0.5
+    velocities; charges +-1 with p = 1/2."""
+    g = torch.Generator().manual_seed(seed)
+    sigma = (N / 5.0) ** (1.0 / 3.0)
+    loc = torch.randn(B, N, 3, generator=g) * sigma
+    vel = torch.randn(B, N, 3, generator=g)
+    vel = vel / vel.norm(dim=-1, keepdim=True) * 0.5
+    q = (torch.randint(0, 2, (B, N, 1), generator=g) * 2 - 1).float()
+    return loc, vel, q
+
+
+def synthetic_gravity(B, N, seed):
+    """SURVEY §8d gravity generator: masses 1 + 0.1 N(0,1); positions, velocities ~ N(0,1) with the
+    centre-of-mass velocity removed (synthetic_sim.py:370-378)."""
+    g = torch.Generator().manual_seed(seed)
+    mass = 1.0 + 0.1 * torch.randn(B, N, 1, generator=g)
+    loc = torch.randn(B, N, 3, generator=g)
+    vel = torch.randn(B, N, 3, generator=g)
+    vel = vel - (mass * vel).sum(1, keepdim=True) / mass.sum(1, keepdim=True)
+    return loc, vel, mass
+
+
+def rank_batch(B_per, world, rank, N, seed):
+    """This rank's shard of the global synthetic batch of B_per * world samples (weak scaling: the
+    per-GPU batch is fixed). Concatenating every rank's shard gives the global batch."""
+    from no_node_comparison_amd.sharding import shard_range
+    loc, vel, q = synthetic_charged(B_per * world, N, seed)
+    lo, hi = shard_range(B_per * world, world, rank)
+    return loc[lo:hi], vel[lo:hi], q[lo:hi]
+
+
+def build_egno_case(B, N, T, seed, dev, world=1, rank=0, plan=None):
     import no_node_comparison_amd as pkg
-    loc, vel, q = rank_batch(B, world, rank, N, seed)
+    if plan is None:
+        loc, vel, q = rank_batch(B, world, rank, N, seed)
+    else:
+        loc, vel, q = synthetic_charged(plan["B_global"], N, seed)
+        loc, vel, q = loc[plan["lo"]:plan["hi"]], vel[plan["lo"]:plan["hi"]], q[plan["lo"]:plan["hi"]]
     edges = pkg.harness.get_edges(B, N, dev)
     loc, vel, q = loc.to(dev), vel.to(dev), q.to(dev)
     qq = q.reshape(-1, 1)
     eao = qq[edges[0]] * qq[edges[1]]
     x, v, ea, nodes, lm = pkg.harness.prepare_inputs(loc, vel, eao, edges, N, 1, q)
     t_out = torch.arange(1, T + 1, device=dev).repeat(B, 1)
-    return dict(x=x, h=nodes, edges=edges, edge_fea=ea, v=v, loc_mean=lm, t_out=t_out)
+    return dict(x=x, h=nodes, edges=edges, edge_fea=ea, v=v, loc_mean=lm, t_out=t_out, eao=eao, q=q)
 
 
-def cpu_baseline_egno(model, case, N, T, budget_s=12.0, max_b=64):
-    """Oracle (numpy restatement, test infrastructure) on the host cores over a bounded sample of
-    the same workload: the first samples of rank 0's batch."""
-    from oracle import egno as oe
-    from oracle import harness as oh
-    try:
-        import threadpoolctl
-        cores = max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
-    except Exception:
-        cores = os.cpu_count() or 1
-    p = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
-    Bc = max_b
-    r, c = oh.full_edges(Bc, N)
-    sl = lambda t, w: t[: Bc * w].detach().cpu().numpy()  # noqa: E731
-    args = dict(x=sl(case["x"], N), h=sl(case["h"], N), row=r, col=c, edge_fea=sl(case["edge_fea"], N * (N - 1)),
-                v=sl(case["v"], N), loc_mean=sl(case["loc_mean"], N), t_out=case["t_out"][:Bc].cpu().numpy())
-    done, t0, out = 0, time.perf_counter(), None
-    while True:
-        out = oe.egno_forward(p, **args, T=T)
-        done += 1
-        if time.perf_counter() - t0 > budget_s or done >= 20:
+# ---------------------------------------------------------------------------------------------------
+# CPU baseline: the reference's torch operators on the host cores (oracle/torch_ref.py)
+def cpu_time(fn, budget_s, min_calls=1, max_calls=20):
+    """Median wall time of fn() over as many calls as fit in budget_s (at least min_calls)."""
+    times, out = [], None
+    t_all = time.perf_counter()
+    while len(times) < max_calls:
+        t0 = time.perf_counter()
+        out = fn()
+        times.append(time.perf_counter() - t0)
+        if len(times) >= min_calls and time.perf_counter() - t_all + times[-1] > budget_s:
             break
-    el = time.perf_counter() - t0
-    return {"value": Bc * done / el, "unit": "trajectories/s", "cores": int(cores), "kind": "port",
-            "sample": f"oracle/egno.py (numpy fp32) EGNO forward, B={Bc} of the same synthetic batch, "
-                      f"N={N}, T={T}, {done} calls in {el:.1f} s"}, out, Bc
+    return float(np.median(times)), len(times), out
 
 
-def run_egno(args, world, rank, dev):
+def _cpu(t, rows=None):
+    t = t.detach()
+    return (t[:rows] if rows is not None else t).cpu()
+
+
+def _cpu_params(model):
+    return {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+
+
+def _baseline(units, med, calls, sample, unit="trajectories/s"):
+    return {"value": units / med, "unit": unit, "cores": torch.get_num_threads(), "kind": "torch-ref",
+            "median_s_per_call": med, "calls": calls,
+            "sample": sample + f"; oracle/torch_ref.py (the reference's torch ops, op by op) on "
+                               f"{torch.get_num_threads()} host threads, median of {calls} calls"}
+
+
+def _parity(got, ref, key="pos"):
+    got = got.double().numpy()
+    ref = ref.double().numpy()
+    return {f"{key}_mse_vs_ref": float(np.mean((got - ref) ** 2)),
+            f"{key}_maxnorm_rel_vs_ref": float(np.abs(got - ref).max() / np.abs(ref).max())}
+
+
+# ---------------------------------------------------------------------------------------------------
+# workloads
+def _result(args, world, plan, ms, value, name, extra_cfg, backend, allreduce_bytes=0, **kw):
+    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": plan["scaling"],
+           "vs_baseline": None, "dtype": DTYPE, "data": "synthetic (SURVEY §8d generators, seeded)",
+           "world_size": world, "backend": backend, "allreduce_bytes_per_step": allreduce_bytes,
+           "config": dict({"workload": name, "batch_per_gpu": plan["B"], "global_batch": plan["B_global"]},
+                          **extra_cfg)}
+    res.update(kw)
+    return res
+
+
+def run_egno(args, world, rank, dev, backend):
     import no_node_comparison_amd as pkg
-    B, N, T = args.batch, 20, 10
+    from no_node_comparison_amd import _lib
+    from no_node_comparison_amd.sharding import max_over_ranks
+    N, T = 20, 10
+    plan = batch_plan(args, world, rank, 512)
+    B = plan["B"]
     torch.manual_seed(0)
     model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
                      num_timesteps=T, time_emb_dim=32, device=dev).eval()
-    case = build_egno_case(B, N, T, seed=1234, dev=dev, world=world, rank=rank)
-    from no_node_comparison_amd import _lib
+    case = build_egno_case(B, N, T, seed=1234, dev=dev, plan=plan)
     call = lambda: model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],  # noqa: E731
                          loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
     with torch.no_grad():
@@ -180,80 +313,64 @@ def run_egno(args, world, rank, dev):
             for _ in range(args.steps):
                 out = call()
             records = _lib.profile_end()
-    layer_events = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
-    tconv_ms = [ms for kind, ms in records if kind in (2, 3)]
-    from no_node_comparison_amd.sharding import max_over_ranks
     el = max_over_ranks(el, dev)
-    ms = el / args.steps * 1e3
-    value = B * world * args.steps / el
-    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d charged generator, seeded)",
-           "frames_per_s": value * T,
-           "config": {"workload": "C2: EGNO forward (4 layers, hidden 64, 2 modes), charged N=20, T=10, "
-                                  f"B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world, "n_balls": N,
-                      "num_timesteps": T, "parallelism": f"batch-sharded replicas x{world} (no collective)"}}
-    # dominant kernel: egnn_layer_kernel, timed live with HIP events on the launch stream
+    value = plan["B_global"] * args.steps / el
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
+    res = _result(args, world, plan, el / args.steps * 1e3, value,
+                  f"C2: EGNO forward (4 layers, hidden 64, 2 modes), charged N={N}, T={T}, B={B} per GPU",
+                  {"n_balls": N, "num_timesteps": T, "layer_workgroups": min(T * B, cus),
+                   "parallelism": f"batch-sharded replicas x{world} (no collective)"}, backend,
+                  frames_per_s=value * T)
+    layer_events = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
+    tconv_ms = [ms for kind, ms in records if kind in (_lib.PROF_TCONV, _lib.PROF_TCONV_FIRST)]
     if layer_events:
-        durs = layer_events
-        avg_ms = float(np.mean(durs))
-        E = T * B * N * (N - 1)
-        n = T * B * N
+        avg_ms = float(np.mean(layer_events))
+        E, n = T * B * N * (N - 1), T * B * N
         flop = 2.0 * (E * MAC_PER_EDGE + n * MAC_PER_NODE)
         achieved = flop / (avg_ms * 1e-3) / 1e12
+        agg_gbs = AGG_BYTES(E, n) / (avg_ms * 1e-3) / 1e9
         res["roofline"] = {"kernel": "egnn_layer_kernel<EGNO>", "bound": "mfma", "achieved": achieved,
                            "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
                            "frac_of_fp32_mfma_peak": achieved / FP32_PEAK_TFLOPS,
                            "traffic": pmc_traffic("egnn_layer_kernel<EGNO>"), "avg_launch_ms": avg_ms,
-                           "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(durs),
-                           "tconv_avg_launch_ms": float(np.mean(tconv_ms)) if tconv_ms else None}
+                           "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(layer_events),
+                           "tconv_avg_launch_ms": float(np.mean(tconv_ms)) if tconv_ms else None,
+                           "north_star_hbm": {
+                               "materialised_aggregation_bytes_per_layer": AGG_BYTES(E, n),
+                               "equivalent_GBs": agg_gbs, "frac_of_hbm_peak": agg_gbs / HBM_PEAK_GBS,
+                               "note": "the reference's aggregation bytes (messages materialised, SURVEY §8d) "
+                                       "over the fused layer's time; this build never materialises messages, "
+                                       "so HBM is not its bound and the kernel is priced against the MFMA "
+                                       "ceiling (DESIGN.md §3.1)"}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, ref_out, Bc = cpu_baseline_egno(model, case, N, T)
-        res["cpu_baseline"] = cb
-        x = out[0].view(T, B, N, 3)[:, :Bc].reshape(-1, 3).double().cpu().numpy()
-        xr = ref_out[0]
-        res["parity"] = {"pos_mse_vs_oracle": float(np.mean((x - xr) ** 2)),
-                         "pos_maxnorm_rel_vs_oracle": float(np.abs(x - xr).max() / np.abs(xr).max()),
-                         "samples_checked": Bc}
+        from oracle import torch_ref as tr
+        p = _cpu_params(model)
+        r, c = tr.full_edges(B, N)
+        inp = [_cpu(case[k]) for k in ("x", "h")] + [r, c] + [_cpu(case[k]) for k in ("edge_fea", "v", "loc_mean")]
+        t_out = _cpu(case["t_out"])
+        with torch.no_grad():
+            med, calls, ref = cpu_time(lambda: tr.egno_forward(p, *inp, t_out, T=T), args.cpu_budget, 3)
+        res["cpu_baseline"] = _baseline(B, med, calls, f"EGNO forward at the measured batch B={B}, N={N}, T={T}")
+        res["parity"] = dict(_parity(_cpu(out[0]), ref[0]), samples_checked=B,
+                             bar="1e-5 max-norm relative (north_star)")
     return res
 
 
-def synthetic_gravity(B, N, seed):
-    """SURVEY §8d gravity generator: masses 1 + 0.1 N(0,1); positions, velocities ~ N(0,1) with the
-    centre-of-mass velocity removed (synthetic_sim.py:370-378)."""
-    g = torch.Generator().manual_seed(seed)
-    mass = 1.0 + 0.1 * torch.randn(B, N, 1, generator=g)
-    loc = torch.randn(B, N, 3, generator=g)
-    vel = torch.randn(B, N, 3, generator=g)
-    vel = vel - (mass * vel).sum(1, keepdim=True) / mass.sum(1, keepdim=True)
-    return loc, vel, mass
-
-
-def c5_substeps(total=50, seed=0):
-    """C5 multi-horizon substep list: draws in [5, 10) from default_rng(0) until they sum to 50
-    (the last one clipped), SURVEY §8d."""
-    rng = np.random.default_rng(seed)
-    out = []
-    while sum(out) < total:
-        out.append(int(min(rng.integers(5, 10), total - sum(out))))
-    return out
-
-
-def run_segno(args, world, rank, dev, gravity=False):
+def run_segno(args, world, rank, dev, backend, gravity=False):
     """C3 (SEGNO charged N=20, B=512 per GPU, one forward of 10 substeps) or C5 (SEGNO gravity
     N=100, B=256 per GPU, a 50-frame multi-horizon rollout: segments of c5_substeps() substeps)."""
     import no_node_comparison_amd as pkg
+    from no_node_comparison_amd import _lib
     from no_node_comparison_amd.sharding import max_over_ranks
     N = 100 if gravity else 20
-    B = args.batch if args.batch != 512 or not gravity else 256
+    plan = batch_plan(args, world, rank, 256 if gravity else 512)
+    B = plan["B"]
     torch.manual_seed(0)
     model = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=4, recurrent=True, device=dev).eval()
     gen = synthetic_gravity if gravity else synthetic_charged
-    loc, vel, q = gen(B * world, N, 4321)
-    from no_node_comparison_amd.sharding import shard_range
-    lo, hi = shard_range(B * world, world, rank)
-    loc, vel, q = loc[lo:hi].to(dev), vel[lo:hi].to(dev), q[lo:hi].to(dev)
+    loc, vel, q = gen(plan["B_global"], N, 4321)
+    loc, vel, q = (t[plan["lo"]:plan["hi"]].to(dev) for t in (loc, vel, q))
     edges = pkg.harness.get_edges(B, N, dev)
     x = loc.reshape(-1, 3)
     v = vel.reshape(-1, 3)
@@ -268,30 +385,31 @@ def run_segno(args, world, rank, dev, gravity=False):
                                              energy_dataset="gravity", batch_size=B)[0]
         return model(his, x, edges, v, ea, T=steps[0])[0]
 
-    from no_node_comparison_amd import _lib
     with torch.no_grad():
         _prewarm(call, args, dev)
         for _ in range(args.warmup):
             call()
         barrier_sync(world, dev)
-        if args.kernel_events:
-            _lib.profile_begin(8 * args.steps * len(steps) + 64)
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            call()
+            out = call()
         barrier_sync(world, dev)
         el = time.perf_counter() - t0
-        records = _lib.profile_end() if args.kernel_events else []
+        records = []
+        if args.kernel_events:
+            _lib.profile_begin(8 * args.steps * len(steps) + 64)
+            for _ in range(args.steps):
+                out = call()
+            records = _lib.profile_end()
     el = max_over_ranks(el, dev)
-    value = B * world * args.steps / el
+    value = plan["B_global"] * args.steps / el
     name = "C5: SEGNO gravity N=100, 50-frame multi-horizon rollout (nonode_segno_rollout: per-segment " \
         "re-featurisation + gravity energy on the GPU)" if gravity else \
         "C3: SEGNO charged N=20, 10 integrator substeps (one fused launch)"
-    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d, seeded)",
-           "config": {"workload": f"{name}, B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world,
-                      "n_balls": N, "substeps": steps, "parallelism": f"batch-sharded replicas x{world}"}}
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
+    res = _result(args, world, plan, el / args.steps * 1e3, value, f"{name}, B={B} per GPU",
+                  {"n_balls": N, "substeps": steps, "layer_workgroups": min(B, cus),
+                   "parallelism": f"batch-sharded replicas x{world}"}, backend)
     layer = [ms for kind, ms in records if kind == _lib.VARIANT_SEGNO]
     if layer:
         E = B * N * (N - 1) * sum(steps) / len(steps)
@@ -303,40 +421,89 @@ def run_segno(args, world, rank, dev, gravity=False):
                            "achieved": ach, "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
                            "frac_of_fp32_mfma_peak": ach / FP32_PEAK_TFLOPS,
-                           "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
-                           "launches_timed": len(layer)}
+                           "traffic": pmc_traffic("egnn_layer_kernel<SEGNO>"), "avg_launch_ms": avg,
+                           "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(layer),
+                           "launch_ms_min_max": [float(np.min(layer)), float(np.max(layer))]}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import torch_ref as tr
+        p = _cpu_params(model)
+        if gravity:
+            # the dense one-hot mean (gcl.py:16-23) needs 259 GB per substep here: the scatter-mean
+            # variant (same values) on the first Bc samples
+            Bc = min(B, args.cpu_samples or 16)
+            r, c = tr.full_edges(Bc, N)
+            rows, erows = Bc * N, Bc * N * (N - 1)
+            args_c = (_cpu(his, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(ea, erows), steps,
+                      _cpu(q.reshape(-1), rows))
+            with torch.no_grad():
+                med, calls, ref = cpu_time(lambda: tr.segno_rollout(p, *args_c, dense_mean=False), args.cpu_budget)
+            res["cpu_baseline"] = _baseline(Bc, med, calls, f"SEGNO gravity rollout, first {Bc} samples of the "
+                                            f"batch, substeps {steps}, scatter mean (the reference's dense mean "
+                                            f"is infeasible at this size)")
+            got = _cpu(out).reshape(len(steps), B, N, 3)[:, :Bc].reshape(len(steps), -1, 3)
+            res["parity"] = dict(_parity(got[:1], ref[:1]), samples_checked=Bc,
+                                 all_segments=_parity(got, ref), bar="1e-5 max-norm relative, first segment")
+        else:
+            r, c = tr.full_edges(B, N)
+            args_c = (_cpu(his), _cpu(x), r, c, _cpu(v), _cpu(ea))
+            with torch.no_grad():
+                med, calls, ref = cpu_time(lambda: tr.segno_forward_step(p, *args_c, T=steps[0], dense_mean=True),
+                                           args.cpu_budget)
+            res["cpu_baseline"] = _baseline(B, med, calls, f"SEGNO embedding + forward_step at the measured batch "
+                                            f"B={B}, {steps[0]} substeps, the reference's dense one-hot mean")
+            res["parity"] = dict(_parity(_cpu(out), ref[0]), samples_checked=B,
+                                 bar="1e-5 max-norm relative (north_star)")
     return res
 
 
-def run_egno_train(args, world, rank, dev):
-    """C4: EGNO training step, charged N=20, T=10, B=512 per GPU (4096 over 8 GPUs): forward with
-    saved state, the reference loss (main_simulation_simple_no.py:273-280), backward through the HIP
-    kernels, ONE all-reduce of the flat gradient buffer (RCCL over xGMI), Adam(lr 1e-4, wd 1e-8,
-    model_confs.yaml:15-17)."""
+def run_egno_train(args, world, rank, dev, backend):
+    """C4: EGNO training step, charged N=20, T=10, B=512 per GPU (or --global-batch 4096 over the
+    ranks): forward with saved state, the reference loss (main_simulation_simple_no.py:273-280),
+    backward through the HIP kernels, ONE all-reduce of the flat gradient buffer (RCCL over xGMI),
+    Adam(lr 1e-4, wd 1e-8, model_confs.yaml:15-17). The loop is the reference's order:
+    optimizer.zero_grad(); loss.backward(); [all-reduce]; optimizer.step()."""
     import no_node_comparison_amd as pkg
     from no_node_comparison_amd.sharding import FlatGrads, max_over_ranks
     from no_node_comparison_amd import _lib
-    B, N, T = args.batch, 20, 10
+    N, T = 20, 10
+    plan = batch_plan(args, world, rank, 512)
+    B = plan["B"]
     torch.manual_seed(0)
     model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
                      num_timesteps=T, time_emb_dim=32, device=dev).train()
-    case = build_egno_case(B, N, T, seed=1234, dev=dev, world=world, rank=rank)
-    g = torch.Generator().manual_seed(777 + rank)
-    loc_true = torch.randn(B, N, T, 3, generator=g).to(dev)
+    p0 = _cpu_params(model)
+    case = build_egno_case(B, N, T, seed=1234, dev=dev, plan=plan)
+    g = torch.Generator().manual_seed(777)
+    loc_true = torch.randn(plan["B_global"], N, T, 3, generator=g)[plan["lo"]:plan["hi"]].to(dev)
     fg = FlatGrads(model.parameters())
     opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=1e-8)
 
+    def loss_of(x):
+        pred = x.reshape(T, B, N, 3).permute(1, 2, 0, 3)
+        # per-rank mean over its shard; with unequal strong-scaling shards the all-reduce averages
+        # shard means, so weight by the shard size to keep the global-mean gradient
+        w = B * world / plan["B_global"]
+        return torch.nn.functional.mse_loss(pred, loc_true, reduction="none").mean((0, 1, 3)).mean() * w
+
     def step():
-        fg.zero_()
+        opt.zero_grad()
         x, _, _ = model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],
                         loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
-        pred = x.reshape(T, B, N, 3).permute(1, 2, 0, 3)
-        loss = torch.nn.functional.mse_loss(pred, loc_true, reduction="none").mean((0, 1, 3)).mean()
+        loss = loss_of(x)
         loss.backward()
         fg.allreduce_()
         opt.step()
         return loss
 
+    grads0 = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # gradients of the first step at the initial weights, for the parity check below
+        opt.zero_grad()
+        x, _, _ = model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],
+                        loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
+        loss_of(x).backward()
+        fg.gather_()
+        grads0 = {k: _cpu(q.grad) for k, q in model.named_parameters()}
     _prewarm(step, args, dev)
     for _ in range(args.warmup):
         step()
@@ -346,26 +513,74 @@ def run_egno_train(args, world, rank, dev):
         loss = step()
     barrier_sync(world, dev)
     el = max_over_ranks(time.perf_counter() - t0, dev)
-    value = B * world * args.steps / el
-    return {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d, seeded)",
-            "loss": float(loss.detach()),
-            "config": {"workload": f"C4: EGNO training step (fwd + bwd + 1 all-reduce + Adam), charged N=20, T=10, "
-                                   f"B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world, "n_balls": N,
-                       "num_timesteps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
-                       "parallelism": f"data-parallel x{world}, one RCCL all-reduce per step"}}
+    records = []
+    if args.kernel_events:
+        _lib.profile_begin(64 * args.steps + 64)
+        for _ in range(args.steps):
+            step()
+        records = _lib.profile_end()
+    value = plan["B_global"] * args.steps / el
+    res = _result(args, world, plan, el / args.steps * 1e3, value,
+                  f"C4: EGNO training step (fwd + bwd + 1 all-reduce + Adam), charged N={N}, T={T}, B={B} per GPU",
+                  {"n_balls": N, "num_timesteps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                   "parallelism": f"data-parallel x{world}, one {backend or 'no'} all-reduce per step"},
+                  backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0, loss=float(loss.detach()))
+    e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
+    e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
+    if e0 and e1:
+        avg = float(np.mean(e0) + np.mean(e1))
+        E = T * B * N * (N - 1)
+        flop = 2.0 * E * MAC_PER_EDGE_BWD
+        ach = flop / (avg * 1e-3) / 1e12
+        layer = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
+        res["roofline"] = {"kernel": "edge_bwd_kernel (pass 0 + pass 1, one layer)", "bound": "mfma", "achieved": ach,
+                           "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
+                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
+                           "traffic": None, "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0)), float(np.mean(e1))],
+                           "algorithmic_gflop_per_launch": flop / 1e9,
+                           "algorithmic_basis": "reverse of W2 and Wc1 per edge (data + weight gradients); "
+                                                "the forward recompute is not counted",
+                           "launches_timed": len(e0) + len(e1),
+                           "share_of_step": float(np.sum(e0) + np.sum(e1)) / (el * 1e3),
+                           "forward_layer_avg_ms": float(np.mean(layer)) if layer else None}
+    if grads0 is not None:
+        from oracle import torch_ref as tr
+        Bc = min(B, args.cpu_samples or 512)
+        r, c = tr.full_edges(Bc, N)
+        rows, erows = Bc * N, Bc * N * (N - 1)
+        p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+        copt = torch.optim.Adam(list(p.values()), lr=1e-4, weight_decay=1e-8)
+        inp = [_cpu(case["x"], rows), _cpu(case["h"], rows), r, c, _cpu(case["edge_fea"], erows),
+               _cpu(case["v"], rows), _cpu(case["loc_mean"], rows)]
+        tgt, t_out = _cpu(loc_true, Bc), _cpu(case["t_out"], Bc)
+        first = {}
+
+        def cstep():
+            copt.zero_grad()
+            xx, _, _ = tr.egno_forward(p, *inp, t_out, T=T)
+            pred = xx.reshape(T, Bc, N, 3).permute(1, 2, 0, 3)
+            loss = torch.nn.functional.mse_loss(pred, tgt, reduction="none").mean((0, 1, 3)).mean()
+            loss.backward()
+            if not first:
+                first.update({k: t.grad.clone() for k, t in p.items() if t.grad is not None})
+            copt.step()
+
+        med, calls, _ = cpu_time(cstep, args.cpu_budget)
+        res["cpu_baseline"] = _baseline(Bc, med, calls, f"EGNO training step (forward, loss, autograd backward, "
+                                        f"Adam) at B={Bc}")
+        if Bc == B:
+            errs = {k: float((grads0[k] - first[k]).abs().max() / first[k].abs().max())
+                    for k in first if float(first[k].abs().max()) > 0}
+            worst = max(errs, key=errs.get)
+            res["parity"] = {"grad_maxnorm_rel_vs_ref_max": errs[worst], "worst_tensor": worst,
+                             "grad_maxnorm_rel_vs_ref_median": float(np.median(list(errs.values()))),
+                             "tensors_checked": len(errs), "samples_checked": B,
+                             "note": "first step's gradients at the initial weights, HIP backward vs torch "
+                                     "autograd of the op-by-op restatement (both fp32)"}
+    return res
 
 
-def _host_cores():
-    try:
-        import threadpoolctl
-        return max(i.get("num_threads", 1) for i in threadpoolctl.threadpool_info()) or 1
-    except Exception:
-        return os.cpu_count() or 1
-
-
-def run_egno_rollout(args, world, rank, dev):
+def run_egno_rollout(args, world, rank, dev, backend):
     """rollout_fn (main_simulation_simple_no.py:342-384) at the C2 shape, traj_len =
     10 segments (the script's --traj_len default, :79) with per-frame charged energies, as ONE
     native call (nonode_egno_rollout: 10 forwards + on-device re-featurisation + energy). A
@@ -373,16 +588,15 @@ def run_egno_rollout(args, world, rank, dev):
     import no_node_comparison_amd as pkg
     from no_node_comparison_amd import _lib
     from no_node_comparison_amd.sharding import max_over_ranks
-    B, N, T, L = args.batch, 20, 10, 10
+    N, T, L = 20, 10, 10
+    plan = batch_plan(args, world, rank, 512)
+    B = plan["B"]
     torch.manual_seed(0)
     model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
                      num_timesteps=T, time_emb_dim=32, device=dev).eval()
-    loc, vel, q = rank_batch(B, world, rank, N, 1234)
-    edges = pkg.harness.get_edges(B, N, dev)
-    loc, vel, q = loc.to(dev), vel.to(dev), q.to(dev)
-    qq = q.reshape(-1, 1)
-    eao = qq[edges[0]] * qq[edges[1]]
-    x, v, ea, nodes, lm = pkg.harness.prepare_inputs(loc, vel, eao, edges, N, 1, q)
+    case = build_egno_case(B, N, T, seed=1234, dev=dev, plan=plan)
+    edges, eao, q = case["edges"], case["eao"], case["q"]
+    x, v, ea, nodes, lm = case["x"], case["v"], case["edge_fea"], case["h"], case["loc_mean"]
     t_all = torch.arange(1, T * L + 1, device=dev, dtype=torch.float32).repeat(B, 1)
     call = lambda: pkg.harness.egno_rollout(model, nodes, x, edges, v, eao, ea, lm, N, L, B,  # noqa: E731
                                             charges=q.reshape(-1), num_steps=T, timesteps_out=t_all,
@@ -401,15 +615,12 @@ def run_egno_rollout(args, world, rank, dev):
         _lib.profile_begin(16 * L * 2 + 64)
         out = call()
         records = _lib.profile_end()
-    value = B * world * args.steps / el
-    res = {"metric": METRIC, "value": value, "unit": "trajectories/s", "n_gpus": world, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY §8d, seeded)",
-           "frames_per_s": value * T * L,
-           "config": {"workload": f"f1: EGNO rollout_fn, charged N=20, T=10, traj_len={L} (100 frames + per-frame "
-                                  f"energy), B={B} per GPU", "batch_per_gpu": B, "global_batch": B * world,
-                      "n_balls": N, "num_timesteps": T, "traj_len": L,
-                      "parallelism": f"batch-sharded replicas x{world} (no collective)"}}
+    value = plan["B_global"] * args.steps / el
+    res = _result(args, world, plan, el / args.steps * 1e3, value,
+                  f"f1: EGNO rollout_fn, charged N={N}, T={T}, traj_len={L} (100 frames + per-frame energy), "
+                  f"B={B} per GPU", {"n_balls": N, "num_timesteps": T, "traj_len": L,
+                                     "parallelism": f"batch-sharded replicas x{world} (no collective)"},
+                  backend, frames_per_s=value * T * L)
     layer = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
     if layer:
         avg = float(np.mean(layer))
@@ -423,30 +634,32 @@ def run_egno_rollout(args, world, rank, dev):
                            "launches_timed": len(layer),
                            "layer_kernel_share": float(np.sum(layer)) / (el / args.steps * 1e3)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import harness as oh
-        p = {k: t.detach().cpu().numpy() for k, t in model.state_dict().items()}
-        Bc = 8
-        r, c = oh.full_edges(Bc, N)
-        cut = lambda t, w: t[: Bc * w].detach().cpu().numpy()  # noqa: E731
-        t_c = t_all[:Bc].cpu().numpy()
-        done, t0 = 0, time.perf_counter()
-        while True:
-            ref, _, _ = oh.egno_rollout(p, cut(nodes, N), cut(x, N), r, c, cut(v, N), cut(eao, N * (N - 1)),
-                                        cut(ea, N * (N - 1)), cut(lm, N), N, L, Bc, cut(q.reshape(-1), N), T=T,
-                                        t_out=t_c)
-            done += 1
-            if time.perf_counter() - t0 > 10.0 or done >= 5:
-                break
-        cel = time.perf_counter() - t0
-        res["cpu_baseline"] = {"value": Bc * done / cel, "unit": "trajectories/s", "cores": int(_host_cores()),
-                               "kind": "port", "sample": f"oracle/harness.py egno_rollout (numpy fp32 + f64 energy), "
-                               f"B={Bc} of the same batch, traj_len={L}, {done} calls in {cel:.1f} s"}
-        got = out[0][:T].reshape(T, B, N, 3)[:, :Bc].reshape(-1, 3).double().cpu().numpy()
-        want = ref[:T]
-        res["parity"] = {"first_segment_pos_maxnorm_rel_vs_oracle": float(np.abs(got - want.reshape(-1, 3)).max()
-                                                                           / np.abs(want).max()),
-                         "samples_checked": Bc}
+        from oracle import torch_ref as tr
+        p = _cpu_params(model)
+        Bc = min(B, args.cpu_samples or 64)
+        r, c = tr.full_edges(Bc, N)
+        rows, erows = Bc * N, Bc * N * (N - 1)
+        args_c = (_cpu(nodes, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(eao, erows), _cpu(ea, erows),
+                  _cpu(lm, rows), N, L, Bc, _cpu(q.reshape(-1), rows))
+        with torch.no_grad():
+            med, calls, ref = cpu_time(lambda: tr.egno_rollout(p, *args_c, T=T, t_out=_cpu(t_all, Bc)),
+                                       args.cpu_budget)
+        res["cpu_baseline"] = _baseline(Bc, med, calls, f"EGNO rollout_fn positions, first {Bc} samples of the "
+                                        f"batch, traj_len={L} (energies not included)")
+        got = _cpu(out[0][:T]).reshape(T, B, N, 3)[:, :Bc].reshape(T, Bc * N, 3)
+        res["parity"] = dict(_parity(got, ref[:T]), samples_checked=Bc,
+                             bar="1e-5 max-norm relative, first segment (later segments are chaotic)")
     return res
+
+
+def c5_substeps(total=50, seed=0):
+    """C5 multi-horizon substep list: draws in [5, 10) from default_rng(0) until they sum to 50
+    (the last one clipped), SURVEY §8d."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while sum(out) < total:
+        out.append(int(min(rng.integers(5, 10), total - sum(out))))
+    return out
 
 
 # ChargedParticlesSim (synthetic_sim.py:244-260) per ordered pair and step, float64, as the kernel
@@ -456,15 +669,16 @@ FLOP_PER_PAIR_CHARGED = 22
 FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, AMD spec (not in the microarch guide)
 
 
-def run_sim_charged(args, world, rank, dev):
+def run_sim_charged(args, world, rank, dev, backend):
     """ChargedParticlesSim.sample_trajectory (synthetic_sim.py:220-296) as
     generate_dataset.py's documented charged N=20 run (its header, :10: --length 20000,
     --sample-freq 100; 3000 training simulations): S trajectories integrated in one launch from
     initial states already in HBM. A trajectory is one 20000-step simulation (199 saved frames)."""
     import no_node_comparison_amd as pkg
     from no_node_comparison_amd import _lib
-    from no_node_comparison_amd.sharding import max_over_ranks, shard_range
-    S = args.batch if args.batch != 512 else 3000
+    from no_node_comparison_amd.sharding import max_over_ranks
+    plan = batch_plan(args, world, rank, 3000)
+    S = plan["B"]
     N, Tn, freq = 20, 20000, 100
     sim = pkg.sim.ChargedParticlesSim(n_balls=N, vel_norm=0.5)
     np.random.seed(43 + rank)
@@ -486,14 +700,13 @@ def run_sim_charged(args, world, rank, dev):
     el = time.perf_counter() - t0
     records = _lib.profile_end() if args.kernel_events else []
     el = max_over_ranks(el, dev)
-    value = S * world * args.steps / el
-    res = {"metric": "simulated N-body trajectories/s (charged, N=20, 20000 leapfrog steps)", "value": value,
-           "unit": "trajectories/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "f64", "data": "synthetic initial states (the reference's draws, np seed 43 + rank)",
-           "config": {"workload": f"f3: ChargedParticlesSim N={N}, length {Tn}, sample_freq {freq}, S={S} per GPU",
-                      "sims_per_gpu": S, "n_balls": N, "length": Tn, "sample_freq": freq,
-                      "parallelism": f"independent simulations x{world}"}}
+    value = plan["B_global"] * args.steps / el
+    res = _result(args, world, plan, el / args.steps * 1e3, value,
+                  f"f3: ChargedParticlesSim N={N}, length {Tn}, sample_freq {freq}, S={S} per GPU",
+                  {"n_balls": N, "length": Tn, "sample_freq": freq, "parallelism": f"independent simulations x{world}"},
+                  backend)
+    res.update(metric="simulated N-body trajectories/s (charged, N=20, 20000 leapfrog steps)", dtype="f64",
+               data="synthetic initial states (the reference's draws, np seed 43 + rank)")
     sims = [ms for kind, ms in records if kind == _lib.PROF_SIM_CHARGED]
     if sims:
         avg = float(np.mean(sims))
@@ -533,37 +746,48 @@ def pmc_traffic(kernel):
         return None
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="samples per GPU")
+    ap.add_argument("--batch", type=int, default=0, help="samples per GPU (weak scaling; 0 = the workload's default)")
+    ap.add_argument("--global-batch", type=int, default=0, help="total samples over all GPUs (strong scaling)")
     ap.add_argument("--workload", default="egno",
                     choices=["egno", "segno", "segno_gravity", "egno_train", "egno_rollout", "sim_charged"],
                     help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4; "
                          "egno_rollout = SURVEY row f1; sim_charged = row f3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU baseline work (median of calls)")
+    ap.add_argument("--cpu-samples", type=int, default=0, help="CPU baseline sample size where it is bounded")
     ap.add_argument("--prewarm-ms", type=float, default=300.0,
                     help="untimed clock-ramp calls (wall ms) before the W warmup steps")
     ap.add_argument("--no-kernel-events", dest="kernel_events", action="store_false")
-    args = ap.parse_args()
-    world, rank, dev = setup_dist()
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    if args.workload == "egno":
-        res = run_egno(args, world, rank, dev)
-    elif args.workload == "egno_train":
-        res = run_egno_train(args, world, rank, dev)
-    elif args.workload == "egno_rollout":
-        res = run_egno_rollout(args, world, rank, dev)
-    elif args.workload == "sim_charged":
-        res = run_sim_charged(args, world, rank, dev)
+    ap.add_argument("--check-launch", action="store_true", help=argparse.SUPPRESS)
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.global_batch and args.global_batch < args.gpus:
+        ap.error("--global-batch must be >= --gpus")
+    return args
+
+
+def main():
+    args = parse_args()
+    maybe_launch(args)            # before anything touches the GPU
+    world, rank, dev, backend = setup_dist(args)
+    if args.check_launch:
+        res = check_launch(args, world, rank, dev, backend)
     else:
-        res = run_segno(args, world, rank, dev, gravity=args.workload == "segno_gravity")
+        runners = {"egno": run_egno, "egno_train": run_egno_train, "egno_rollout": run_egno_rollout,
+                   "sim_charged": run_sim_charged, "segno": run_segno,
+                   "segno_gravity": lambda *a: run_segno(*a, gravity=True)}
+        res = runners[args.workload](args, world, rank, dev, backend)
+        if rank == 0:
+            res["prewarm_ms"] = args.prewarm_ms
+            res["device"] = device_info(dev)
     if rank == 0:
-        res["prewarm_ms"] = args.prewarm_ms
-        print(json.dumps(res))
+        print(json.dumps(res), flush=True)
     if world > 1:
         _barrier(dev)
         dist.destroy_process_group()

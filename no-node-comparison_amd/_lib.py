@@ -29,7 +29,7 @@ SYMBOLS = (
 VARIANT_EGNO = 0
 VARIANT_SEGNO = 1
 # profile_end() record kinds beyond the two layer variants (csrc/nonode.hip ProfScope)
-PROF_TCONV, PROF_TCONV_FIRST, PROF_SIM_CHARGED, PROF_SIM_GRAVITY = 2, 3, 4, 5
+PROF_TCONV, PROF_TCONV_FIRST, PROF_SIM_CHARGED, PROF_SIM_GRAVITY, PROF_EDGE_BWD0, PROF_EDGE_BWD1 = 2, 3, 4, 5, 6, 7
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int

@@ -121,7 +121,7 @@ struct ProfState {
 
 // record kinds: 0 / 1 egnn_layer_kernel<EGNO / SEGNO>, 2 / 3 tconv_kernel (later / first layer),
 // 4 / 5 sim_charged_kernel / sim_gravity_kernel
-constexpr int PROF_SIM_CHARGED = 4, PROF_SIM_GRAVITY = 5;
+constexpr int PROF_SIM_CHARGED = 4, PROF_SIM_GRAVITY = 5, PROF_EDGE_BWD0 = 6, PROF_EDGE_BWD1 = 7;
 
 struct ProfScope {
   int slot = -1;

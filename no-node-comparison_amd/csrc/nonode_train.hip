@@ -863,10 +863,16 @@ int launch_edge_bwd(int ne, EdgeBwdArgs a, int G, hipStream_t s) {
     });
     size_t lds = 0;
     if (int rc = edge_bwd_config(0, a.n_graphs, a.N, G, &a.ct, &a.s_max, &lds)) return rc;
-    hipLaunchKernelGGL(k0, dim3(G), dim3(256), lds, s, a);
+    {
+      ProfScope prof(PROF_EDGE_BWD0, s);
+      hipLaunchKernelGGL(k0, dim3(G), dim3(256), lds, s, a);
+    }
     if (int rc = check_launch("edge_bwd_kernel<pass 0>")) return rc;
     if (int rc = edge_bwd_config(1, a.n_graphs, a.N, G, &a.ct, &a.s_max, &lds)) return rc;
-    hipLaunchKernelGGL(k1, dim3(G), dim3(256), lds, s, a);
+    {
+      ProfScope prof(PROF_EDGE_BWD1, s);
+      hipLaunchKernelGGL(k1, dim3(G), dim3(256), lds, s, a);
+    }
     return check_launch("edge_bwd_kernel<pass 1>");
   };
   switch (ne) {

@@ -35,3 +35,35 @@ def maxnorm_rel(a, b):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+# ------------------------------------------------------------------------------------------------
+# measured parity errors: every check_rel() call records (test, quantity, error, bar); the terminal
+# summary prints them and NONODE_PARITY_REPORT=<path> also writes them as JSON
+_PARITY = []
+
+
+def check_rel(name, got, ref, bar):
+    """Assert maxnorm_rel(got, ref) < bar and record the measured error."""
+    if hasattr(got, "detach"):
+        got = got.detach().cpu().numpy()
+    if hasattr(ref, "detach"):
+        ref = ref.detach().cpu().numpy()
+    err = maxnorm_rel(got, ref)
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    _PARITY.append({"test": test, "quantity": name, "maxnorm_rel": err, "bar": bar})
+    assert err < bar, (name, err, bar)
+    return err
+
+
+def pytest_terminal_summary(terminalreporter):
+    if not _PARITY:
+        return
+    terminalreporter.write_sep("-", "measured parity (max-norm relative error / bar)")
+    for r in _PARITY:
+        terminalreporter.write_line(f"{r['maxnorm_rel']:.3e} / {r['bar']:.0e}  {r['quantity']:<48s} {r['test']}")
+    path = os.environ.get("NONODE_PARITY_REPORT")
+    if path:
+        import json
+        with open(path, "w") as f:
+            json.dump(_PARITY, f, indent=1)

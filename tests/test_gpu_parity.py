@@ -14,7 +14,7 @@ import no_node_comparison_amd as pkg
 from oracle import egno as oe
 from oracle import harness as oh
 from oracle import segno as osg
-from tests.conftest import load_golden, maxnorm_rel, params_of
+from tests.conftest import check_rel, load_golden, maxnorm_rel, params_of
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -56,9 +56,9 @@ def test_egno_forward_matches_reference_golden():
         x, v, h = m(_dev(fx["in::x"]), _dev(fx["in::h"]), [_dev(fx["in::row"]), _dev(fx["in::col"])],
                     _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]), loc_mean=_dev(fx["in::loc_mean"]),
                     timesteps_out=_dev(fx["in::t_out"]))
-    assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
-    assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
-    assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL
+    check_rel("x", x.cpu(), fx["out::x"], TOL)
+    check_rel("v", v.cpu(), fx["out::v"], TOL)
+    check_rel("h", h.cpu(), fx["out::h"], TOL)
 
 
 def test_egno_building_blocks_match_reference_layers():
@@ -85,9 +85,9 @@ def test_egno_building_blocks_match_reference_layers():
         pkg._lib.check(L.nonode_egno_tconv(BN, T, 2, P(h_in), P(x_in), P(v_in), P(lm), P(tblobs[i]), P(wx), P(ho),
                                            P(xo), P(vo), s))
         Y = fx[f"cap::tconvx{i}.out"]
-        assert maxnorm_rel(ho.cpu().reshape(T, BN, 64), fx[f"cap::tconv{i}.out"]) < TOL
-        assert maxnorm_rel(xo.cpu(), Y[..., 0].reshape(T * BN, 3) + np.tile(fx["in::loc_mean"], (T, 1))) < TOL
-        assert maxnorm_rel(vo.cpu(), Y[..., 1].reshape(T * BN, 3)) < TOL
+        check_rel("ho.reshape(T, BN, 64)", ho.cpu().reshape(T, BN, 64), fx[f"cap::tconv{i}.out"], TOL)
+        check_rel("xo", xo.cpu(), Y[..., 0].reshape(T * BN, 3) + np.tile(fx["in::loc_mean"], (T, 1)), TOL)
+        check_rel("vo", vo.cpu(), Y[..., 1].reshape(T * BN, 3), TOL)
         # EGNN layer on the reference's layer-i inputs
         x_l = _dev(fx[f"cap::layer{i}.in0"])
         h_l = _dev(fx[f"cap::tconv{i}.out"]).reshape(T * BN, 64)
@@ -95,8 +95,8 @@ def test_egno_building_blocks_match_reference_layers():
         h2, x2 = torch.empty_like(h_l), torch.empty_like(x_l)
         pkg._lib.check(L.nonode_egnn_layer(0, T * B, N, 2, B, P(h_l), P(x_l), P(v_l), P(ef), P(blobs[i]), 0.0, 1.0,
                                            0, P(h2), P(x2), None, s))
-        assert maxnorm_rel(x2.cpu(), fx[f"cap::layer{i}.out0"]) < TOL
-        assert maxnorm_rel(h2.cpu(), fx[f"cap::layer{i}.out2"]) < TOL
+        check_rel("x2", x2.cpu(), fx[f"cap::layer{i}.out0"], TOL)
+        check_rel("h2", h2.cpu(), fx[f"cap::layer{i}.out2"], TOL)
 
 
 def test_egno_rollout_matches_reference_golden():
@@ -111,10 +111,10 @@ def test_egno_rollout_matches_reference_golden():
         m, _dev(fx["in::h"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(fx["raw::edge_attr_o"]),
         _dev(fx["in::edge_attr"]), _dev(fx["in::loc_mean"]), N, Lr, B, charges=_dev(fx["raw::charges"]),
         num_steps=T, timesteps_out=t_full, energy_dataset="charged")
-    assert maxnorm_rel(preds[:T].cpu(), ro["out::loc_preds"][:T]) < TOL
+    check_rel("preds[:T]", preds[:T].cpu(), ro["out::loc_preds"][:T], TOL)
     # the second segment restarts from a chaotic random-init state
-    assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < 1e-4
-    assert maxnorm_rel(en_all[:T].cpu(), ro["out::energies_allsteps"][:T]) < 1e-4
+    check_rel("both segments", preds.cpu(), ro["out::loc_preds"], 1e-4)
+    check_rel("first-segment energies", en_all[:T].cpu(), ro["out::energies_allsteps"][:T], TOL)
 
 
 def test_segno_gcl_step_and_forward_step_match_reference_golden():
@@ -127,9 +127,9 @@ def test_segno_gcl_step_and_forward_step_match_reference_golden():
                                  _dev(fx["in::edge_attr"]), T=T)
         x1, h1, v1 = m.forward_step(_dev(fx["in::h_emb"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]),
                                     _dev(fx["in::edge_attr"]), T=1)
-    assert maxnorm_rel(x.cpu(), fx["step::x"]) < TOL
-    assert maxnorm_rel(v.cpu(), fx["step::v"]) < TOL
-    assert maxnorm_rel(h.cpu(), fx["step::h"]) < TOL
+    check_rel("x", x.cpu(), fx["step::x"], TOL)
+    check_rel("v", v.cpu(), fx["step::v"], TOL)
+    check_rel("h", h.cpu(), fx["step::h"], TOL)
     # one substep with n_layers = T = 1 vs the oracle's single GCL step (gcl.py:111-119)
     p = params_of(fx)
     hr, xr, vr = osg.gcl_forward(p, fx["in::h_emb"], fx["in::row"], fx["in::col"], fx["in::x"], fx["in::v"],
@@ -150,7 +150,7 @@ def test_segno_forward_integrator_and_bug_compat():
     with torch.no_grad():
         x, h, v = m(*args, T=T)
     assert np.array_equal(x.cpu().numpy(), fx["fwd::x"]) and np.array_equal(v.cpu().numpy(), fx["fwd::v"])
-    assert maxnorm_rel(h.cpu(), fx["fwd::h"]) < 1e-6
+    check_rel("h", h.cpu(), fx["fwd::h"], 1e-6)
 
 
 def test_segno_rollout_matches_reference_golden():
@@ -162,8 +162,8 @@ def test_segno_rollout_matches_reference_golden():
     preds, en = pkg.harness.segno_rollout(m, _dev(fx["in::his"]), _dev(fx["in::x"]), ei, _dev(fx["in::v"]),
                                           _dev(fx["in::edge_attr"]), 2, num_steps=[int(s) for s in ro["cfg::num_steps"]],
                                           charges=_dev(fx["raw::charges"]), energy_dataset="charged", batch_size=B)
-    assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < TOL
-    assert maxnorm_rel(en.cpu(), ro["out::energies"]) < 1e-4
+    check_rel("preds", preds.cpu(), ro["out::loc_preds"], TOL)
+    check_rel("en", en.cpu(), ro["out::energies"], 1e-4)
 
 
 def test_segno_gravity_n100_matches_reference_golden():
@@ -174,9 +174,9 @@ def test_segno_gravity_n100_matches_reference_golden():
     with torch.no_grad():
         hh = torch.nn.functional.linear(_dev(fx["in::his"]), m.embedding.weight, m.embedding.bias)
         x, h, v = m.forward_step(hh, _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(fx["in::edge_attr"]), T=T)
-    assert maxnorm_rel(x.cpu(), fx["step::x"]) < TOL
-    assert maxnorm_rel(v.cpu(), fx["step::v"]) < TOL
-    assert maxnorm_rel(h.cpu(), fx["step::h"]) < TOL
+    check_rel("x", x.cpu(), fx["step::x"], TOL)
+    check_rel("v", v.cpu(), fx["step::v"], TOL)
+    check_rel("h", h.cpu(), fx["step::h"], TOL)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -213,9 +213,9 @@ def test_egno_matches_oracle_across_shapes(B, N, T):
     with torch.no_grad():
         x, v, h = m(_dev(case["x"]), _dev(case["h"]), [_dev(case["row"]), _dev(case["col"])], _dev(case["edge_fea"]),
                     v=_dev(case["v"]), loc_mean=_dev(case["loc_mean"]), timesteps_out=_dev(case["t_out"]))
-    assert maxnorm_rel(x.cpu(), xr) < TOL
-    assert maxnorm_rel(v.cpu(), vr) < TOL
-    assert maxnorm_rel(h.cpu(), hr) < TOL
+    check_rel("x", x.cpu(), xr, TOL)
+    check_rel("v", v.cpu(), vr, TOL)
+    check_rel("h", h.cpu(), hr, TOL)
 
 
 @pytest.mark.gpu
@@ -231,9 +231,9 @@ def test_egno_mode_and_frame_bounds_match_oracle(T, modes):
     with torch.no_grad():
         x, v, h = m(_dev(case["x"]), _dev(case["h"]), [_dev(case["row"]), _dev(case["col"])], _dev(case["edge_fea"]),
                     v=_dev(case["v"]), loc_mean=_dev(case["loc_mean"]), timesteps_out=_dev(case["t_out"]))
-    assert maxnorm_rel(x.cpu(), xr) < TOL
-    assert maxnorm_rel(v.cpu(), vr) < TOL
-    assert maxnorm_rel(h.cpu(), hr) < TOL
+    check_rel("x", x.cpu(), xr, TOL)
+    check_rel("v", v.cpu(), vr, TOL)
+    check_rel("h", h.cpu(), hr, TOL)
 
 
 @pytest.mark.parametrize("B,N,T", [(1, 2, 3), (4, 5, 10), (9, 20, 10), (2, 60, 7), (1, 150, 2)])
@@ -251,9 +251,9 @@ def test_segno_matches_oracle_across_shapes(B, N, T):
     with torch.no_grad():
         xo, ho, vo = m(_dev(his.astype(np.float32)), _dev(x.astype(np.float32)), [_dev(r), _dev(c)],
                        _dev(v.astype(np.float32)), _dev(ea.astype(np.float32)), T=T)
-    assert maxnorm_rel(xo.cpu(), xr) < TOL
-    assert maxnorm_rel(vo.cpu(), vr) < TOL
-    assert maxnorm_rel(ho.cpu(), hr) < TOL
+    check_rel("xo", xo.cpu(), xr, TOL)
+    check_rel("vo", vo.cpu(), vr, TOL)
+    check_rel("ho", ho.cpu(), hr, TOL)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -288,9 +288,9 @@ def test_egno_c2_e3_equivariance_and_batch_independence():
         sh = torch.tensor([0.3, -1.2, 2.0], device=DEV)
         xo2, vo2, ho2 = m(x @ R.T + sh, nodes, edges, ea, v=v @ R.T, loc_mean=lm @ R.T + sh, timesteps_out=t)
     assert torch.isfinite(xo).all() and torch.isfinite(ho).all()
-    assert maxnorm_rel((xo @ R.T + sh).cpu(), xo2.cpu()) < 1e-4
-    assert maxnorm_rel((vo @ R.T).cpu(), vo2.cpu()) < 1e-4
-    assert maxnorm_rel(ho.cpu(), ho2.cpu()) < 1e-4
+    check_rel("(xo @ R.T + sh)", (xo @ R.T + sh).cpu(), xo2.cpu(), 1e-4)
+    check_rel("(vo @ R.T)", (vo @ R.T).cpu(), vo2.cpu(), 1e-4)
+    check_rel("ho", ho.cpu(), ho2.cpu(), 1e-4)
     # batch independence: samples 17..19 run alone
     loc, vel, q, eao = raw
     sl = slice(17, 20)
@@ -300,29 +300,51 @@ def test_egno_c2_e3_equivariance_and_batch_independence():
     with torch.no_grad():
         xs, vs, hs = m(x3, n3, e3, ea3, v=v3, loc_mean=lm3, timesteps_out=t[:3])
     big = xo.view(T, B, N, 3)[:, sl].reshape(-1, 3)
-    assert maxnorm_rel(xs.cpu(), big.cpu()) < 1e-5
+    check_rel("xs", xs.cpu(), big.cpu(), 1e-5)
 
 
-def test_egno_c2_oracle_parity_on_sample_subset():
-    """C2 batch, oracle check on a handful of samples (the oracle is too slow for all 512)."""
+def test_egno_c2_whole_batch_matches_f64_reference():
+    """The whole C2 batch (B=512, N=20, T=10) against oracle/torch_ref.py — the reference's torch
+    operators, op by op — in float64 (pinned to the reference's fixtures by tests/test_torch_ref.py)."""
+    from oracle import torch_ref as tr
     B, N, T = 512, 20, 10
     m = _egno(T=T, seed=11)
     x, nodes, edges, ea, v, lm, t, raw = _egno_full(B, N, T, seed=6)
     with torch.no_grad():
         xo, vo, ho = m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)
-    loc, vel, q, eao = raw
-    idx = [0, 255, 511]
-    p = _sd_np(m)
-    for b in idx:
-        r, c = oh.full_edges(1, N)
-        case = dict(x=x.view(B, N, 3)[b].cpu().numpy().astype(np.float64),
-                    h=nodes.view(B, N, 2)[b].cpu().numpy().astype(np.float64), row=r, col=c,
-                    edge_fea=ea.view(B, N * (N - 1), 2)[b].cpu().numpy().astype(np.float64),
-                    v=v.view(B, N, 3)[b].cpu().numpy().astype(np.float64),
-                    loc_mean=lm.view(B, N, 3)[b].cpu().numpy().astype(np.float64), t_out=t[:1].cpu().numpy())
-        xr, vr, hr = oe.egno_forward(p, **case, T=T)
-        assert maxnorm_rel(xo.view(T, B, N, 3)[:, b].reshape(-1, 3).cpu(), xr) < TOL
-        assert maxnorm_rel(ho.view(T, B, N, 64)[:, b].reshape(-1, 64).cpu(), hr) < TOL
+    p = {k: v_.detach().cpu().double() for k, v_ in m.state_dict().items()}
+    r, c = tr.full_edges(B, N)
+    d = lambda a: a.detach().cpu().double()  # noqa: E731
+    with torch.no_grad():
+        xr, vr, hr = tr.egno_forward(p, d(x), d(nodes), r, c, d(ea), d(v), d(lm), t.cpu(), T=T)
+    check_rel("C2 x (512 samples)", xo, xr, TOL)
+    check_rel("C2 v (512 samples)", vo, vr, TOL)
+    check_rel("C2 h (512 samples)", ho, hr, TOL)
+
+
+def test_segno_c3_whole_batch_matches_f64_reference():
+    """The whole C3 batch (B=512, N=20, 10 substeps) against the f64 torch restatement (scatter mean:
+    the same values as gcl.py:16-23's dense mean, tests/test_torch_ref.py)."""
+    from oracle import torch_ref as tr
+    B, N, T = 512, 20, 10
+    m = _segno(seed=7)
+    loc, vel, q = synthetic_charged(B, N, seed=12)
+    x = loc.reshape(-1, 3).to(DEV)
+    v = vel.reshape(-1, 3).to(DEV)
+    edges = pkg.harness.get_edges(B, N, DEV)
+    qq = q.reshape(-1, 1).to(DEV)
+    ea = torch.cat([qq[edges[0]] * qq[edges[1]], ((x[edges[0]] - x[edges[1]]) ** 2).sum(1, keepdim=True)], 1)
+    his = v.norm(dim=1, keepdim=True)
+    with torch.no_grad():
+        xo, ho, vo = m(his, x, edges, v, ea, T=T)
+    p = {k: v_.detach().cpu().double() for k, v_ in m.state_dict().items()}
+    r, c = tr.full_edges(B, N)
+    d = lambda a: a.detach().cpu().double()  # noqa: E731
+    with torch.no_grad():
+        xr, hr, vr = tr.segno_forward_step(p, d(his), d(x), r, c, d(v), d(ea), T=T, dense_mean=False)
+    check_rel("C3 x (512 samples)", xo, xr, TOL)
+    check_rel("C3 v (512 samples)", vo, vr, TOL)
+    check_rel("C3 h (512 samples)", ho, hr, TOL)
 
 
 def test_segno_c3_equivariance_and_permutation():
@@ -340,9 +362,9 @@ def test_segno_c3_equivariance_and_permutation():
         R = _rotation(4).to(DEV)
         xo2, ho2, vo2 = m(his, x @ R.T + 1.5, edges, v @ R.T, ea, T=T)
     assert torch.isfinite(xo).all()
-    assert maxnorm_rel((xo @ R.T + 1.5).cpu(), xo2.cpu()) < 1e-4
-    assert maxnorm_rel((vo @ R.T).cpu(), vo2.cpu()) < 1e-4
-    assert maxnorm_rel(ho.cpu(), ho2.cpu()) < 1e-4
+    check_rel("(xo @ R.T + 1.5)", (xo @ R.T + 1.5).cpu(), xo2.cpu(), 1e-4)
+    check_rel("(vo @ R.T)", (vo @ R.T).cpu(), vo2.cpu(), 1e-4)
+    check_rel("ho", ho.cpu(), ho2.cpu(), 1e-4)
 
 
 def test_rejects_bad_inputs_loudly():
@@ -377,9 +399,9 @@ def test_egno_five_modes_matches_reference_golden():
     with torch.no_grad():
         x, v, h = m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
                     loc_mean=_dev(fx["in::loc_mean"]), timesteps_out=_dev(fx["in::t_out"]))
-    assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
-    assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
-    assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL
+    check_rel("x", x.cpu(), fx["out::x"], TOL)
+    check_rel("v", v.cpu(), fx["out::v"], TOL)
+    check_rel("h", h.cpu(), fx["out::h"], TOL)
 
 
 def test_egno_multi_input_matches_reference_golden():
@@ -395,9 +417,9 @@ def test_egno_multi_input_matches_reference_golden():
         x, v, h = m(_dev(fx["in::x"]), _dev(fx["in::h"]), edges, _dev(fx["in::edge_attr"]), v=_dev(fx["in::v"]),
                     loc_mean=_dev(fx["in::loc_mean"]), timesteps_in=_dev(fx["in::t_in"]),
                     timesteps_out=_dev(fx["in::t_out"]))
-    assert maxnorm_rel(x.cpu(), fx["out::x"]) < TOL
-    assert maxnorm_rel(v.cpu(), fx["out::v"]) < TOL
-    assert maxnorm_rel(h.cpu(), fx["out::h"]) < TOL
+    check_rel("x", x.cpu(), fx["out::x"], TOL)
+    check_rel("v", v.cpu(), fx["out::v"], TOL)
+    check_rel("h", h.cpu(), fx["out::h"], TOL)
 
 
 def test_segno_multi_input_attn_matches_reference_golden():
@@ -414,9 +436,9 @@ def test_segno_multi_input_attn_matches_reference_golden():
         with torch.no_grad():
             x, h, v = m(_dev(fx["in::his"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(fx["in::edge_attr"]),
                         T=T, in_steps=_dev(fx["in::in_steps"]))
-        assert maxnorm_rel(x.cpu(), fx[pre + "::x"]) < TOL
-        assert maxnorm_rel(h.cpu(), fx[pre + "::h"]) < TOL
-        assert maxnorm_rel(v.cpu(), fx[pre + "::v"]) < TOL
+        check_rel("x", x.cpu(), fx[pre + "::x"], TOL)
+        check_rel("h", h.cpu(), fx[pre + "::h"], TOL)
+        check_rel("v", v.cpu(), fx[pre + "::v"], TOL)
 
 
 def test_egno_multi_input_rollout_matches_reference_golden():
@@ -434,10 +456,10 @@ def test_egno_multi_input_rollout_matches_reference_golden():
         m, _dev(fx["in::h"]), _dev(fx["in::x"]), edges, _dev(fx["in::v"]), _dev(ro["raw::edge_attr_o"]),
         _dev(fx["in::edge_attr"]), _dev(fx["in::loc_mean"]), N, Lr, B, charges=_dev(ro["raw::charges"]),
         num_steps=T, timesteps_in=_dev(fx["in::t_in"]), timesteps_out=_dev(ro["in::t_out"]), energy_dataset="charged")
-    assert maxnorm_rel(preds[:T].cpu(), ro["out::loc_preds"][:T]) < TOL
-    assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < 1e-4
-    assert maxnorm_rel(en_all.cpu(), ro["out::energies_all"]) < 1e-4
-    assert maxnorm_rel(en.cpu(), ro["out::energies"]) < 1e-4
+    check_rel("preds[:T]", preds[:T].cpu(), ro["out::loc_preds"][:T], TOL)
+    check_rel("preds", preds.cpu(), ro["out::loc_preds"], 1e-4)
+    check_rel("en_all", en_all.cpu(), ro["out::energies_all"], 1e-4)
+    check_rel("en", en.cpu(), ro["out::energies"], 1e-4)
 
 
 def test_segno_multi_input_rollout_matches_reference_golden():
@@ -454,6 +476,6 @@ def test_segno_multi_input_rollout_matches_reference_golden():
                                           _dev(fx["in::edge_attr"]), 2, num_steps=[T, T // 2],
                                           charges=_dev(ro["raw::charges"]), energy_dataset="charged",
                                           in_steps=_dev(fx["in::in_steps"]))
-    assert maxnorm_rel(preds[0].cpu(), ro["out::loc_preds"][0]) < TOL
-    assert maxnorm_rel(preds.cpu(), ro["out::loc_preds"]) < 1e-4
-    assert maxnorm_rel(en.cpu(), ro["out::energies"]) < 1e-4
+    check_rel("preds[0]", preds[0].cpu(), ro["out::loc_preds"][0], TOL)
+    check_rel("preds", preds.cpu(), ro["out::loc_preds"], 1e-4)
+    check_rel("en", en.cpu(), ro["out::energies"], 1e-4)

@@ -12,7 +12,7 @@ import torch
 
 import no_node_comparison_amd as pkg
 from oracle import harness as oh
-from tests.conftest import load_golden, maxnorm_rel, params_of
+from tests.conftest import check_rel, load_golden, maxnorm_rel, params_of
 from tests.test_gpu_parity import DEV, TOL, _dev, _egno, _segno
 
 pytestmark = pytest.mark.gpu
@@ -94,10 +94,10 @@ def test_egno_rollout_restart_frame_matches_oracle():
     ref, ren, ren_all = oh.egno_rollout(p, fx["in::h"], fx["in::x"], row, col, fx["in::v"], fx["raw::edge_attr_o"],
                                         fx["in::edge_attr"], fx["in::loc_mean"], N, 2, B, fx["raw::charges"], T=T,
                                         t_out=t_full, t_in=t_in)
-    assert maxnorm_rel(preds[:T].cpu(), ref[:T]) < TOL
+    check_rel("preds[:T]", preds[:T].cpu(), ref[:T], TOL)
     assert maxnorm_rel(preds.cpu(), ref) < 1e-4     # segment 2 starts from a chaotic random-init state
-    assert maxnorm_rel(en_all[:T].cpu(), ren_all[:T]) < 1e-5
-    assert maxnorm_rel(en.cpu(), ren) < 1e-4
+    check_rel("en_all[:T]", en_all[:T].cpu(), ren_all[:T], 1e-5)
+    check_rel("en", en.cpu(), ren, 1e-4)
     assert en.shape == (2, B, 1) and en_all.shape == (2 * T, B, 1)
 
 
@@ -116,9 +116,9 @@ def test_segno_gravity_vardt_rollout_matches_oracle():
     row, col = oh.full_edges(B, N)
     ref, ren = oh.segno_rollout(p, fx["in::his"], fx["in::x"], row, col, fx["in::v"], fx["in::edge_attr"], 3, steps,
                                 mass, B, dataset="gravity")
-    assert maxnorm_rel(preds[0].cpu(), ref[0]) < TOL
-    assert maxnorm_rel(preds.cpu(), ref) < 1e-4
-    assert maxnorm_rel(en.cpu(), ren) < 1e-4
+    check_rel("preds[0]", preds[0].cpu(), ref[0], TOL)
+    check_rel("preds", preds.cpu(), ref, 1e-4)
+    check_rel("en", en.cpu(), ren, 1e-4)
 
 
 def test_rollout_rejects_mismatched_features():

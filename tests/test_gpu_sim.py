@@ -11,7 +11,7 @@ import pytest
 import no_node_comparison_amd as pkg
 from oracle import harness as oh
 from oracle import sim as osim
-from tests.conftest import load_golden, maxnorm_rel
+from tests.conftest import check_rel, load_golden, maxnorm_rel
 from tests.test_oracle_sim import charged_initial_states, gravity_initial_state
 
 pytestmark = pytest.mark.gpu
@@ -26,8 +26,8 @@ def test_charged_sim_reproduces_reference_dataset(name):
     sim = pkg.sim.ChargedParticlesSim(noise_var=0.0, n_balls=n, vel_norm=0.5)
     loc, vel, edges, q = sim.sample_trajectories(sims, T=T, sample_freq=freq)
     assert np.array_equal(q, g["out::charges"]) and np.array_equal(edges, g["out::edges"])
-    assert maxnorm_rel(loc, g["out::loc"]) < SIMTOL
-    assert maxnorm_rel(vel, g["out::vel"]) < SIMTOL
+    check_rel("loc", loc, g["out::loc"], SIMTOL)
+    check_rel("vel", vel, g["out::vel"], SIMTOL)
 
 
 def test_gravity_sim_reproduces_reference_dataset():
@@ -38,7 +38,7 @@ def test_gravity_sim_reproduces_reference_dataset():
     pos, vel, force, mass = sim.sample_trajectory_batch(T=T, sample_freq=freq, batch_size=B)
     assert np.array_equal(mass, g["out::mass"])
     for got, key in ((pos, "out::loc"), (vel, "out::vel"), (force, "out::force")):
-        assert maxnorm_rel(got, g[key]) < SIMTOL
+        check_rel("got", got, g[key], SIMTOL)
 
 
 @pytest.mark.parametrize("n,sims,T,freq", [(2, 2, 500, 50), (64, 2, 400, 100), (200, 1, 300, 100)])
@@ -48,8 +48,8 @@ def test_charged_sim_matches_oracle(n, sims, T, freq):
     loc, vel, _, _ = sim.sample_trajectories(sims, T=T, sample_freq=freq)
     for s, (q, l0, v0) in enumerate(charged_initial_states(n, n, sims, T, freq)):
         L, V = osim.charged_trajectory(l0, v0, q, T, freq)
-        assert maxnorm_rel(loc[s], L) < SIMTOL
-        assert maxnorm_rel(vel[s], V) < SIMTOL
+        check_rel("loc[s]", loc[s], L, SIMTOL)
+        check_rel("vel[s]", vel[s], V, SIMTOL)
 
 
 @pytest.mark.parametrize("n,B,T,freq", [(1, 2, 200, 100), (100, 2, 300, 100), (257, 1, 200, 100)])
@@ -60,7 +60,7 @@ def test_gravity_sim_matches_oracle(n, B, T, freq):
     p0, v0, m = gravity_initial_state(1000 + n, n, B, T, freq)
     P, V, F = osim.gravity_trajectory(p0, v0, m, T, freq)
     for got, want in ((pos, P), (vel, V), (force, F)):
-        assert maxnorm_rel(got, want) < SIMTOL
+        check_rel("got", got, want, SIMTOL)
 
 
 def test_gravity_long_horizon_conserves_energy():
