@@ -37,6 +37,7 @@ def _inputs(B, lo, hi):
 
 
 def _step_grads(B, lo, hi, allreduce):
+    """(gradients after the optional all-reduce, this rank's local gradients before it)."""
     from no_node_comparison_amd.sharding import FlatGrads
     m = _egno(T=T, seed=3).train()
     fg = FlatGrads(m.parameters())
@@ -48,10 +49,11 @@ def _step_grads(B, lo, hi, allreduce):
     # p.grad to None (dropping the FlatGrads views); allreduce_() must gather them back
     torch.optim.Adam(m.parameters(), lr=1e-4).zero_grad()
     loss.backward()
+    local = {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
     if allreduce:
         fg.allreduce_()
     torch.cuda.synchronize()
-    return {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}
+    return {k: p.grad.detach().cpu().numpy().copy() for k, p in m.named_parameters()}, local
 
 
 def _worker(rank, world, port, out, B):
@@ -59,28 +61,39 @@ def _worker(rank, world, port, out, B):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         per = B // world
-        g = _step_grads(B, rank * per, (rank + 1) * per, allreduce=True)
-        if rank == 0:
-            np.savez(out, **g)
+        g, local = _step_grads(B, rank * per, (rank + 1) * per, allreduce=True)
+        np.savez(f"{out}.{rank}", **{"dp::" + k: v for k, v in g.items()}, **{"local::" + k: v for k, v in local.items()})
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("B", [8, 512])
 def test_dp_step_on_hip_kernels_equals_whole_batch(tmp_path, B):
-    """B=512: two ranks of 256 against the whole C4 shard."""
+    """B=512: two ranks of 256 against the whole C4 shard.
+
+    Checks, per parameter tensor:
+      - the exchange itself: every rank holds exactly (g_0 + g_1) / 2 of the ranks' local gradients;
+      - the result against the single-process whole-batch gradients, to DPTOL scaled by the
+        conditioning of the split, max(|g_r|) / max(|g_whole|): a gradient whose shard terms largely
+        cancel (the TimeConv weights at B=512) carries each shard's fp32 error relative to the larger
+        shard magnitude, which no summation order removes."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    out = str(tmp_path / "dp_grads.npz")
+    out = str(tmp_path / "dp_grads")
     mp.start_processes(_worker, args=(2, port, out, B), nprocs=2, join=True, start_method="spawn")
-    dp = np.load(out)
-    whole = _step_grads(B, 0, B, allreduce=False)
+    r0, r1 = np.load(out + ".0.npz"), np.load(out + ".1.npz")
+    whole, _ = _step_grads(B, 0, B, allreduce=False)
     nonzero = 0
     for k, ref in whole.items():
+        dp = r0["dp::" + k]
+        assert np.array_equal(dp, r1["dp::" + k]), k
+        mean = (r0["local::" + k].astype(np.float64) + r1["local::" + k]) / 2
+        assert np.abs(dp - mean).max() <= 1e-6 * max(np.abs(mean).max(), 1e-30), k
         if np.abs(ref).max() == 0:   # the last layer's h update does not reach the position loss
-            assert np.abs(dp[k]).max() == 0, k
+            assert np.abs(dp).max() == 0, k
             continue
         nonzero += 1
-        check_rel(f"dp B={B} grad {k}", dp[k], ref, DPTOL)
+        cond = max(np.abs(r0["local::" + k]).max(), np.abs(r1["local::" + k]).max()) / np.abs(ref).max()
+        check_rel(f"dp B={B} grad {k} (split cond {cond:.1f})", dp, ref, DPTOL * max(1.0, cond))
     assert nonzero > 50
