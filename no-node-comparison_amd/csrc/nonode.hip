@@ -1124,6 +1124,11 @@ struct TconvArgs {
   // repeat_elements_to_exact_shape does); 0: x, v, h_in, loc_mean are [BN] rows replicated over T
   int frames;
   int xcd;   // 1: workgroup k runs tile (k % 8) * ceil(tiles / 8) + k / 8 (XCD-aware order)
+  // training forward only (else null): the LeakyReLU decision of every h element, y > 0, as the
+  // wave ballots of step 3: mask[((t * ntiles + tile) * 4 + wave) * 4 + q] bit l = element
+  // (column 16 tile + 4 wave + (l >> 4), channel 4 (l & 15) + q) of frame t. The backward uses these
+  // decisions instead of recomputing y (a recompute near y = 0 can take the other branch).
+  unsigned long long* mask_out;
 };
 
 // Packed mixing weights of one TimeConv (layer_no.py:80-126), as W^T fragments (f32 MFMA A operand)
@@ -1347,25 +1352,33 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   __syncthreads();
   // ---- step 3: y[t] (channels chs..chs+3 of column ecol), LeakyReLU(0.01), residual ----
-  if (svalid) {
-    Yr[0] = *reinterpret_cast<const f4*>(&sX[0][ecol][chs]);
+  // (lanes of columns past BN compute on the clamped column sc and store nothing)
+  Yr[0] = *reinterpret_cast<const f4*>(&sX[0][ecol][chs]);
 #pragma unroll
-    for (int m = 1; m < MM; ++m) {
-      if (m < M) {
-        Yr[m] = *reinterpret_cast<const f4*>(&sX[2 * m - 1][ecol][chs]);
-        Yi[m] = *reinterpret_cast<const f4*>(&sX[2 * m][ecol][chs]);
-      }
+  for (int m = 1; m < MM; ++m) {
+    if (m < M) {
+      Yr[m] = *reinterpret_cast<const f4*>(&sX[2 * m - 1][ecol][chs]);
+      Yi[m] = *reinterpret_cast<const f4*>(&sX[2 * m][ecol][chs]);
     }
+  }
 #pragma unroll
-    for (int t = 0; t < TB; ++t) {
-      if (t < T) {
-        f4 y = Yr[0];
+  for (int t = 0; t < TB; ++t) {
+    if (t < T) {
+      f4 y = Yr[0];
 #pragma unroll
-        for (int m = 1; m < MM; ++m)
-          if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
-        f4 o = hvs[t];
+      for (int m = 1; m < MM; ++m)
+        if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
+      f4 o = hvs[t];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
+      for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
+      if (p.mask_out) {   // wave-uniform (training forward only)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const unsigned long long bits = __ballot(y[q] > 0.f);
+          if (lane == q) p.mask_out[(((size_t)t * ntiles + tile) * 4 + wave) * 4 + q] = bits;
+        }
+      }
+      if (svalid) {
 #if NONODE_TC_NT & 2
         __builtin_nontemporal_store(o, reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs));
 #else

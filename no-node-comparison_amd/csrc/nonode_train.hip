@@ -908,7 +908,7 @@ __global__ __launch_bounds__(256) void node_post_kernel(int n, const float* ghp,
 // ---- TimeConv reverse (layer_no.py:80-126; oracle/egno_grad.py spectral_bwd) -------------------
 // Persistent: each 4-wave workgroup walks 16-column tiles (columns c = (b, n)). Per tile:
 //   1. DFT of the input h (wave w: input channels 16w..16w+15) -> sX (the forward's layout);
-//   2. forward mixing recompute on MFMA -> Yr, Yi (output channels 16w..);
+//   2. (no forward recompute: the LeakyReLU decisions come from the forward, TrainState::mask);
 //   3. gy[t] = gout[t] * leaky'(y[t]);  gYr_m = (c_m/T) sum_t cos gy,  gYi_m = -(c_m/T) sum_t sin gy
 //      -> sG (zero for columns past BN);
 //   4. backward mixing on MFMA: gXr = Wr gYr + Wi gYi, gXi = -Wi gYr + Wr gYi (wave w: input
@@ -939,6 +939,7 @@ struct TconvBwdArgs {
   const float* wb;     // backward fragments (tconv_pack_bwd_kernel layout)
   float* gh;           // gradient of the input
   float* wpart;        // [grid][M][2][64][64]
+  const unsigned long long* mask;   // the forward's LeakyReLU decisions (TconvArgs::mask_out layout)
 };
 
 template <int MM>
@@ -992,7 +993,6 @@ __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
       }
     }
     __syncthreads();
-    // ---- 2: forward mixing recompute (output tile mo = wave) ----
     auto mix = [&](f4& acc, const float* frags, int mat, const float (*src)[ROWP]) {
       f4 in[4];
       load_ecl(in, &src[e][0], g);
@@ -1004,19 +1004,11 @@ __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
         for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
       }
     };
-    f4 Yr[MM], Yi[MM];
-    Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
-    mix(Yr[0], p.wp, 0, sX[0]);
-#pragma unroll
-    for (int m = 1; m < MM; ++m) {
-      const int mat = 1 + 3 * (m - 1);
-      Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
-      Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
-      mix(Yr[m], p.wp, mat + 0, sX[2 * m - 1]);
-      mix(Yr[m], p.wp, mat + 1, sX[2 * m]);
-      mix(Yi[m], p.wp, mat + 1, sX[2 * m - 1]);
-      mix(Yi[m], p.wp, mat + 2, sX[2 * m]);
-    }
+    // the forward's LeakyReLU decisions for this lane's element (column e, channels ch..ch+3): word
+    // ((t * ntiles + tile) * 4 + e / 4) * 4 + q, bit ((e & 3) << 4) | (ch >> 2)
+    const unsigned long long* mrow = p.mask + ((size_t)tile * 4 + (e >> 2)) * 4;
+    const int mbit = ((e & 3) << 4) | (ch >> 2);
+    const size_t mstride = (size_t)p.ntiles * 16;
     // ---- 3: gy and its spectral coefficients ----
     {
       f4 gR[MM], gI[MM];
@@ -1025,12 +1017,9 @@ __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
 #pragma unroll
       for (int t = 0; t < TMAX; ++t) {
         if (t < T) {
-          f4 y = Yr[0];
-#pragma unroll
-          for (int m = 1; m < MM; ++m) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
           f4 gy = hval(p.gout, t);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) gy[q] *= (y[q] > 0.f ? 1.f : 0.01f);
+          for (int q = 0; q < 4; ++q) gy[q] *= ((mrow[t * mstride + q] >> mbit) & 1) ? 1.f : 0.01f;
 #pragma unroll
           for (int m = 0; m < MM; ++m) {
             gR[m] += gy * sCos[m * TMAX + t];
@@ -1397,6 +1386,7 @@ struct Gemm {
 
 // ---- state layout of the training forward ---------------------------------------------------------
 struct TrainState {
+  unsigned long long* mask;   // L x T x ntiles x 16: TimeConv LeakyReLU decisions (TconvArgs::mask_out)
   float *hs, *xs, *vs;        // (L+1) x n x {64, 3, 3}: inputs of each layer's TimeConv (hs[0] = h0)
   float *he, *xe, *ve;        // L x n x {64, 3, 3}: TimeConv outputs = EGNN inputs
   float *Ms, *Fs;             // L x n x {64, 4}: message / force sums of each EGNN layer
@@ -1408,11 +1398,13 @@ TrainState train_state(void* base, int B, int N, int T, int L, int in_node, int 
   TrainState st;
   float* p = (float*)base;
   auto take = [&](size_t cnt) { float* q = p; if (p) p += cnt; return q; };
+  const size_t mask_words = (size_t)L * T * (((size_t)B * N + 15) / 16) * 16;
+  st.mask = reinterpret_cast<unsigned long long*>(take(2 * mask_words));   // first: 8-byte aligned
   st.hs = take((L + 1) * n * 64); st.xs = take((L + 1) * n * 3); st.vs = take((L + 1) * n * 3);
   st.he = take(L * n * 64); st.xe = take(L * n * 3); st.ve = take(L * n * 3);
   st.Ms = take(L * n * 64); st.Fs = take(L * n * 4);
   st.emb_in = take(n * (in_node + temb));
-  st.floats = (size_t)((L + 1) * n * 70 + L * n * 70 + L * n * 68 + n * (in_node + temb));
+  st.floats = (size_t)(2 * mask_words + (L + 1) * n * 70 + L * n * 70 + L * n * 68 + n * (in_node + temb));
   return st;
 }
 
@@ -1526,6 +1518,7 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
     a.wp = tconv_blobs[l]; a.wx = tconvx_w[l]; a.frames = frames;
     a.h = st.hs + l * n * 64; a.x = st.xs + l * n * 3; a.v = st.vs + l * n * 3; a.lm = loc_mean;
     a.h_out = st.he + l * n * 64; a.x_out = st.xe + l * n * 3; a.v_out = st.ve + l * n * 3;
+    a.mask_out = st.mask + (size_t)l * T * ((BN + 15) / 16) * 16;
     if (int rc = launch_tconv(false, a, s)) return rc;
     if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, a.h_out, a.x_out, a.v_out, edge_fea, blobs[l], 0.f, 1.f,
                                     0, st.hs + (l + 1) * n * 64, st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
@@ -1687,16 +1680,13 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     }
     // ---- TimeConv reverse: h of the layer's TimeConv input ----
     {
-      const int nmat = 1 + 3 * (M - 1);
-      hipLaunchKernelGGL(tconv_pack_kernel, dim3((nmat * 4096 + 255) / 256), dim3(256), 0, s, tconv_w[l], modes, M, T,
-                         w.twf);
-      if (int rc = check_launch("tconv_pack_kernel")) return rc;
       hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, tconv_w[l], modes,
                          M, w.twb);
       if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
       TconvBwdArgs ta;
       ta.BN = BN; ta.T = T; ta.M = M; ta.ntiles = (BN + 15) / 16;
       ta.h = st.hs + l * n * 64; ta.gout = w.ghe; ta.wp = w.twf; ta.wb = w.twb; ta.gh = w.gh[nxt]; ta.wpart = w.tpart;
+      ta.mask = st.mask + (size_t)l * T * ta.ntiles * 16;
       int TG = num_cus();
       TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;
       TG = ta.ntiles < TG ? ta.ntiles : TG;

@@ -51,7 +51,7 @@ def check_rel(name, got, ref, bar):
         ref = ref.detach().cpu().numpy()
     err = maxnorm_rel(got, ref)
     test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
-    _PARITY.append({"test": test, "quantity": name, "maxnorm_rel": err, "bar": bar})
+    _PARITY.append({"test": test, "quantity": name, "maxnorm_rel": float(err), "bar": float(bar)})
     assert err < bar, (name, err, bar)
     return err
 
