@@ -32,17 +32,12 @@ typedef float f8 __attribute__((ext_vector_type(8)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
-// Pair loop with unit B's VALU stages placed beside unit A's MFMA blocks: 1 = SEGNO only (there
-// it fits the register file; for EGNO it spills and slows the guard path), 2 = both
-#ifndef NONODE_STAGGER
-#define NONODE_STAGGER 1
-#endif
+// Pair loop with unit B's VALU stages placed beside unit A's MFMA blocks: SEGNO only (there it fits
+// the register file; for EGNO it spills and slows the guard path)
+template <int VARIANT> constexpr bool kStagger = VARIANT == 1;
 // tconv_kernel h stream cache policy: bit 0 = nontemporal loads, bit 1 = nontemporal stores
 #ifndef NONODE_TC_NT
 #define NONODE_TC_NT 0
-#endif
-#ifndef NONODE_REG_FRAGS
-#define NONODE_REG_FRAGS 1
 #endif
 constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
 constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
@@ -387,19 +382,6 @@ __device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
       a[mt][q + 1] = y.y;
     }
 }
-#ifndef NONODE_ABLATE
-#define NONODE_ABLATE 0   // 1: compile the phase-B internal ablation bits (8/16/32) into the kernel
-#endif
-__device__ __forceinline__ void silu_ecl_dbg(f4 (&a)[4], int debug) {
-  if (NONODE_ABLATE && (debug & 16)) {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[mt][q] = fminf(fmaxf(a[mt][q], -1.f), 1.f);
-  } else {
-    silu_ecl(a);
-  }
-}
 // sum over the 4 lane groups (lanes e, e+16, e+32, e+48): the full 64-channel dot product
 // (gfx950 permlane swaps: v + v^32 and then v + v^16 without an LDS round trip)
 __device__ __forceinline__ float group_sum(float v) {
@@ -554,9 +536,10 @@ struct LayerArgs {
   // training forward only (else null): per-receiver message sums (true scale) [n][64] and force
   // sums [n][4] (f summed over the N-1 senders, before the mean and clamp)
   float* m_out; float* f_out;
-  int n_total, n_graphs, N, ne, ef_mod, ct, s_max, recurrent;
-  int debug;   // profiling ablation (NONODE_DEBUG): 1 skip edges, 2 skip node update, 4 skip projections,
-               // 8 no edge-feature loads, 16 SiLU -> clamp, 32 skip the per-edge fp16 MFMAs
+  int n_total, n_graphs, N, ne, ef_mod, recurrent;
+  // chunking: a unit is cg whole graphs (cpg = 1) or, for large N, one graph cut into cpg chunks of
+  // ct receiver tiles; workgroups own whole units (n_units, the last may be short)
+  int cg, cpg, n_units, ct, s_rows;
   float inv_deg, dt, cw;
   // XCD-aware chunk order (EGNO forward): workgroup k runs graph chunk chunk_of[k], chosen so that
   // k % 8 (its XCD) owns the same 1/8 of the columns as the TimeConv tiles on that XCD
@@ -564,34 +547,42 @@ struct LayerArgs {
   unsigned short chunk_of[256];
 };
 
-size_t layer_lds_floats(int ct, int N, int* s_max_out) {
-  const int s_max = ((16 * ct - 1) / N + 2) * N;
-  if (s_max_out) *s_max_out = s_max;
-  return 8192 + EDGE_STAGE_FLOATS + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * (ROWP + 4) +
-         (size_t)ct * 16 * 4;
+// LDS of one chunk: ct receiver tiles (P, two message-sum slots, two force-sum slots) and s_rows senders
+size_t layer_lds_floats(int ct, int s_rows) {
+  return 8192 + EDGE_STAGE_FLOATS + (size_t)ct * 16 * ROWP * 3 + (size_t)s_rows * (ROWP + 4) +
+         (size_t)ct * 16 * 4 * 2;
 }
 
 // One workgroup owns a contiguous range of whole graphs (so every sender of its receivers is its
 // own: substeps need no grid-wide sync) and walks it as 16-receiver tiles, in chunks of `ct` tiles.
 // Per chunk:  A) P = W1[h_i] h + b1 for receivers, Q = W1[h_j] h for every sender of the touched
 //                graphs (LDS tables), sender positions;
-//             B) (tile, k) units split evenly over the waves: receiver r (lane column) meets
-//                sender (n + k) mod N of its graph; edge MLP + coord MLP on MFMA; partial
-//                message / force sums flushed into LDS accumulators;
-//             C) node update per tile: x (and v) update, node MLP, stores.
-// KF: feature k-steps (1 + ne scalar edge inputs, 4 per step); NW: waves per workgroup.
-template <int VARIANT, int KF, int NW, bool PAIR>
-__global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
+//             B) units (tile, k): receiver r (lane column) meets sender (n + k) mod N of its graph;
+//                edge MLP + coord MLP on MFMA. The chunk's units are split evenly over the waves
+//                (contiguous ranges); wave w flushes its partial message / force sums of a tile
+//                into slot w & 1. A tile spans at most 4 consecutive waves, so each slot of a
+//                receiver gets at most two contributions and the LDS float atomics commute exactly;
+//             C) node update per tile (sums = slot 0 + slot 1): x (and v) update, node MLP, stores.
+// A chunk is a fixed number (cg) of whole graphs, or a fixed slice of one graph's receivers when a
+// graph does not fit, so its tile layout and work split depend only on (cg, ct, N): the layer's
+// outputs are bitwise run-to-run deterministic and, for batch shards that are multiples of cg
+// samples with the same chunking, identical to the whole batch's.
+// KF: feature k-steps (1 + ne scalar edge inputs, 4 per step). Four waves, one per SIMD (512-register
+// budget), two units per iteration.
+template <int VARIANT, int KF>
+__global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
+  constexpr int NW = 4;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
   float* sW = smem;                              // W2 | Wc1 fp16 hi/lo fragments (8192 floats)
   float* sV = sW + 8192;                         // feat k-steps (512) | b2 | bc1 | wc2 (vp order)
   float* sP = sV + EDGE_STAGE_FLOATS;            // [ct*16][ROWP]
-  float* sQ = sP + p.ct * 16 * ROWP;             // [s_max][ROWP]
-  float* sX = sQ + p.s_max * ROWP;               // [s_max][4]
-  float* sM = sX + p.s_max * 4;                  // [ct*16][ROWP] message sums
-  float* sF = sM + p.ct * 16 * ROWP;             // [ct*16][4]   force sums
+  float* sQ = sP + p.ct * 16 * ROWP;             // [s_rows][ROWP]
+  float* sX = sQ + p.s_rows * ROWP;              // [s_rows][4]
+  float* sM = sX + p.s_rows * 4;                 // [2][ct*16][ROWP] message sums (slots 0 | 1)
+  float* sF = sM + 2 * p.ct * 16 * ROWP;         // [2][ct*16][4]   force sums (slots 0 | 1)
+  const int slotM = p.ct * 16 * ROWP, slotF = p.ct * 16 * 4;
 
   for (int i = tid; i < 2048; i += NW * 64) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_H16)[i];
   if (tid < EDGE_STAGE_FLOATS / 4)
@@ -605,12 +596,54 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
 
   const int G = gridDim.x;
   const int cb = p.use_perm ? (int)p.chunk_of[blockIdx.x] : (int)blockIdx.x;
-  const int nb = (int)(((long long)cb * p.n_graphs) / G) * N;         // first receiver
-  const int nend = (int)(((long long)(cb + 1) * p.n_graphs) / G) * N;  // one past the last
+  const int ch0 = (int)(((long long)cb * p.n_units) / G) * p.cpg;        // this workgroup's chunks
+  const int ch1 = (int)(((long long)(cb + 1) * p.n_units) / G) * p.cpg;
   __syncthreads();
-
-  const int ntw = (nend - nb + 15) >> 4;
-  const int nch = (ntw + p.ct - 1) / p.ct;
+  // message / force sums start at zero; every node-update job zeroes the rows it consumed, so the
+  // next chunk's edge phase finds them zero
+  for (int i = tid; i < 2 * p.ct * 16 * ROWP; i += NW * 64) sM[i] = 0.f;
+  for (int i = tid; i < 2 * p.ct * 16 * 4; i += NW * 64) sF[i] = 0.f;
+  // rows of chunk ci: receivers [rbase, nend), senders [s0, s0 + S)
+  auto chunk_at = [&](int ci, int& rbase, int& nend, int& s0, int& S) __attribute__((always_inline)) {
+    if (p.cpg == 1) {   // cg whole graphs: the chunk's rows are its receivers and senders alike
+      const int g_lo = ci * p.cg, g_hi = min(g_lo + p.cg, p.n_graphs);
+      rbase = g_lo * N; nend = g_hi * N; s0 = rbase; S = nend - rbase;
+    } else {            // receiver slice `part` of graph gi; senders: the whole graph
+      const int gi = ci / p.cpg, part = ci - gi * p.cpg;
+      s0 = gi * N; S = N;
+      rbase = s0 + part * 16 * p.ct; nend = min(rbase + 16 * p.ct, s0 + N);
+    }
+  };
+  // phase A job of a chunk: job < ctc: receiver projections P = W1[h_i] h + b1 of tile `job`;
+  // else sender projections Q = W1[h_j] h of sender tile job - ctc (LDS tables), and the sender
+  // positions (all threads)
+  auto proj_job = [&](const float* __restrict__ hI, const float* blob, int rbase, int nend, int s0, int S,
+                      int job) __attribute__((always_inline)) {
+    const int ctc = (nend - rbase + 15) >> 4;
+    const bool isP = job < ctc;                       // wave-uniform
+    const int local = (isP ? job : job - ctc) * 16 + e;
+    int node = isP ? rbase + local : s0 + local;
+    const bool valid = isP ? (node < nend) : (local < S);
+    node = valid ? node : (isP ? nend - 1 : s0);
+    f4 hin[4];
+    load_ecl(hin, hI + (size_t)node * HID, g);
+    f4 acc[4];
+    if (isP) {
+      load_vp(acc, blob + OFF_VEC + V_B1 * 64, g);
+    } else {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    mm64(acc, reinterpret_cast<const h8*>(blob + OFF_H16N + (isP ? H_WA : H_WB) * 4096),
+         blob + (isP ? OFF_WA : OFF_WB), hin, lane);
+    if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
+  };
+  auto load_sx = [&](const float* __restrict__ xI, int s0, int S) __attribute__((always_inline)) {
+    for (int i = tid; i < S * 3; i += NW * 64) {
+      const int s = i / 3, d = i - 3 * s;
+      sX[s * 4 + d] = xI[(size_t)(s0 + s) * 3 + d];
+    }
+  };
   STAMP_DECL
   #pragma unroll 1
   for (int step = 0; step < p.steps; ++step) {
@@ -620,83 +653,42 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
   float* hO = step == p.steps - 1 ? p.h_out : p.pp_h[step & 1];
   float* xO = step == p.steps - 1 ? p.x_out : p.pp_x[step & 1];
   float* vO = step == p.steps - 1 ? p.v_out : p.pp_v[step & 1];
+  {   // ---------------- phase A of the step's first chunk ----------------
+    int rbase, nend, s0, S;
+    chunk_at(ch0, rbase, nend, s0, S);
+    load_sx(xI, s0, S);
+    const int J = ((nend - rbase + 15) >> 4) + ((S + 15) >> 4);
+    #pragma unroll 1
+    for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job);
+  }
+  STAMP(6);
+  __syncthreads();
+  STAMP(7);
   #pragma unroll 1
-  for (int ci = 0; ci < nch; ++ci) {
-    const int c0 = (ci * ntw) / nch;
-    const int ctc = ((ci + 1) * ntw) / nch - c0;
+  for (int ci = ch0; ci < ch1; ++ci) {
     // keep per-chunk loads of weights/vectors inside the loop (LICM would pin them in VGPRs
     // across all phases)
     int boff = 0;
     asm volatile("" : "+s"(boff));
     const float* blob = p.blob + boff;
-    const int rbase = nb + c0 * 16;
-    const int r_last = min(rbase + ctc * 16, nend) - 1;
-    const int g_lo = rbase / N, g_hi = r_last / N;
-    const int s0 = g_lo * N;
-    const int S = (g_hi - g_lo + 1) * N;
-    const int nsT = (S + 15) >> 4;
-
-    // ---------------- phase A: node projections into LDS ----------------
-    for (int i = tid; i < ctc * 16 * ROWP; i += NW * 64) sM[i] = 0.f;
-    for (int i = tid; i < ctc * 16 * 4; i += NW * 64) sF[i] = 0.f;
-    if (p.debug & 4) {   // ablation: projections skipped, tables zeroed so later phases stay finite
-      for (int i = tid; i < ctc * 16 * ROWP; i += NW * 64) sP[i] = 0.f;
-      for (int i = tid; i < S * ROWP; i += NW * 64) sQ[i] = 0.f;
-    }
-    for (int i = tid; i < S * 3; i += NW * 64) {
-      const int s = i / 3, d = i - 3 * s;
-      sX[s * 4 + d] = xI[(size_t)(s0 + s) * 3 + d];
-    }
-    #pragma unroll 1
-    for (int job = wave; job < ((p.debug & 4) ? 0 : ctc + nsT); job += NW) {
-      const bool isP = job < ctc;                       // wave-uniform
-      const int local = (isP ? job : job - ctc) * 16 + e;
-      int node = isP ? rbase + local : s0 + local;
-      const bool valid = isP ? (node < nend) : (local < S);
-      node = valid ? node : (isP ? nend - 1 : s0);
-      f4 hin[4];
-      load_ecl(hin, hI + (size_t)node * HID, g);
-      f4 acc[4];
-      if (isP) {
-        load_vp(acc, blob + OFF_VEC + V_B1 * 64, g);
-      } else {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      }
-      mm64(acc, reinterpret_cast<const h8*>(blob + OFF_H16N + (isP ? H_WA : H_WB) * 4096),
-           blob + (isP ? OFF_WA : OFF_WB), hin, lane);
-      if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
-    }
-    STAMP(6);
-    __syncthreads();
-    STAMP(7);
+    int rbase, nend, s0, S;
+    chunk_at(ci, rbase, nend, s0, S);
+    const int ctc = (nend - rbase + 15) >> 4;
 
     // ---------------- phase B: edges ----------------
     // Units (tile, k) are split evenly over the waves; a wave walks its range tile segment by
     // tile segment and processes the units of a segment two at a time, so that the VALU work of
-    // one unit (SiLU, gathers) can issue under the MFMA chains of the other.
+    // one unit (SiLU, gathers) can issue under the MFMA chains of the other. W2 / Wc1 fragments
+    // are read from LDS (each read feeds two units' MFMAs); b2 / bc1 / wc2 stay in registers for
+    // the edge phase.
     {
-      const int U = (p.debug & 1) ? 0 : ctc * Nm1;
-      const int u0 = (wave * U) / NW, u1 = ((wave + 1) * U) / NW;
-      int u = u0;
-      // 8-wave single-unit loop: W2 / Wc1 fp16 fragments stay in registers for the edge phase.
-      // PAIR reads them from LDS (each read feeds two units' MFMAs; the registers go to the
-      // second unit instead)
-      constexpr bool REGF = NONODE_REG_FRAGS && !PAIR;
-      H16Frags fw2, fwc1;
-      if (REGF) {
-        load_h16frags(fw2, reinterpret_cast<const h8*>(sW), lane);
-        load_h16frags(fwc1, reinterpret_cast<const h8*>(sW + 4096), lane);
-      }
-      // PAIR (one wave per SIMD): b2 / bc1 / wc2 also stay in registers for the edge phase
-      // (8-wave PAIR: two waves share a SIMD's 512 registers, so these stay in LDS)
-      constexpr bool RV = PAIR && NW <= 4;
+      const int U = ctc * Nm1;
+      const int u1 = ((wave + 1) * U) / NW;
+      int u = (wave * U) / NW;
       f4 rB2[4], rBC1[4], rWC2[4];
-      if (RV) {
-        load_vp(rB2, vB2_, g);
-        load_vp(rBC1, vBC1_, g);
-        load_vp(rWC2, vWC2_, g);
-      }
+      load_vp(rB2, vB2_, g);
+      load_vp(rBC1, vBC1_, g);
+      load_vp(rWC2, vWC2_, g);
       #pragma unroll 1
       while (u < u1) {
         const int tau = u / Nm1;
@@ -714,9 +706,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         const size_t ebase = ((size_t)(gr % p.ef_mod) * N + n) * Nm1;
         int voff = 0;
         asm volatile("" : "+v"(voff));   // keeps the vector reads per segment (not hoisted), LDS space kept
-        const float* vB2 = vB2_ + voff;
-        const float* vBC1 = vBC1_ + voff;
-        const float* vWC2 = vWC2_ + voff;
         const float* vFEAT = vFEAT_ + voff;
         const float* Prow = sP + rl * ROWP;            // re-read per unit (saves 16 live VGPRs)
         const float xr0 = sX[(sb + n) * 4 + 0], xr1 = sX[(sb + n) * 4 + 1], xr2 = sX[(sb + n) * 4 + 2];
@@ -740,7 +729,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           const int kne = k * p.ne;
 #pragma unroll
           for (int kf = 0; kf < KF; ++kf)
-            ev[kf] = (NONODE_ABLATE && (p.debug & 8)) ? 0.5f : ef_seg[ef_lane[kf] + kne - sub];
+            ev[kf] = ef_seg[ef_lane[kf] + kne - sub];
         };
         // pre-activation of edge (r, k): P_r + Q_s + W1[:, scalars] [|r|^2, e_rs] on MFMA
         auto head = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
@@ -766,8 +755,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           }
         };
         auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
-          silu_ecl_dbg(c1, p.debug);
-          const float c = (RV ? dot_r(c1, rWC2) : dot_vp(c1, vWC2, g)) + bc2;
+          silu_ecl(c1);
+          const float c = dot_r(c1, rWC2) + bc2;
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
           if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
             f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -782,14 +771,14 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         const float* w2f = p.blob + OFF_W2;     // exact fp32 fragments (global) for the guard path
         const float* wc1f = p.blob + OFF_WC1;
         int k = k_lo;
-        if (PAIR) {
+        {
           // Two units (32 edges, same receivers) per iteration. The hot body is ONE basic block:
           // both units always take the fp16x3 path while the largest |activation| is tracked, and
           // only if it exceeded the fp16 range (rare) is the pair recomputed on exact f32 MFMAs
           // before its sums are committed. So the scheduler can put one unit's MFMAs beside the
           // other unit's SiLU work.
           f4 pr[4];
-          if (RV) load_ecl(pr, Prow, g);               // receiver projection, fixed for the segment
+          load_ecl(pr, Prow, g);                       // receiver projection, fixed for the segment
           auto head2 = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
               __attribute__((always_inline)) {
             int j = n + k;
@@ -799,7 +788,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
             const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
             load_ecl(a, sQ + sl * ROWP, g);
-            if (!RV) load_ecl(pr, Prow, g);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
 #pragma unroll
@@ -814,7 +802,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           auto edge_f = [&](f4 (&c1)[4], float r0, float r1, float r2, float& f0, float& f1, float& f2)
               __attribute__((always_inline)) {
             silu_ecl(c1);
-            const float c = (RV ? dot_r(c1, rWC2) : dot_vp(c1, vWC2, g)) + bc2;
+            const float c = dot_r(c1, rWC2) + bc2;
             f0 = r0 * c; f1 = r1 * c; f2 = r2 * c;
             if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
               f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -831,12 +819,10 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             silu_ecl(a);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
-            if (!RV) load_vp(m, vB2, g);
             mfma_dense<4>(m, w2f, a, lane);
             silu_ecl(m);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
-            if (!RV) load_vp(c, vBC1, g);
             mfma_dense<4>(c, wc1f, m, lane);
             edge_f(c, r0, r1, r2, f0, f1, f2);
           };
@@ -858,7 +844,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             float f00, f01, f02, f10, f11, f12;
             f4 pm[4];
             float gmax;
-            if constexpr (NONODE_STAGGER == 2 || (NONODE_STAGGER == 1 && VARIANT == SEGNO)) {
+            if constexpr (kStagger<VARIANT>) {
             // The two units run half a stage apart, so every MFMA block of one unit has the other
             // unit's VALU stage (gathers, SiLU, fp16 split) beside it in program order:
             //   W2(A) | head+SiLU(B) ;  W2(B) | SiLU(m_A) ;  Wc1(A) | SiLU(m_B) ;  Wc1(B) | coord(A)
@@ -874,7 +860,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               load_h16frags(fw2, w2l, lane);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) m0[mt] = rB2[mt];
-              if (!RV) load_vp(m0, vB2, g);
               mfma_h16r(m0, fw2, xh0, xl0);                       // W2(A)
               head2(k + 1, e1, a1, r10, r11, r12);                // | head + SiLU + split (B)
               silu_ecl(a1);
@@ -882,7 +867,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               h16_split(a1, xh1, xl1);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) m1[mt] = rB2[mt];
-              if (!RV) load_vp(m1, vB2, g);
               mfma_h16r(m1, fw2, xh1, xl1);                       // W2(B)
               load_h16frags(fwc1, wc1l, lane);
               silu_ecl(m0);                                       // | SiLU + split (m_A)
@@ -890,7 +874,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               h16_split(m0, xh0, xl0);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) a0[mt] = rBC1[mt];
-              if (!RV) load_vp(a0, vBC1, g);
               mfma_h16r(a0, fwc1, xh0, xl0);                      // Wc1(A)
               silu_ecl(m1);                                       // | SiLU + split (m_B)
               gmax = fmaxf(gmax, amax_ecl(m1));
@@ -900,7 +883,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
                 pm[mt] = m0[mt] + m1[mt];
                 a1[mt] = rBC1[mt];
               }
-              if (!RV) load_vp(a1, vBC1, g);
               mfma_h16r(a1, fwc1, xh1, xl1);                      // Wc1(B)
               edge_f(a0, r00, r01, r02, f00, f01, f02);           // | coord MLP (A)
               STAMP(2);
@@ -915,7 +897,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             gmax = fmaxf(amax_ecl(a0), amax_ecl(a1));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; }
-            if (!RV) { load_vp(m0, vB2, g); load_vp(m1, vB2, g); }
             {
               h8 ah0[2], al0[2], ah1[2], al1[2];
               h16_split(a0, ah0, al0);
@@ -932,7 +913,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               a0[mt] = rBC1[mt];
               a1[mt] = rBC1[mt];
             }
-            if (!RV) { load_vp(a0, vBC1, g); load_vp(a1, vBC1, g); }
             {
               h8 mh0[2], ml0[2], mh1[2], ml1[2];
               h16_split(m0, mh0, ml0);
@@ -972,34 +952,28 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
 #pragma unroll
           for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
           STAMP(0);
-          silu_ecl_dbg(a, p.debug);
-          load_vp(m, vB2, g);
+          silu_ecl(a);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
           if (__builtin_expect(__any(amax_ecl(a) > H16_LIMIT), 0)) {
             mfma_dense<4>(m, w2f, a, lane);
           } else {
             h8 ah[2], al[2];
             h16_split(a, ah, al);
-            if (REGF) {
-              if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(m, fw2, ah, al);    // m = SiLU(W2 a + b2)
-            } else {
-              mfma_h16(m, w2h, ah, al, lane);
-            }
+            mfma_h16(m, w2h, ah, al, lane);   // m = SiLU(W2 a + b2)
           }
           STAMP(1);
-          silu_ecl_dbg(m, p.debug);
+          silu_ecl(m);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
-          load_vp(a, vBC1, g);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) a[mt] = rBC1[mt];
           if (__builtin_expect(__any(amax_ecl(m) > H16_LIMIT), 0)) {
             mfma_dense<4>(a, wc1f, m, lane);
           } else {
             h8 mh[2], ml[2];
             h16_split(m, mh, ml);
-            if (REGF) {
-              if (!(NONODE_ABLATE && (p.debug & 32))) mfma_h16r(a, fwc1, mh, ml);   // SiLU(Wc1 m + bc1)
-            } else {
-              mfma_h16(a, wc1h, mh, ml, lane);
-            }
+            mfma_h16(a, wc1h, mh, ml, lane);  // SiLU(Wc1 m + bc1)
           }
           STAMP(2);
           tail(a, r0, r1, r2);
@@ -1007,15 +981,17 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         }
         // ---- flush the segment's partial sums ----
         if (rvalid) {
-          float* mrow = sM + rl * ROWP + 4 * g;
+          const int slot = wave & 1;
+          float* mrow = sM + slot * slotM + rl * ROWP + 4 * g;
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
             for (int q = 0; q < 4; ++q) atomicAdd(mrow + 16 * mt + q, msum[mt][q]);
           if (g == 0) {
-            atomicAdd(sF + rl * 4 + 0, fs0);
-            atomicAdd(sF + rl * 4 + 1, fs1);
-            atomicAdd(sF + rl * 4 + 2, fs2);
+            float* frow = sF + slot * slotF + rl * 4;
+            atomicAdd(frow + 0, fs0);
+            atomicAdd(frow + 1, fs1);
+            atomicAdd(frow + 2, fs2);
           }
         }
         STAMP(9);
@@ -1025,79 +1001,116 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     __syncthreads();
     STAMP(11);
 
-    // ---------------- phase C: node update ----------------
-    #pragma unroll 1
-    for (int tau = wave; tau < ((p.debug & 2) ? 0 : ctc); tau += NW) {
-      const int rl = 16 * tau + e;
-      const int r = rbase + rl;
-      const bool rvalid = r < nend;
-      const int rc = rvalid ? r : nend - 1;
-      f4 in8[8];
-      f4 hr[4], Mr[4];
-      load_ecl(hr, hI + (size_t)rc * HID, g);
-      load_ecl(Mr, sM + rl * ROWP, g);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
-      const float F0 = sF[rl * 4 + 0], F1 = sF[rl * 4 + 1], F2 = sF[rl * 4 + 2];
-      const float* xp = xI + (size_t)rc * 3;
-      const float* vpn = vI + (size_t)rc * 3;
-      const float x0 = xp[0], x1 = xp[1], x2 = xp[2];
-      const float v0 = vpn[0], v1 = vpn[1], v2 = vpn[2];
-      float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
-      if (VARIANT == EGNO) {
-        // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
-        f4 t[4];
-        load_vp(t, blob + OFF_VEC + V_BV1 * 64, g);
-        mm64(t, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WV1 * 4096), blob + OFF_WV1, hr, lane);
-        silu_ecl(t);
-        const float phi = dot_vp(t, blob + OFF_VEC + V_WV2 * 64, g) + bv2;
-        nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
-        nx1 = x1 + phi * v1 + fminf(fmaxf(F1 * p.inv_deg, -100.f), 100.f);
-        nx2 = x2 + phi * v2 + fminf(fmaxf(F2 * p.inv_deg, -100.f), 100.f);
-      } else {
-        // v <- v + agg/T ; x <- x + v/T   (gcl.py:255-257 with coords_weight, gcl.py:242)
-        nv0 = v0 + (F0 * p.inv_deg * p.cw) * p.dt;
-        nv1 = v1 + (F1 * p.inv_deg * p.cw) * p.dt;
-        nv2 = v2 + (F2 * p.inv_deg * p.cw) * p.dt;
-        nx0 = x0 + nv0 * p.dt;
-        nx1 = x1 + nv1 * p.dt;
-        nx2 = x2 + nv2 * p.dt;
+    // ---------------- phase C (node update of this chunk) + phase A of the next chunk ----------------
+    // One job list: the ctc node-update tiles (cost ~4 projection jobs each), then the next chunk's
+    // projection jobs (the next chunk of the same step only: the next step's projections read this
+    // step's outputs). Jobs go to the least-loaded wave in order (the same greedy on every wave), so
+    // a chunk of 5 tiles no longer leaves 3 waves idle for a tile's node update.
+    {
+      const bool has_next = ci + 1 < ch1;
+      int nrb = 0, nne = 0, ns0 = 0, nS = 0;
+      if (has_next) {
+        chunk_at(ci + 1, nrb, nne, ns0, nS);
+        load_sx(xI, ns0, nS);
       }
-      // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
-      f4 z[4];
-      load_vp(z, blob + OFF_VEC + V_BN1 * 64, g);
-      if (__builtin_expect(__any(fmaxf(amax_ecl(hr), amax_ecl(Mr)) > H16_LIMIT), 0)) {
-        mfma_dense<8>(z, blob + OFF_WN1, in8, lane);
-      } else {
-        h8 xh[2], xl[2];
-        h16_split(hr, xh, xl);
-        mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1A * 4096), xh, xl, lane);
-        h16_split(Mr, xh, xl);
-        mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1B * 4096), xh, xl, lane);
-      }
-      silu_ecl(z);
-      f4 hn[4];
-      load_vp(hn, blob + OFF_VEC + V_BN2 * 64, g);
-      mm64(hn, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN2 * 4096), blob + OFF_WN2, z, lane);
-      if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
-      }
-      if (rvalid && p.m_out) {
-        f4 mt4[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[mt] * NEG_LN2;    // sM holds -log2e * sum m
-        store_ecl(p.m_out + (size_t)r * HID, mt4, g);
-        if (g == 0) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
-      }
-      if (rvalid) {
-        store_ecl(hO + (size_t)r * HID, hn, g);
-        if (g == 0) {
-          float* xo = xO + (size_t)r * 3;
-          xo[0] = nx0; xo[1] = nx1; xo[2] = nx2;
-          if (VARIANT == SEGNO) {
-            float* vo = vO + (size_t)r * 3;
-            vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
+      const int J = ctc + (has_next ? ((nne - nrb + 15) >> 4) + ((nS + 15) >> 4) : 0);
+      constexpr int C_COST = 4;
+      int ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
+      #pragma unroll 1
+      for (int j = 0; j < J; ++j) {
+        const int m01 = min(ld0, ld1), m23 = min(ld2, ld3);
+        const int w = m01 <= m23 ? (ld0 <= ld1 ? 0 : 1) : (ld2 <= ld3 ? 2 : 3);
+        const int c = j < ctc ? C_COST : 1;
+        ld0 += w == 0 ? c : 0; ld1 += w == 1 ? c : 0; ld2 += w == 2 ? c : 0; ld3 += w == 3 ? c : 0;
+        if (w != wave) continue;
+        if (j >= ctc) {
+          proj_job(hI, blob, nrb, nne, ns0, nS, j - ctc);
+          continue;
+        }
+        const int tau = j;
+        const int rl = 16 * tau + e;
+        const int r = rbase + rl;
+        const bool rvalid = r < nend;
+        const int rc = rvalid ? r : nend - 1;
+        f4 in8[8];
+        f4 hr[4], Mr[4], Mb[4];
+        load_ecl(hr, hI + (size_t)rc * HID, g);
+        load_ecl(Mr, sM + rl * ROWP, g);
+        load_ecl(Mb, sM + slotM + rl * ROWP, g);
+  #pragma unroll
+        for (int mt = 0; mt < 4; ++mt) { Mr[mt] += Mb[mt]; in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
+        const float* fa = sF + rl * 4;
+        const float* fb = sF + slotF + rl * 4;
+        const float F0 = fa[0] + fb[0], F1 = fa[1] + fb[1], F2 = fa[2] + fb[2];
+        {   // the rows are consumed: zero both slots for the next chunk's edge phase
+          const f4 z4[4] = {};
+          store_ecl(sM + rl * ROWP, z4, g);
+          store_ecl(sM + slotM + rl * ROWP, z4, g);
+          if (g == 0) {
+            *reinterpret_cast<f4*>(sF + rl * 4) = z4[0];
+            *reinterpret_cast<f4*>(sF + slotF + rl * 4) = z4[0];
+          }
+        }
+        const float* xp = xI + (size_t)rc * 3;
+        const float* vpn = vI + (size_t)rc * 3;
+        const float x0 = xp[0], x1 = xp[1], x2 = xp[2];
+        const float v0 = vpn[0], v1 = vpn[1], v2 = vpn[2];
+        float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
+        if (VARIANT == EGNO) {
+          // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
+          f4 t[4];
+          load_vp(t, blob + OFF_VEC + V_BV1 * 64, g);
+          mm64(t, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WV1 * 4096), blob + OFF_WV1, hr, lane);
+          silu_ecl(t);
+          const float phi = dot_vp(t, blob + OFF_VEC + V_WV2 * 64, g) + bv2;
+          nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
+          nx1 = x1 + phi * v1 + fminf(fmaxf(F1 * p.inv_deg, -100.f), 100.f);
+          nx2 = x2 + phi * v2 + fminf(fmaxf(F2 * p.inv_deg, -100.f), 100.f);
+        } else {
+          // v <- v + agg/T ; x <- x + v/T   (gcl.py:255-257 with coords_weight, gcl.py:242)
+          nv0 = v0 + (F0 * p.inv_deg * p.cw) * p.dt;
+          nv1 = v1 + (F1 * p.inv_deg * p.cw) * p.dt;
+          nv2 = v2 + (F2 * p.inv_deg * p.cw) * p.dt;
+          nx0 = x0 + nv0 * p.dt;
+          nx1 = x1 + nv1 * p.dt;
+          nx2 = x2 + nv2 * p.dt;
+        }
+        // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
+        f4 z[4];
+        load_vp(z, blob + OFF_VEC + V_BN1 * 64, g);
+        if (__builtin_expect(__any(fmaxf(amax_ecl(hr), amax_ecl(Mr)) > H16_LIMIT), 0)) {
+          mfma_dense<8>(z, blob + OFF_WN1, in8, lane);
+        } else {
+          h8 xh[2], xl[2];
+          h16_split(hr, xh, xl);
+          mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1A * 4096), xh, xl, lane);
+          h16_split(Mr, xh, xl);
+          mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1B * 4096), xh, xl, lane);
+        }
+        silu_ecl(z);
+        f4 hn[4];
+        load_vp(hn, blob + OFF_VEC + V_BN2 * 64, g);
+        mm64(hn, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN2 * 4096), blob + OFF_WN2, z, lane);
+        if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
+  #pragma unroll
+          for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
+        }
+        if (rvalid && p.m_out) {
+          f4 mt4[4];
+  #pragma unroll
+          for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[mt] * NEG_LN2;    // sM holds -log2e * sum m
+          store_ecl(p.m_out + (size_t)r * HID, mt4, g);
+          if (g == 0) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
+        }
+        if (rvalid) {
+          store_ecl(hO + (size_t)r * HID, hn, g);
+          if (g == 0) {
+            float* xo = xO + (size_t)r * 3;
+            xo[0] = nx0; xo[1] = nx1; xo[2] = nx2;
+            if (VARIANT == SEGNO) {
+              float* vo = vO + (size_t)r * 3;
+              vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
+            }
           }
         }
       }
@@ -1443,15 +1456,15 @@ bool xcd_on() {
   static const int on = getenv("NONODE_XCD") ? atoi(getenv("NONODE_XCD")) : 1;
   return on != 0;
 }
-template <int VARIANT, int NW, bool PAIR>
+template <int VARIANT>
 void launch_cfg(int kf, int G, size_t lds, hipStream_t stream, const LayerArgs& a) {
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, NW, PAIR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, NW, PAIR>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, NW, PAIR>), dim3(G), dim3(NW * 64), lds, stream, a);
-  else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, NW, PAIR>), dim3(G), dim3(NW * 64), lds, stream, a);
+  if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1>), dim3(G), dim3(256), lds, stream, a);
+  else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2>), dim3(G), dim3(256), lds, stream, a);
 }
 // steps > 1 runs that many substeps in one launch (SEGNO forward_step), ping-ponging through
 // pp = {h0, h1, x0, x1, v0, v1} (each n_graphs*N rows)
@@ -1463,17 +1476,36 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
                  int xcd_cols = 0) {
   const int n_total = n_graphs * N;
   const int cus = num_cus();
-  const int G = n_graphs < cus ? n_graphs : cus;
-  const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
-  int ct = 8 < tiles_per ? 8 : tiles_per;
-  int s_max = 0;
-  while (ct > 1 && layer_lds_floats(ct, N, &s_max) * 4 > 160 * 1024) --ct;
-  const size_t lds = layer_lds_floats(ct, N, &s_max) * 4;
-  if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "N=%d too large for the LDS sender table", N);
+  // graphs per chunk: at most the graphs per CU, at most 8 tiles, within LDS; among those the one
+  // whose rows fill its tiles best (ties: the larger). N = 20: 4 graphs = 80 rows = 5 full tiles.
+  // A graph of more than 8 tiles (or beyond the LDS) is cut into cpg receiver slices of ct tiles.
+  constexpr size_t LDS_MAX = 160 * 1024;
+  const int cap = n_graphs / cus > 1 ? n_graphs / cus : 1;
+  int cg = 0, cpg = 1, ct = 0;
+  double best = -1.0;
+  for (int c = 1; c <= cap; ++c) {
+    const int tiles = (c * N + 15) / 16;
+    if (tiles > 8 || layer_lds_floats(tiles, c * N) * 4 > LDS_MAX) break;
+    const double fill = (double)(c * N) / (16.0 * tiles);
+    if (fill >= best - 1e-12) { best = fill; cg = c; ct = tiles; }
+  }
+  if (cg == 0) {
+    cg = 1;
+    ct = (N + 15) / 16 < 8 ? (N + 15) / 16 : 8;
+    while (ct > 1 && layer_lds_floats(ct, N) * 4 > LDS_MAX) --ct;
+    if (layer_lds_floats(ct, N) * 4 > LDS_MAX) return fail(NONODE_EUNSUPPORTED, "N=%d too large for the LDS sender table", N);
+    cpg = (N + 16 * ct - 1) / (16 * ct);
+    ct = ((N + cpg - 1) / cpg + 15) / 16;   // the same slice count with the least padding
+  }
+  const int s_rows = cg * N;
+  const size_t lds = layer_lds_floats(ct, s_rows) * 4;
+  const int n_units = (n_graphs + cg - 1) / cg;
+  const int G = n_units < cus ? n_units : cus;
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
-  a.n_total = n_total; a.n_graphs = n_graphs; a.N = N; a.ne = ne; a.ef_mod = ef_mod; a.ct = ct;
+  a.n_total = n_total; a.n_graphs = n_graphs; a.N = N; a.ne = ne; a.ef_mod = ef_mod;
+  a.cg = cg; a.cpg = cpg; a.n_units = n_units; a.ct = ct; a.s_rows = s_rows;
   if (steps < 1 || (steps > 1 && !pp)) return fail(NONODE_EINVAL, "layer: steps=%d", steps);
   a.steps = steps;
   a.m_out = m_out; a.f_out = f_out;
@@ -1482,12 +1514,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
     a.pp_x[i] = pp ? pp[2 + i] : nullptr;
     a.pp_v[i] = pp ? pp[4 + i] : nullptr;
   }
-  static const int dbg = getenv("NONODE_DEBUG") ? atoi(getenv("NONODE_DEBUG")) : 0;
-  // wave configuration (NONODE_CFG): 0 = 8 waves, one unit per iteration; 1 = 4 waves (one per
-  // SIMD, 512-register budget), two units per iteration; 2 = 8 waves, two units per iteration
-  static const int cfg = getenv("NONODE_CFG") ? atoi(getenv("NONODE_CFG")) : 1;
-  a.debug = dbg;
-  a.s_max = s_max; a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
+  a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
   a.use_perm = 0;
   if (xcd_cols > 0 && G % 8 == 0 && G <= 256 && xcd_on()) {
     // chunk c starts at column (first receiver row mod xcd_cols); its XCD block is that column's
@@ -1496,7 +1523,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
     int left[256], nleft = 0;
     for (int k = 0; k < G; ++k) a.chunk_of[k] = 0xffff;
     for (int c = 0; c < G; ++c) {
-      const long long row0 = (((long long)c * n_graphs) / G) * N;
+      const long long row0 = (((long long)c * n_units) / G) * cg * N;
       const int x = (int)((row0 % xcd_cols) * 8 / xcd_cols);
       if (slot_fill[x] < G / 8) a.chunk_of[x + 8 * slot_fill[x]++] = (unsigned short)c;
       else left[nleft++] = c;
@@ -1508,9 +1535,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   ProfScope prof(VARIANT, stream);
   if (ne == 0) { a.ef = blob; a.ne = 1; a.ef_mod = 1; }   // dummy gather target; feature weights are 0
   const int kf = a.ne <= 3 ? 1 : 2;
-  if (cfg == 1) launch_cfg<VARIANT, 4, true>(kf, G, lds, stream, a);
-  else if (cfg == 2) launch_cfg<VARIANT, 8, true>(kf, G, lds, stream, a);
-  else launch_cfg<VARIANT, 8, false>(kf, G, lds, stream, a);
+  launch_cfg<VARIANT>(kf, G, lds, stream, a);
   return check_launch("egnn_layer_kernel");
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one rocprofv3 --pmc run each, <= 8 SQ counters) over the C2 bench, then a per-kernel
-# summary (tools/pmc_summary.py). NONODE_DEBUG / NONODE_LIB pass through.
+# summary (tools/pmc_summary.py). NONODE_LIB passes through.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp PYTHONDONTWRITEBYTECODE=1
 OUT=gpurun_out/prof_${TAG:-pmc}
