@@ -34,7 +34,10 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 // Pair loop with unit B's VALU stages placed beside unit A's MFMA blocks: SEGNO only (there it fits
 // the register file; for EGNO it spills and slows the guard path)
-template <int VARIANT> constexpr bool kStagger = VARIANT == 1;
+#ifndef NONODE_STAGGER_EGNO
+#define NONODE_STAGGER_EGNO 0
+#endif
+template <int VARIANT> constexpr bool kStagger = VARIANT == 1 || NONODE_STAGGER_EGNO;
 // tconv_kernel h stream cache policy: bit 0 = nontemporal loads, bit 1 = nontemporal stores
 #ifndef NONODE_TC_NT
 #define NONODE_TC_NT 0
@@ -409,6 +412,31 @@ __device__ __forceinline__ float dot_vp(const f4 (&a)[4], const float* vp, int g
   return group_sum(s);
 }
 
+// max over the 4 lane groups (the column max of an ECL activation)
+__device__ __forceinline__ float group_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+// acc = W x + bias for one 16-column unit whose activations may leave the fp16 range (the guard
+// path): every column (edge) is scaled by 2^-s, s >= 0 the smallest shift that brings its largest
+// |value| below 2^13, before the fp16x3 split, and the product is scaled back by 2^s. Both scalings
+// are exact, so the result keeps the fp16x3 path's ~2^-22 relative accuracy at any magnitude.
+__device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const h8* wh, const f4 (&x)[4], int lane) {
+  const float cmax = group_max(amax_ecl(x));
+  const int s = max(__builtin_amdgcn_frexp_expf(cmax) - 13, 0);
+  const float dn = __uint_as_float((unsigned)(127 - s) << 23), up = __uint_as_float((unsigned)(127 + min(s, 127)) << 23);
+  f4 xs[4], t[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { xs[mt] = x[mt] * dn; t[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
+  h8 xh[2], xl[2];
+  h16_split(xs, xh, xl);
+  mfma_h16(t, wh, xh, xl, lane);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt] += t[mt] * up;
+}
+
 // ---- weight packing ---------------------------------------------------------------------------
 struct PackArgs {
   const float* w1; int ld1; int colA, colB, colS;   // edge W1 [64][ld1]
@@ -569,9 +597,11 @@ size_t layer_lds_floats(int ct, int s_rows) {
 // samples with the same chunking, identical to the whole batch's.
 // KF: feature k-steps (1 + ne scalar edge inputs, 4 per step). Four waves, one per SIMD (512-register
 // budget), two units per iteration.
-template <int VARIANT, int KF>
-__global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
-  constexpr int NW = 4;
+// NW = 4: one wave per SIMD (512-register budget), two units per iteration; NW = 8: two waves per
+// SIMD (256 registers each), one unit per iteration, fragments and biases read from LDS.
+template <int VARIANT, int KF, int NW>
+__global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
+  constexpr bool PAIR = NW == 4;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
@@ -614,11 +644,42 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
       rbase = s0 + part * 16 * p.ct; nend = min(rbase + 16 * p.ct, s0 + N);
     }
   };
-  // phase A job of a chunk: job < ctc: receiver projections P = W1[h_i] h + b1 of tile `job`;
-  // else sender projections Q = W1[h_j] h of sender tile job - ctc (LDS tables), and the sender
-  // positions (all threads)
+  // phase A jobs of a chunk (LDS tables of the edge phase). Whole-graph chunks (cpg = 1: the
+  // receivers are the senders): job = tile, P = W1[h_i] h + b1 and Q = W1[h_j] h from one h load and
+  // one fp16 split. Receiver slices of a large graph: job < ctc: P of receiver tile `job`, else Q of
+  // sender tile job - ctc.
+  auto proj_jobs = [&](int rbase, int nend, int S) __attribute__((always_inline)) {
+    const int ctc = (nend - rbase + 15) >> 4;
+    return p.cpg == 1 ? ctc : ctc + ((S + 15) >> 4);
+  };
   auto proj_job = [&](const float* __restrict__ hI, const float* blob, int rbase, int nend, int s0, int S,
                       int job) __attribute__((always_inline)) {
+    int joff = 0;
+    asm volatile("" : "+s"(joff));   // weight reads stay in the job (LICM would pin them in VGPRs)
+    blob += joff;
+    if (p.cpg == 1) {
+      const int local = job * 16 + e;
+      const bool valid = rbase + local < nend;
+      f4 hin[4], ap[4], aq[4];
+      load_ecl(hin, hI + (size_t)(valid ? rbase + local : nend - 1) * HID, g);
+      load_vp(ap, blob + OFF_VEC + V_B1 * 64, g);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) aq[mt] = f4{0.f, 0.f, 0.f, 0.f};
+      if (__builtin_expect(__any(amax_ecl(hin) > H16_LIMIT), 0)) {
+        mfma_dense<4>(ap, blob + OFF_WA, hin, lane);
+        mfma_dense<4>(aq, blob + OFF_WB, hin, lane);
+      } else {
+        h8 xh[2], xl[2];
+        h16_split(hin, xh, xl);
+        mfma_h16(ap, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), xh, xl, lane);
+        mfma_h16(aq, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), xh, xl, lane);
+      }
+      if (valid) {
+        store_ecl(sP + local * ROWP, ap, g);
+        store_ecl(sQ + local * ROWP, aq, g);
+      }
+      return;
+    }
     const int ctc = (nend - rbase + 15) >> 4;
     const bool isP = job < ctc;                       // wave-uniform
     const int local = (isP ? job : job - ctc) * 16 + e;
@@ -657,7 +718,7 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
     int rbase, nend, s0, S;
     chunk_at(ch0, rbase, nend, s0, S);
     load_sx(xI, s0, S);
-    const int J = ((nend - rbase + 15) >> 4) + ((S + 15) >> 4);
+    const int J = proj_jobs(rbase, nend, S);
     #pragma unroll 1
     for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job);
   }
@@ -683,12 +744,17 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
     // the edge phase.
     {
       const int U = ctc * Nm1;
-      const int u1 = ((wave + 1) * U) / NW;
-      int u = (wave * U) / NW;
+      // waves taking part: a tile must span at most 4 waves (two contributions per sum slot), so
+      // every wave's range holds at least a third of a tile
+      const int NWB = min(NW, 3 * ctc);
+      const int u1 = wave < NWB ? ((wave + 1) * U) / NWB : 0;
+      int u = wave < NWB ? (wave * U) / NWB : 0;
       f4 rB2[4], rBC1[4], rWC2[4];
-      load_vp(rB2, vB2_, g);
-      load_vp(rBC1, vBC1_, g);
-      load_vp(rWC2, vWC2_, g);
+      if (PAIR) {
+        load_vp(rB2, vB2_, g);
+        load_vp(rBC1, vBC1_, g);
+        load_vp(rWC2, vWC2_, g);
+      }
       #pragma unroll 1
       while (u < u1) {
         const int tau = u / Nm1;
@@ -756,7 +822,7 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
         };
         auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
           silu_ecl(c1);
-          const float c = dot_r(c1, rWC2) + bc2;
+          const float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2_, g)) + bc2;
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
           if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
             f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -768,10 +834,8 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
 
         const h8* w2h = reinterpret_cast<const h8*>(sW);
         const h8* wc1h = reinterpret_cast<const h8*>(sW + 4096);
-        const float* w2f = p.blob + OFF_W2;     // exact fp32 fragments (global) for the guard path
-        const float* wc1f = p.blob + OFF_WC1;
         int k = k_lo;
-        {
+        if constexpr (PAIR) {
           // Two units (32 edges, same receivers) per iteration. The hot body is ONE basic block:
           // both units always take the fp16x3 path while the largest |activation| is tracked, and
           // only if it exceeded the fp16 range (rare) is the pair recomputed on exact f32 MFMAs
@@ -810,7 +874,7 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
               f2 = fminf(fmaxf(f2, -100.f), 100.f);
             }
           };
-          // exact f32 recomputation of one unit (the guard path)
+          // recomputation of one unit with column-scaled fp16x3 products (the guard path)
           auto exact_unit = [&](int k, const float (&ev)[KF], f4 (&m)[4], float& f0, float& f1, float& f2)
               __attribute__((always_inline)) {
             f4 a[4], c[4];
@@ -819,11 +883,11 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
             silu_ecl(a);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
-            mfma_dense<4>(m, w2f, a, lane);
+            mm64_scaled(m, w2h, a, lane);
             silu_ecl(m);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
-            mfma_dense<4>(c, wc1f, m, lane);
+            mm64_scaled(c, wc1h, m, lane);
             edge_f(c, r0, r1, r2, f0, f1, f2);
           };
           float e0[KF], e1[KF];
@@ -946,6 +1010,13 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
         for (; k <= k_hi; ++k) {
           float en[KF];
           fetch_ef(min(k + 1, k_hi), en);
+          // fragment / bias reads stay in the loop (LICM would pin them in VGPRs)
+          int loff = 0;
+          asm volatile("" : "+v"(loff));
+          const h8* w2l = w2h + loff;
+          const h8* wc1l = wc1h + loff;
+          const float* vB2l = vB2_ + loff;
+          const float* vBC1l = vBC1_ + loff;
           f4 a[4], m[4];
           float r0, r1, r2;
           head(k, e0, a, r0, r1, r2);
@@ -953,27 +1024,35 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
           for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
           STAMP(0);
           silu_ecl(a);
+          if (PAIR) {
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
+            for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
+          } else {
+            load_vp(m, vB2l, g);
+          }
           if (__builtin_expect(__any(amax_ecl(a) > H16_LIMIT), 0)) {
-            mfma_dense<4>(m, w2f, a, lane);
+            mm64_scaled(m, w2l, a, lane);
           } else {
             h8 ah[2], al[2];
             h16_split(a, ah, al);
-            mfma_h16(m, w2h, ah, al, lane);   // m = SiLU(W2 a + b2)
+            mfma_h16(m, w2l, ah, al, lane);   // m = SiLU(W2 a + b2)
           }
           STAMP(1);
           silu_ecl(m);
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
+          if (PAIR) {
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) a[mt] = rBC1[mt];
+            for (int mt = 0; mt < 4; ++mt) a[mt] = rBC1[mt];
+          } else {
+            load_vp(a, vBC1l, g);
+          }
           if (__builtin_expect(__any(amax_ecl(m) > H16_LIMIT), 0)) {
-            mfma_dense<4>(a, wc1f, m, lane);
+            mm64_scaled(a, wc1l, m, lane);
           } else {
             h8 mh[2], ml[2];
             h16_split(m, mh, ml);
-            mfma_h16(a, wc1h, mh, ml, lane);  // SiLU(Wc1 m + bc1)
+            mfma_h16(a, wc1l, mh, ml, lane);  // SiLU(Wc1 m + bc1)
           }
           STAMP(2);
           tail(a, r0, r1, r2);
@@ -1013,18 +1092,27 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
         chunk_at(ci + 1, nrb, nne, ns0, nS);
         load_sx(xI, ns0, nS);
       }
-      const int J = ctc + (has_next ? ((nne - nrb + 15) >> 4) + ((nS + 15) >> 4) : 0);
+      const int J = ctc + (has_next ? proj_jobs(nrb, nne, nS) : 0);
       constexpr int C_COST = 4;
-      int ld0 = 0, ld1 = 0, ld2 = 0, ld3 = 0;
+      const int A_COST = p.cpg == 1 ? 2 : 1;
+      int ld[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) ld[i] = 0;
       #pragma unroll 1
       for (int j = 0; j < J; ++j) {
-        const int m01 = min(ld0, ld1), m23 = min(ld2, ld3);
-        const int w = m01 <= m23 ? (ld0 <= ld1 ? 0 : 1) : (ld2 <= ld3 ? 2 : 3);
-        const int c = j < ctc ? C_COST : 1;
-        ld0 += w == 0 ? c : 0; ld1 += w == 1 ? c : 0; ld2 += w == 2 ? c : 0; ld3 += w == 3 ? c : 0;
+        int w = 0, lw = ld[0];
+#pragma unroll
+        for (int i = 1; i < NW; ++i)
+          if (ld[i] < lw) { lw = ld[i]; w = i; }
+        const int c = j < ctc ? C_COST : A_COST;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) ld[i] += i == w ? c : 0;
         if (w != wave) continue;
+        int joff = 0;
+        asm volatile("" : "+s"(joff));   // weight reads stay in the job (LICM would pin them in VGPRs)
+        const float* bj = blob + joff;
         if (j >= ctc) {
-          proj_job(hI, blob, nrb, nne, ns0, nS, j - ctc);
+          proj_job(hI, bj, nrb, nne, ns0, nS, j - ctc);
           continue;
         }
         const int tau = j;
@@ -1059,10 +1147,10 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
         if (VARIANT == EGNO) {
           // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
           f4 t[4];
-          load_vp(t, blob + OFF_VEC + V_BV1 * 64, g);
-          mm64(t, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WV1 * 4096), blob + OFF_WV1, hr, lane);
+          load_vp(t, bj + OFF_VEC + V_BV1 * 64, g);
+          mm64(t, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WV1 * 4096), bj + OFF_WV1, hr, lane);
           silu_ecl(t);
-          const float phi = dot_vp(t, blob + OFF_VEC + V_WV2 * 64, g) + bv2;
+          const float phi = dot_vp(t, bj + OFF_VEC + V_WV2 * 64, g) + bv2;
           nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
           nx1 = x1 + phi * v1 + fminf(fmaxf(F1 * p.inv_deg, -100.f), 100.f);
           nx2 = x2 + phi * v2 + fminf(fmaxf(F2 * p.inv_deg, -100.f), 100.f);
@@ -1077,20 +1165,20 @@ __global__ __launch_bounds__(256) void egnn_layer_kernel(LayerArgs p) {
         }
         // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
         f4 z[4];
-        load_vp(z, blob + OFF_VEC + V_BN1 * 64, g);
+        load_vp(z, bj + OFF_VEC + V_BN1 * 64, g);
         if (__builtin_expect(__any(fmaxf(amax_ecl(hr), amax_ecl(Mr)) > H16_LIMIT), 0)) {
-          mfma_dense<8>(z, blob + OFF_WN1, in8, lane);
+          mfma_dense<8>(z, bj + OFF_WN1, in8, lane);
         } else {
           h8 xh[2], xl[2];
           h16_split(hr, xh, xl);
-          mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1A * 4096), xh, xl, lane);
+          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1A * 4096), xh, xl, lane);
           h16_split(Mr, xh, xl);
-          mfma_h16(z, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN1B * 4096), xh, xl, lane);
+          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1B * 4096), xh, xl, lane);
         }
         silu_ecl(z);
         f4 hn[4];
-        load_vp(hn, blob + OFF_VEC + V_BN2 * 64, g);
-        mm64(hn, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WN2 * 4096), blob + OFF_WN2, z, lane);
+        load_vp(hn, bj + OFF_VEC + V_BN2 * 64, g);
+        mm64(hn, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN2 * 4096), bj + OFF_WN2, z, lane);
         if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
   #pragma unroll
           for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
@@ -1456,16 +1544,21 @@ bool xcd_on() {
   static const int on = getenv("NONODE_XCD") ? atoi(getenv("NONODE_XCD")) : 1;
   return on != 0;
 }
-template <int VARIANT>
+template <int VARIANT, int NW>
 void launch_cfg(int kf, int G, size_t lds, hipStream_t stream, const LayerArgs& a) {
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1>), dim3(G), dim3(256), lds, stream, a);
-  else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2>), dim3(G), dim3(256), lds, stream, a);
+  if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, NW>), dim3(G), dim3(NW * 64), lds, stream, a);
+  else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, NW>), dim3(G), dim3(NW * 64), lds, stream, a);
 }
+// waves per workgroup: 4 (one per SIMD, paired units) for N < 64, else 8 (two per SIMD, single
+// units): measured C2 (N = 20) 255 vs 271 us per launch, C5 (N = 100) 1594 vs 1496 us
+#ifndef NONODE_LAYER_WAVES
+#define NONODE_LAYER_WAVES 0   // 0: by N as above; 4 / 8: forced (A/B builds)
+#endif
 // steps > 1 runs that many substeps in one launch (SEGNO forward_step), ping-ponging through
 // pp = {h0, h1, x0, x1, v0, v1} (each n_graphs*N rows)
 template <int VARIANT>
@@ -1535,7 +1628,9 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   ProfScope prof(VARIANT, stream);
   if (ne == 0) { a.ef = blob; a.ne = 1; a.ef_mod = 1; }   // dummy gather target; feature weights are 0
   const int kf = a.ne <= 3 ? 1 : 2;
-  launch_cfg<VARIANT>(kf, G, lds, stream, a);
+  const int nw = NONODE_LAYER_WAVES ? NONODE_LAYER_WAVES : (N < 64 ? 4 : 8);
+  if (nw == 8) launch_cfg<VARIANT, 8>(kf, G, lds, stream, a);
+  else launch_cfg<VARIANT, 4>(kf, G, lds, stream, a);
   return check_launch("egnn_layer_kernel");
 }
 
