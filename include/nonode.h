@@ -191,7 +191,7 @@ typedef struct {
 
 /* Floats in one backward blob (unscaled forward + transposed fragments). */
 size_t nonode_bwd_blob_floats(void);
-/* Pack one EGNO layer for the backward pass (EGNO only). */
+/* Pack one EGNO (or SEGNO) layer for the backward pass. */
 int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
                           float* bblob, void* stream);
 
@@ -248,6 +248,28 @@ int nonode_egno_backward_frames(int B, int N, int T, int n_layers, int in_node, 
                                 const float* g_h, const nonode_layer_grads* layer_grads, float* const* g_tconv,
                                 float* const* g_tconvx, float* g_emb_w, float* g_emb_b, void* workspace,
                                 size_t workspace_bytes, void* stream);
+
+/*
+ * SEGNO training (replaces loss.backward() of SEGNO/train_nbody.py:168-179 through forward_step,
+ * SEGNO/models/model.py:95-102, = T applications of SEGNO_GCL.forward, gcl.py:111-119, dt = 1/T).
+ * nonode_segno_forward_train: forward_step from an embedded h [B*N][64] (the caller's embedding
+ * Linear, model.py:73, stays on the autograd tape) that also saves every substep's inputs and sums;
+ * outputs equal nonode_segno_forward_step's. blob: nonode_pack_layer(..., NONODE_VARIANT_SEGNO, ...).
+ * nonode_segno_backward: given the gradients of (x, v, h) after the T substeps (g_v, g_h may be
+ * null = zero), writes the gradients of the shared GCL weights into *grads (vel_* fields unused:
+ * coord_mlp_vel is not on SEGNO's forward path) and of the inputs h, x, v (each may be null).
+ * bblob: nonode_pack_layer_bwd(..., NONODE_VARIANT_SEGNO, ...).
+ */
+size_t nonode_segno_train_state_bytes(int B, int N, int T);
+int nonode_segno_forward_train(int B, int N, int T, int n_edge_feat, const float* h, const float* x,
+                               const float* v, const float* edge_attr, const float* blob, float coords_weight,
+                               int recurrent, float* x_out, float* v_out, float* h_out, void* state,
+                               size_t state_bytes, void* stream);
+size_t nonode_segno_backward_workspace_bytes(int B, int N);
+int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_weight, int recurrent,
+                          const float* edge_attr, const float* bblob, const void* state, const float* g_x,
+                          const float* g_v, const float* g_h, const nonode_layer_grads* grads, float* g_h_in,
+                          float* g_x_in, float* g_v_in, void* workspace, size_t workspace_bytes, void* stream);
 
 
 /* ---- rollout drivers (rollout_fn / prepare_inputs / energy on the GPU) ---- */

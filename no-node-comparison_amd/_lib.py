@@ -20,6 +20,8 @@ SYMBOLS = (
     "nonode_profile_end", "nonode_tconv_blob_floats", "nonode_pack_tconv",
     "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
     "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
+    "nonode_segno_train_state_bytes", "nonode_segno_forward_train", "nonode_segno_backward_workspace_bytes",
+    "nonode_segno_backward",
     "nonode_egno_forward_train_frames", "nonode_egno_backward_frames",
     "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
     "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout", "nonode_sim_charged", "nonode_sim_gravity",
@@ -99,6 +101,13 @@ def lib():
     L.nonode_egno_backward.argtypes = ([_i] * 9 + [_vp] * 2 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
                                        + [ctypes.POINTER(LayerGrads), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]
                                        + [_vp] * 3 + [_sz, _vp])
+    L.nonode_segno_train_state_bytes.argtypes = [_i] * 3
+    L.nonode_segno_train_state_bytes.restype = _sz
+    L.nonode_segno_forward_train.argtypes = [_i] * 4 + [_vp] * 5 + [_f, _i] + [_vp] * 4 + [_sz, _vp]
+    L.nonode_segno_backward_workspace_bytes.argtypes = [_i] * 2
+    L.nonode_segno_backward_workspace_bytes.restype = _sz
+    L.nonode_segno_backward.argtypes = ([_i] * 4 + [_f, _i] + [_vp] * 6 + [ctypes.POINTER(LayerGrads)]
+                                        + [_vp] * 4 + [_sz, _vp])
     L.nonode_prepare_inputs.argtypes = [_i, _i, _i] + [_vp] * 5 + [_i] + [_vp] * 6
     L.nonode_energy.argtypes = [_i] * 4 + [_vp] * 5
     L.nonode_egno_rollout_workspace_bytes.argtypes = [_i] * 6

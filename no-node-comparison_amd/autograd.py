@@ -100,3 +100,64 @@ def egno_forward_train(model, x, h, edge_fea, v, loc_mean, t_out, B, N, t_in=Non
     multi-input form, see EGNO._forward_multi)."""
     params = [p for _, p in model.named_parameters()]
     return EGNOTrain.apply(model, x, h, edge_fea, v, loc_mean, t_out, t_in, B, N, *params)
+
+
+class SEGNOStepTrain(torch.autograd.Function):
+    """SEGNO.forward_step (SEGNO/models/model.py:95-102) on the autograd tape: T substeps of
+    SEGNO_GCL (gcl.py:111-119) from an embedded h. Forward: nonode_segno_forward_train (the inference
+    kernels, one launch per substep, saving each substep's state); backward: nonode_segno_backward
+    (gradients of the shared GCL weights and of h, x, v)."""
+
+    @staticmethod
+    def forward(ctx, model, h, x, v, edge_attr, T, B, N, *params):
+        L = _lib.lib()
+        dev = x.device
+        h, x, v, ea = _f32(h), _f32(x), _f32(v), _f32(edge_attr)
+        blob = model._packed()
+        n = B * N
+        x_out = torch.empty(n, 3, device=dev)
+        v_out = torch.empty(n, 3, device=dev)
+        h_out = torch.empty(n, model.hidden_nf, device=dev)
+        st_bytes = L.nonode_segno_train_state_bytes(B, N, T)
+        state = torch.empty((st_bytes + 3) // 4, dtype=torch.float32, device=dev)
+        _lib.check(L.nonode_segno_forward_train(B, N, T, model.in_edge_nf, _lib.ptr(h), _lib.ptr(x), _lib.ptr(v),
+                                                _lib.ptr(ea), _lib.ptr(blob), float(model.coords_weight),
+                                                int(bool(model.recurrent)), _lib.ptr(x_out), _lib.ptr(v_out),
+                                                _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.stream_of(x)))
+        ctx.model, ctx.T, ctx.B, ctx.N = model, T, B, N
+        ctx.state, ctx.ea = state, ea
+        return x_out, h_out, v_out
+
+    @staticmethod
+    def backward(ctx, gx, gh, gv):
+        model, T, B, N = ctx.model, ctx.T, ctx.B, ctx.N
+        L = _lib.lib()
+        dev = ctx.state.device
+        n = B * N
+        bblob = model._packed_bwd()
+        names = model.gcl_param_names()
+        named = dict(model.named_parameters())
+        grads = {nm: torch.empty_like(named[nm]) for nm in names if nm is not None}
+        lg = _lib.LayerGrads(*[grads[nm].data_ptr() if nm is not None else None for nm in names])
+        ws_bytes = L.nonode_segno_backward_workspace_bytes(B, N)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+        gx = _f32(gx) if gx is not None else None
+        gv = _f32(gv) if gv is not None else None
+        gh = _f32(gh) if gh is not None else None
+        g_h = torch.empty(n, model.hidden_nf, device=dev)
+        g_x = torch.empty(n, 3, device=dev)
+        g_v = torch.empty(n, 3, device=dev)
+        _lib.check(L.nonode_segno_backward(B, N, T, model.in_edge_nf, float(model.coords_weight),
+                                           int(bool(model.recurrent)), _lib.ptr(ctx.ea), _lib.ptr(bblob),
+                                           _lib.ptr(ctx.state), _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh),
+                                           ctypes.byref(lg), _lib.ptr(g_h), _lib.ptr(g_x), _lib.ptr(g_v),
+                                           _lib.ptr(ws), ws_bytes, _lib.stream_of(g_h)))
+        ctx.state = None
+        out = [grads.get(nm) for nm, _ in model.module.named_parameters(prefix="module")]
+        return (None, g_h, g_x, g_v, None, None, None, None) + tuple(out)
+
+
+def segno_step_train(model, h, x, v, edge_attr, T, B, N):
+    """forward_step that records the kernels' backward on the autograd tape."""
+    params = [p for _, p in model.module.named_parameters()]
+    return SEGNOStepTrain.apply(model, h, x, v, edge_attr, T, B, N, *params)

@@ -82,12 +82,12 @@ __global__ void pack_bwd_kernel(PackArgs a) {
     case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
     case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
     case 3: if (d < 4096) pack_frag(B + BOFF_WC1, a.cw1, 64, 0, 4, d, 1.f); break;
-    case 4: if (d < 4096) pack_frag(B + BOFF_WV1, a.vw1, 64, 0, 4, d, 1.f); break;
+    case 4: if (d < 4096) { if (a.vw1) pack_frag(B + BOFF_WV1, a.vw1, 64, 0, 4, d, 1.f); else B[BOFF_WV1 + d] = 0.f; } break;
     case 5: pack_frag(B + BOFF_WN1, a.nw1, 128, 0, 8, d, 1.f); break;
     case 6: if (d < 4096) pack_frag(B + BOFF_WN2, a.nw2, 64, 0, 4, d, 1.f); break;
     case 7: if (d < 4096) pack_frag_t(B + BOFF_W2T, a.w2, 64, 0, d); break;
     case 8: if (d < 4096) pack_frag_t(B + BOFF_WC1T, a.cw1, 64, 0, d); break;
-    case 9: if (d < 4096) pack_frag_t(B + BOFF_WV1T, a.vw1, 64, 0, d); break;
+    case 9: if (d < 4096) { if (a.vw1) pack_frag_t(B + BOFF_WV1T, a.vw1, 64, 0, d); else B[BOFF_WV1T + d] = 0.f; } break;
     case 10: if (d < 4096) pack_frag_t(B + BOFF_WN2T, a.nw2, 64, 0, d); break;
     case 11: if (d < 4096) pack_frag_t(B + BOFF_WN1TH, a.nw1, 128, 0, d); break;
     case 12: if (d < 4096) pack_frag_t(B + BOFF_WN1TM, a.nw1, 128, HID, d); break;
@@ -378,6 +378,8 @@ constexpr int EB_TSTRIDE = 2 * 16 * ROWT; // per-wave transpose tile (two [16][R
 
 struct EdgeBwdArgs {
   int n_graphs, N, ne, ef_mod, ct, s_max;
+  int segno;   // SEGNO_GCL (gcl.py:97-100): every edge's translation r c is clamped to +-100 before the
+               // mean, so its gradient passes only where |r_d c| <= 100 (EGNO clamps the mean instead)
   const float* h; const float* x; const float* ef; const float* bb;
   const float* gF; const float* gM;
   float* GA; float* GB; float* GX;                                    // per node (GB, GX atomically)
@@ -706,8 +708,13 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         silu_keep(z3, sg3, c1);
         c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
       }
-      // reverse: f = r c
-      const float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
+      // reverse: f = r c (SEGNO: clamp(r c, +-100) per edge)
+      float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
+      if (p.segno) {
+        gF0 = fabsf(r0 * c) <= 100.f ? gF0 : 0.f;
+        gF1 = fabsf(r1 * c) <= 100.f ? gF1 : 0.f;
+        gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
+      }
       const float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
       float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
       // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
@@ -1449,15 +1456,18 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   if (!w || !bblob) return fail(NONODE_EINVAL, "pack_layer_bwd: null pointer");
   if (hidden != HID || n_edge_feat < 0 || n_edge_feat > 4)
     return fail(NONODE_EUNSUPPORTED, "pack_layer_bwd: hidden=%d n_edge_feat=%d", hidden, n_edge_feat);
-  if (variant != NONODE_VARIANT_EGNO) return fail(NONODE_EUNSUPPORTED, "pack_layer_bwd: EGNO only");
-  if (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2)
+  const bool egno = variant == NONODE_VARIANT_EGNO;
+  if (!egno && variant != NONODE_VARIANT_SEGNO) return fail(NONODE_EINVAL, "pack_layer_bwd: variant %d", variant);
+  if (egno && (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2))
     return fail(NONODE_EINVAL, "pack_layer_bwd: EGNO needs node_v_net weights");
   PackArgs a;
   a.ld1 = 2 * HID + 1 + n_edge_feat;
-  a.colS = 0; a.colA = 1; a.colB = 1 + HID;
+  if (egno) { a.colS = 0; a.colA = 1; a.colB = 1 + HID; }       // [s, h_i, h_j, e]  basic.py:152-154
+  else { a.colA = 0; a.colB = HID; a.colS = 2 * HID; }          // [h_i, h_j, s, e]  gcl.py:78
   a.w1 = w->edge_w1; a.b1 = w->edge_b1; a.w2 = w->edge_w2; a.b2 = w->edge_b2;
   a.cw1 = w->coord_w1; a.cb1 = w->coord_b1; a.cw2 = w->coord_w2; a.cb2 = w->coord_b2;
-  a.vw1 = w->vel_w1; a.vb1 = w->vel_b1; a.vw2 = w->vel_w2; a.vb2 = w->vel_b2;
+  a.vw1 = egno ? w->vel_w1 : nullptr; a.vb1 = egno ? w->vel_b1 : nullptr;
+  a.vw2 = egno ? w->vel_w2 : nullptr; a.vb2 = egno ? w->vel_b2 : nullptr;
   a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
   a.ne = n_edge_feat;
   a.blob = bblob;
@@ -1626,6 +1636,7 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
       static const int ebdbg = getenv("NONODE_EBDBG") ? atoi(getenv("NONODE_EBDBG")) : 0;
       ea.dbg = ebdbg;
       ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = frames ? T * B : B; ea.ct = 0; ea.s_max = 0;
+      ea.segno = 0;
       ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
       ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
@@ -1735,6 +1746,229 @@ int nonode_egno_backward_frames(int B, int N, int T, int n_layers, int in_node, 
   return egno_backward_impl(1, (with_t_in ? 2 : 1) * time_emb_dim, B, N, T, n_layers, in_node, n_edge_feat,
                             time_emb_dim, modes, Bt, loc_mean, edge_fea, bblobs, tconv_w, tconvx_w, state, g_x, g_v,
                             g_h, layer_grads, g_tconv, g_tconvx, g_emb_w, g_emb_b, workspace, workspace_bytes, stream);
+}
+
+}  // extern "C"
+
+// ================================================================================================
+// SEGNO training: forward_step (model.py:95-102) = T applications of SEGNO_GCL (gcl.py:111-119) with
+// shared weights and dt = 1/T, run as T single-substep launches that save every substep's inputs and
+// message / force sums; the reverse pass walks the substeps backwards on the EGNO backward kernels
+// (edge_bwd_kernel with the per-edge clamp of gcl.py:99-100, node_post_kernel, the GEMMs) and adds
+// every substep's weight gradients into the same outputs. Replaces loss.backward() of
+// train_nbody.py:168-179 through forward_step.
+namespace {
+
+struct SegnoNodeBwdArgs {
+  int n, N, recurrent;
+  float dt, cw;
+  const float* h; const float* M;                       // substep inputs h, saved message sums
+  const float* gxo; const float* gvo; const float* gho;  // grads of the substep outputs
+  const float* bb;
+  float* gv; float* gF; float* gM; float* ghp;           // outputs
+  float* op_z; float* op_gz;                             // GEMM operands (node MLP weight gradients)
+};
+
+// reverse of  v' = v + cw mean_j clamp(r_ij c_ij) dt ;  x' = x + v' dt   (gcl.py:255-257, 242)
+//             h' = [h +] WN2 SiLU(WN1 [h, M] + bn1) + bn2                 (gcl.py:85-95)
+// gF is the gradient of the per-receiver sum of the clamped edge translations (the per-edge clamp
+// mask is applied by edge_bwd_kernel, which recomputes r c)
+__global__ __launch_bounds__(256) void segno_node_bwd_kernel(SegnoNodeBwdArgs p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
+  const int r0 = (blockIdx.x * 4 + wave) * 16;
+  if (r0 >= p.n) return;
+  const int r = min(r0 + e, p.n - 1);
+  const bool valid = r0 + e < p.n;
+  const float* bb = p.bb;
+  f4 hr[4], Mr[4], in8[8];
+  load_ecl(hr, p.h + (size_t)r * HID, g);
+  load_ecl(Mr, p.M + (size_t)r * HID, g);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
+  f4 zp[4], z[4];
+  load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
+  mfma_dense<8>(zp, bb + BOFF_WN1, in8, lane);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
+  silu_true(z);
+  f4 gho[4], gz[4], gh[4], gM[4];
+  load_ecl(gho, p.gho + (size_t)r * HID, g);
+  zero4(gz);
+  mfma_dense<4>(gz, bb + BOFF_WN2T, gho, lane);
+  mul_dsilu(gz, zp);
+  if (p.recurrent) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) gh[mt] = gho[mt];
+  } else {
+    zero4(gh);
+  }
+  mfma_dense<4>(gh, bb + BOFF_WN1TH, gz, lane);
+  zero4(gM);
+  mfma_dense<4>(gM, bb + BOFF_WN1TM, gz, lane);
+  if (valid) {
+    const size_t o = (size_t)r * HID;
+    store_ecl(p.ghp + o, gh, g);
+    store_ecl(p.gM + o, gM, g);
+    store_ecl(p.op_z + o, z, g);
+    store_ecl(p.op_gz + o, gz, g);
+    if (g == 0) {
+      const float f = p.dt * p.cw / (float)(p.N - 1);
+      float gvt[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        gvt[d] = p.gvo[(size_t)r * 3 + d] + p.gxo[(size_t)r * 3 + d] * p.dt;
+        p.gv[(size_t)r * 3 + d] = gvt[d];
+      }
+      *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gvt[0] * f, gvt[1] * f, gvt[2] * f, 0.f};
+    }
+  }
+}
+
+struct SegnoState {
+  float *hs, *xs, *vs;   // (T + 1) x n x {64, 3, 3}: substep inputs (index T: the result)
+  float *Ms, *Fs;        // T x n x {64, 4}: message sums, clamped-translation sums of each substep
+  size_t floats;
+};
+SegnoState segno_state(void* base, int B, int N, int T) {
+  const size_t n = (size_t)B * N;
+  SegnoState st;
+  float* p = (float*)base;
+  auto take = [&](size_t cnt) { float* q = p; if (p) p += cnt; return q; };
+  st.hs = take((T + 1) * n * 64); st.xs = take((T + 1) * n * 3); st.vs = take((T + 1) * n * 3);
+  st.Ms = take(T * n * 64); st.Fs = take(T * n * 4);
+  st.floats = (size_t)(T + 1) * n * 70 + (size_t)T * n * 68;
+  return st;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t nonode_segno_train_state_bytes(int B, int N, int T) {
+  return segno_state(nullptr, B, N, T < 0 ? 0 : T).floats * sizeof(float);
+}
+
+int nonode_segno_forward_train(int B, int N, int T, int n_edge_feat, const float* h, const float* x,
+                               const float* v, const float* edge_attr, const float* blob, float coords_weight,
+                               int recurrent, float* x_out, float* v_out, float* h_out, void* state,
+                               size_t state_bytes, void* stream) {
+  if (B <= 0 || N < 2 || T < 0 || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "segno_forward_train: B=%d N=%d T=%d ne=%d", B, N, T, n_edge_feat);
+  if (!h || !x || !v || !blob || !x_out || !v_out || !h_out || !state || (n_edge_feat > 0 && !edge_attr))
+    return fail(NONODE_EINVAL, "segno_forward_train: null pointer");
+  if (state_bytes < nonode_segno_train_state_bytes(B, N, T))
+    return fail(NONODE_EINVAL, "segno_forward_train: state too small");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)B * N;
+  SegnoState st = segno_state(state, B, N, T);
+  hipMemcpyAsync(st.hs, h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(st.xs, x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(st.vs, v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  for (int t = 0; t < T; ++t) {
+    if (int rc = launch_layer<SEGNO>(B, N, n_edge_feat, B, st.hs + t * n * 64, st.xs + t * n * 3, st.vs + t * n * 3,
+                                     edge_attr, blob, 1.0f / (float)T, coords_weight, recurrent,
+                                     st.hs + (t + 1) * n * 64, st.xs + (t + 1) * n * 3, st.vs + (t + 1) * n * 3, s, 1,
+                                     nullptr, st.Ms + t * n * 64, st.Fs + t * n * 4))
+      return rc;
+  }
+  hipMemcpyAsync(h_out, st.hs + T * n * 64, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(x_out, st.xs + T * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(v_out, st.vs + T * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  return check_launch("segno_forward_train");
+}
+
+size_t nonode_segno_backward_workspace_bytes(int B, int N) {
+  return bwd_ws(nullptr, B, N, 1, 1).floats * sizeof(float);
+}
+
+int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_weight, int recurrent,
+                          const float* edge_attr, const float* bblob, const void* state, const float* g_x,
+                          const float* g_v, const float* g_h, const nonode_layer_grads* grads, float* g_h_in,
+                          float* g_x_in, float* g_v_in, void* workspace, size_t workspace_bytes, void* stream) {
+  if (B <= 0 || N < 2 || T < 0 || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "segno_backward: B=%d N=%d T=%d ne=%d", B, N, T, n_edge_feat);
+  if (!bblob || !state || !grads || !workspace || (n_edge_feat > 0 && !edge_attr))
+    return fail(NONODE_EINVAL, "segno_backward: null pointer");
+  const nonode_layer_grads& lg = *grads;
+  if (!lg.edge_w1 || !lg.edge_b1 || !lg.edge_w2 || !lg.edge_b2 || !lg.coord_w1 || !lg.coord_b1 || !lg.coord_w2 ||
+      !lg.coord_b2 || !lg.node_w1 || !lg.node_b1 || !lg.node_w2 || !lg.node_b2)
+    return fail(NONODE_EINVAL, "segno_backward: missing gradient pointer");
+  if (workspace_bytes < nonode_segno_backward_workspace_bytes(B, N))
+    return fail(NONODE_EINVAL, "segno_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int ne = n_edge_feat, ld1 = 2 * HID + 1 + ne;
+  const size_t n = (size_t)B * N;
+  const SegnoState st = segno_state(const_cast<void*>(state), B, N, T);
+  BwdWs w = bwd_ws(workspace, B, N, 1, 1);
+  Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
+  float *gx = w.gx[0], *gv = w.gv[0], *gh = w.gh[0];
+  if (g_x) hipMemcpyAsync(gx, g_x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  else hipMemsetAsync(gx, 0, n * 3 * sizeof(float), s);
+  if (g_v) hipMemcpyAsync(gv, g_v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  else hipMemsetAsync(gv, 0, n * 3 * sizeof(float), s);
+  if (g_h) hipMemcpyAsync(gh, g_h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  else hipMemsetAsync(gh, 0, n * 64 * sizeof(float), s);
+  if (T == 0) {   // no substep: every weight gradient is zero, the input gradients pass through
+    hipMemsetAsync(lg.edge_w1, 0, (size_t)64 * ld1 * sizeof(float), s);
+    for (float* q : {lg.edge_w2, lg.coord_w1, lg.node_w2}) hipMemsetAsync(q, 0, 64 * 64 * sizeof(float), s);
+    hipMemsetAsync(lg.node_w1, 0, 64 * 128 * sizeof(float), s);
+    for (float* q : {lg.edge_b1, lg.edge_b2, lg.coord_b1, lg.coord_w2, lg.node_b1, lg.node_b2})
+      hipMemsetAsync(q, 0, 64 * sizeof(float), s);
+    hipMemsetAsync(lg.coord_b2, 0, sizeof(float), s);
+  }
+  const int ntile = (int)((n + 15) / 16);
+  int cur = 0;
+  for (int t = T - 1; t >= 0; --t) {
+    const int acc = t < T - 1;   // substeps share the weights: add into the gradients after the first
+    const float* hs = st.hs + t * n * 64;
+    const float* Ms = st.Ms + t * n * 64;
+    const int nxt = cur ^ 1;
+    SegnoNodeBwdArgs na;
+    na.n = (int)n; na.N = N; na.recurrent = recurrent; na.dt = 1.0f / (float)T; na.cw = coords_weight;
+    na.h = hs; na.M = Ms; na.gxo = gx; na.gvo = gv; na.gho = gh; na.bb = bblob;
+    na.gv = w.gv[nxt]; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp; na.op_z = w.op_z; na.op_gz = w.op_gz;
+    hipLaunchKernelGGL(segno_node_bwd_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, na);
+    if (int rc = check_launch("segno_node_bwd_kernel")) return rc;
+    hipMemsetAsync(w.GB, 0, n * 64 * sizeof(float), s);
+    hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
+    {
+      int G = num_cus();
+      G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
+      G = B < G ? B : G;
+      EdgeBwdArgs ea;
+      ea.dbg = 0; ea.segno = 1;
+      ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
+      ea.h = hs; ea.x = st.xs + t * n * 3; ea.ef = ne ? edge_attr : bblob; ea.bb = bblob; ea.gF = w.gF;
+      ea.gM = w.gM; ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
+      if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
+      auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int col0) {
+        const int NO = M_ * (N_ + 1);
+        hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, w.wpart + off, G, M_, N_, dst, ld,
+                           col0, 1, bias, acc, 1.f, 1 << 30, 0, (long long)EW_STRIDE);
+        return check_launch("gemm_reduce(segno edge)");
+      };
+      if (int rc = red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 0)) return rc;
+      if (int rc = red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 0)) return rc;
+      if (int rc = red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 0)) return rc;
+      // edge Linear 1 scalar columns [s | e] (SEGNO order [h_i, h_j, s, e], gcl.py:78)
+      if (int rc = red(EW_FEAT, 64, 1 + ne, lg.edge_w1, ld1, nullptr, 2 * HID)) return rc;
+    }
+    hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, (int)n, w.ghp, w.GA, w.GB, gx, w.GX,
+                       bblob, w.gh[nxt], w.gx[nxt]);
+    if (int rc = check_launch("node_post_kernel")) return rc;
+    // node-level weight gradients of this substep (edge Linear 1 h_i / h_j blocks, node MLP)
+    if (int rc = gemm(w.GA, 64, 64, hs, 64, 64, (long long)n, lg.edge_w1, ld1, 0, lg.edge_b1, acc)) return rc;
+    if (int rc = gemm(w.GB, 64, 64, hs, 64, 64, (long long)n, lg.edge_w1, ld1, HID, nullptr, acc)) return rc;
+    if (int rc = gemm(w.op_gz, 64, 64, hs, 64, 64, (long long)n, lg.node_w1, 128, 0, lg.node_b1, acc)) return rc;
+    if (int rc = gemm(w.op_gz, 64, 64, Ms, 64, 64, (long long)n, lg.node_w1, 128, HID, nullptr, acc)) return rc;
+    if (int rc = gemm(gh, 64, 64, w.op_z, 64, 64, (long long)n, lg.node_w2, 64, 0, lg.node_b2, acc)) return rc;
+    cur = nxt;
+    gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
+  }
+  if (g_h_in) hipMemcpyAsync(g_h_in, gh, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (g_x_in) hipMemcpyAsync(g_x_in, gx, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (g_v_in) hipMemcpyAsync(g_v_in, gv, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  return check_launch("segno_backward");
 }
 
 }  // extern "C"

@@ -7,6 +7,10 @@ Semantics note: the reference's live ``forward`` (model
 discards the integrator result for a single input and returns its inputs. This class returns
 the integrator result (what the shadowed forward at model.py:28-51 and ``forward_step`` compute);
 ``bug_compat=True`` reproduces the reference's identity behaviour exactly.
+
+Training (train_nbody.py:168-179): in train mode with gradients enabled, the embedding Linear runs
+as a torch op and forward_step goes through autograd.SEGNOStepTrain (the HIP integrator forward
+with saved substeps and its hand-written reverse pass), so loss.backward() reaches every parameter.
 """
 import ctypes
 
@@ -88,7 +92,34 @@ class SEGNO(nn.Module):
         self.bug_compat = bug_compat
         self._blob = None
         self._blob_key = None
+        self._bblob = None
+        self._bblob_key = None
         self.to(device)
+
+    def gcl_param_names(self):
+        """Parameter names in nonode_layer_grads field order (vel_* = None: coord_mlp_vel is not on
+        the forward path, gcl.py:111-119)."""
+        pre = "module."
+        e, c, n = "edge_mlp", "coord_mlp", "node_mlp"
+        names = [pre + f"{mlp}.{k}.{wb}" for mlp in (e, c) for k in (0, 2) for wb in ("weight", "bias")]
+        return names + [None] * 4 + [pre + f"{n}.{k}.{wb}" for k in (0, 2) for wb in ("weight", "bias")]
+
+    def _packed_bwd(self):
+        """Backward fragments of the GCL (unscaled forward + transposed), rebuilt like _packed()."""
+        params = list(self.module.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._bblob is not None and key == self._bblob_key:
+            return self._bblob
+        L = _lib.lib()
+        bb = torch.empty(L.nonode_bwd_blob_floats(), dtype=torch.float32, device=self.embedding.weight.device)
+        w = self.module.weight_struct()
+        _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), _lib.VARIANT_SEGNO, self.hidden_nf, self.in_edge_nf,
+                                           _lib.ptr(bb), _lib.stream_of(bb)))
+        self._bblob, self._bblob_key = bb, key
+        return bb
+
+    def _training(self):
+        return self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     def _packed(self):
         params = list(self.module.parameters())
@@ -106,12 +137,13 @@ class SEGNO(nn.Module):
     def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
         """model.py:53-92 (single input). his [BN, in_node_nf], x, v [BN, 3], edges 2 x [E],
         edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T."""
-        self._check_trainable()
         if x.dim() == 3:
             return self._forward_multi(his, x, edges, v, edge_attr, int(T), in_steps)
         if self.bug_compat:
             # the live reference forward returns its inputs (and the embedded h)
             return x, self._embed(his), v
+        if self._training():
+            return self._step(self._embed(his), x, edges, v, edge_attr, int(T))
         return self._run(his, None, x, edges, v, edge_attr, int(T))
 
     def _forward_multi(self, his, x, edges, v, edge_attr, T, in_steps):
@@ -128,11 +160,11 @@ class SEGNO(nn.Module):
         _lib.require_device(his, x, v, edge_attr, self.embedding.weight)
         st = in_steps.tolist() if torch.is_tensor(in_steps) else list(in_steps)
         steps = [int(b) - int(a) for a, b in zip(st[:-1], st[1:])] + [int(T)]
-        with torch.no_grad():
+        with torch.set_grad_enabled(self._training()):
             h = self._embed(his.to(torch.float32))
             h_, x_, v_ = h[:, 0].contiguous(), x[:, 0].contiguous(), v[:, 0].contiguous()
             for i, step in enumerate(steps):
-                xi, hi, vi = self._run(None, h_, x_, edges, v_, edge_attr, step)
+                xi, hi, vi = self._step(h_, x_, edges, v_, edge_attr, step)
                 if i < len(steps) - 1:
                     if self.multiple_agg == "sum":
                         h_, x_, v_ = h[:, i + 1] + hi, x[:, i + 1] + xi, v[:, i + 1] + vi
@@ -150,26 +182,27 @@ class SEGNO(nn.Module):
 
     def forward_step(self, h, x, edges, v, edge_attr, T=10):
         """model.py:95-102: T substeps of the shared layer from an already-embedded h."""
-        self._check_trainable()
         self.module.n_layers = T
         self.n_layers = T
-        out = self._run(None, h, x, edges, v, edge_attr, int(T))
-        return out
+        return self._step(h, x, edges, v, edge_attr, int(T))
 
-    def _check_trainable(self):
-        """The fused integrator has no reverse pass yet: in train mode with gradients enabled the
-        outputs could not carry a gradient, so say so instead of returning detached tensors (the
-        reference fails later, at train_nbody.py:178, with "does not require grad")."""
-        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) \
-                and not self.bug_compat:
-            raise RuntimeError("SEGNO (MI355X kernels): training through the fused integrator "
-                               "(train_nbody.py:168-179) is not implemented; call model.eval() or run "
-                               "under torch.no_grad() for inference")
+    def _step(self, h, x, edges, v, edge_attr, T):
+        """forward_step from an embedded h: on the autograd tape in training, else the fused
+        inference launch."""
+        if not self._training():
+            return self._run(None, h, x, edges, v, edge_attr, T)
+        _lib.require_device(h, x, v, edge_attr, self.embedding.weight)
+        B, N = check_full_graph(edges, x.shape[0])
+        if edge_attr.shape != (B * N * (N - 1), self.in_edge_nf):
+            raise ValueError(f"edge_attr must be [{B * N * (N - 1)}, {self.in_edge_nf}]")
+        from .autograd import segno_step_train
+        return segno_step_train(self, h, x, v, edge_attr, T, B, N)
 
     def _embed(self, his):
+        """SEGNO.embedding (model.py:73): a torch op on the device, so it is on the autograd tape
+        in training."""
         _lib.require_device(his, self.embedding.weight)
-        with torch.no_grad():
-            return torch.nn.functional.linear(his, self.embedding.weight, self.embedding.bias)
+        return torch.nn.functional.linear(his.to(torch.float32), self.embedding.weight, self.embedding.bias)
 
     @torch.no_grad()
     def _run(self, his, h_in, x, edges, v, edge_attr, T):

@@ -32,6 +32,9 @@ What each fixture pins (reference file:line):
   segno_multi.npz     SEGNO live forward with num_inputs=3, multiple_agg='attn' (model.py:53-92,
                       104-139) and the discarded last forward_step; segno_multi_rollout.npz: the
                       2-segment num_prev = 3 rollout_fn through the integrator.
+  segno_grad.npz      one SEGNO training step of run_epoch (train_nbody.py:150-178, num_inputs=1)
+                      routed through forward_step (model.py:95-102, the integrator): criterion =
+                      nn.MSELoss (train_nbody.py:31), loss and every parameter gradient, T=10.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
                       torch.manual_seed(0) (RNG-consumption order of the constructors).
 """
@@ -298,6 +301,45 @@ def make_segno(B=4, N=20, T=10):
         "out::loc_preds": _np(preds), "out::energies": _np(energies)})
 
 
+def make_segno_grad(B=4, N=20, T=10):
+    """One training step (train_nbody.py:150-178) through forward_step. The live forward returns
+    its inputs, so loss.backward() on it fails in the reference; the
+    gradients recorded here are those of the integrator the shadowed forward intends."""
+    loc_all, vel_all, q = charged_trajectories(B, N, seed=45)
+    start = 20
+    edges = full_edges(B, N)
+    rows, cols = edges
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start])).reshape(-1, 3)
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start])).reshape(-1, 3)
+    loc_end = torch.tensor(np.ascontiguousarray(loc_all[:, start + T])).reshape(-1, 3)
+    charges = torch.tensor(q).reshape(-1, 1)
+    prod = charges[rows] * charges[cols]
+    h = torch.sqrt(torch.sum(vel ** 2, dim=1)).unsqueeze(-1)                     # train_nbody.py:121
+    loc_dist = torch.sum((loc[rows] - loc[cols]) ** 2, 1).unsqueeze(1)
+    edge_attr = torch.cat([prod, loc_dist], 1)                                     # train_nbody.py:123
+    torch.manual_seed(1)
+    model = SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True,
+                  norm_diff=False, tanh=False, device="cpu", varDT=False, multiple_agg=None)
+    model.train()
+    model.zero_grad()
+    edge_index = torch.stack(edges)
+    hh = model.embedding(h)
+    x_pred, h_pred, v_pred = model.forward_step(hh, loc.detach(), edge_index, vel.detach(), edge_attr, T=T)
+    loss = torch.nn.MSELoss()(x_pred, loc_end)
+    loss.backward()
+    fx = dict(_sd(model))
+    fx.update({
+        "cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T),
+        "in::x": _np(loc), "in::v": _np(vel), "in::his": _np(h), "in::edge_attr": _np(edge_attr),
+        "in::row": _np(rows), "in::col": _np(cols), "in::loc_end": _np(loc_end),
+        "out::x": _np(x_pred.detach()), "out::loss": np.array(float(loss.detach())),
+    })
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            fx["grad::" + k] = _np(p.grad)
+    np.savez_compressed(os.path.join(HERE, "segno_grad.npz"), **fx)
+
+
 def make_segno_gravity(B=2, N=100, T=5):
     rng = np.random.RandomState(7)
     # GravitySim init (synthetic_sim.py:370-378): masses, positions, velocities, COM removed
@@ -502,6 +544,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if sys.argv[1:] == ["egno_m5"]:
         make_egno_modes()
+        sys.exit(0)
+    if sys.argv[1:] == ["segno_grad"]:
+        make_segno_grad()
         sys.exit(0)
     if sys.argv[1:] == ["egno_multi"]:
         make_egno_multi()

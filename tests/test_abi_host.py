@@ -111,16 +111,19 @@ def test_unsupported_configs_raise():
         pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, multiple_agg="max")
 
 
-def test_segno_train_mode_raises_clearly():
-    """Until the fused integrator has a reverse pass, train mode with grad enabled must not return
-    silently detached outputs (train_nbody.py:168-179 would fail later with a generic message)."""
+def test_segno_train_mode_has_no_cpu_path():
+    """Training goes through the HIP reverse pass (autograd.SEGNOStepTrain); on CPU tensors both
+    the training and the inference path stop at the device check (no silent CPU fallback)."""
     m = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True).train()
     z = torch.zeros(20, 3)
-    with pytest.raises(RuntimeError, match="not implemented"):
+    with pytest.raises(pkg.NonodeError, match="no CPU path"):
         m(torch.zeros(20, 1), z, pkg.graph.full_edges(1, 20), z, torch.zeros(380, 2), T=10)
-    with pytest.raises(pkg.NonodeError, match="no CPU path"):   # eval mode gets as far as the device check
+    with pytest.raises(pkg.NonodeError, match="no CPU path"):
         with torch.no_grad():
             m(torch.zeros(20, 1), z, pkg.graph.full_edges(1, 20), z, torch.zeros(380, 2), T=10)
+    assert [n for n in m.gcl_param_names() if n] == [k for k, _ in m.module.named_parameters(prefix="module")
+                                                      if "coord_mlp_vel" not in k and "node_mlp" not in k] + \
+        [k for k, _ in m.module.named_parameters(prefix="module") if "node_mlp" in k]
 
 
 def test_no_cpu_fallback():

@@ -64,6 +64,30 @@ def test_egno_autograd_gradients_match_reference():
             assert maxnorm_rel(t.grad.numpy(), ref) < 1e-5, k
 
 
+def test_segno_autograd_gradients_match_reference():
+    """One SEGNO training step (train_nbody.py:150-178 through forward_step, nn.MSELoss): loss and
+    every parameter gradient of torch autograd through the restatement, in float32 against the
+    reference's own autograd (segno_grad.npz) and in float64 (the bar the GPU test uses)."""
+    gd = load_golden("segno_grad")
+    T = int(gd["cfg::T"])
+    for dt, tol in ((torch.float32, 1e-5), (torch.float64, 1e-5)):
+        p = {k: torch.tensor(v, dtype=dt, requires_grad=True) for k, v in params_of(gd).items()}
+        t = lambda k: torch.tensor(gd[k]).to(dt) if gd[k].dtype.kind == "f" else torch.tensor(gd[k])  # noqa: E731
+        x, _, _ = tr.segno_forward_step(p, t("in::his"), t("in::x"), t("in::row"), t("in::col"), t("in::v"),
+                                        t("in::edge_attr"), T=T, dense_mean=False)
+        loss = torch.nn.functional.mse_loss(x, t("in::loc_end"))
+        loss.backward()
+        assert abs(float(loss.detach()) - float(gd["out::loss"])) <= 1e-6 * abs(float(gd["out::loss"]))
+        n = 0
+        for k, q in p.items():
+            if "grad::" + k not in gd:
+                assert q.grad is None or float(q.grad.abs().max()) == 0, k   # coord_mlp_vel
+                continue
+            n += 1
+            assert maxnorm_rel(q.grad.double().numpy(), gd["grad::" + k]) < tol, (dt, k)
+        assert n == 14
+
+
 def test_segno_forward_step_dense_and_scatter():
     fx = load_golden("segno_fwd")
     p = _p(fx)
