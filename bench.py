@@ -169,6 +169,11 @@ def device_info(dev):
     p = torch.cuda.get_device_properties(dev)
     info = {"name": p.name, "arch": getattr(p, "gcnArchName", None), "cus": p.multi_processor_count,
             "hbm_gib": round(p.total_memory / 2 ** 30, 1)}
+    if "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        # under rocprofv3 every child process carries its preload (which initialises the GPU) and
+        # rocm-smi is a script that re-execs its interpreter: skip it there
+        info["smi"] = "skipped under rocprofv3"
+        return info
     try:
         r = subprocess.run(["rocm-smi", "--showclocks", "--showcomputepartition", "--showmemorypartition",
                             "--showpower", "--json"], capture_output=True, text=True, timeout=20)
