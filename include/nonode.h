@@ -345,17 +345,23 @@ int nonode_sim_gravity(int S, int N, int T, int sample_freq, double dt, double G
 
 /* ---- dataset -> device batches ---- */
 
-/* One batch of NBodyDynamicsDataset (EGNO/simulation/dataset_simple.py:122-178, num_inputs == 1)
- * gathered from a split resident on the device: loc, vel [S][Tf][N][3] (the .npy trajectories in
+/* One batch of NBodyDynamicsDataset (EGNO/simulation/dataset_simple.py:122-178) gathered from a
+ * split resident on the device: loc, vel [S][Tf][N][3] (the .npy trajectories in
  * [sample][frame][node][xyz] order), charges [S][N], edge_attr_src [S][N*(N-1)] (the loader's q_i q_j
- * in the reference edge order, dataset_simple.py:46-72); batch row b is sample idx[b] with input
- * frame frame0[b] and target frames out_idx[b][0..To). Writes loc0, vel0 [B][N][3],
- * charges_out [B][N], edge_attr [B][N*(N-1)] and loc_true [B][N][To][3] (locs_out). Index arrays
- * are device int32. */
-int nonode_gather_batch(int S, int Tf, int N, int B, int To, const float* loc, const float* vel,
+ * in the reference edge order, dataset_simple.py:46-72); batch row b is sample idx[b] with the I
+ * input frames frame0[b][0..I) (num_inputs, dataset_simple.py:133-148; I = 1 for a single input) and
+ * target frames out_idx[b][0..To). Writes loc0, vel0 [B][I][N][3], charges_out [B][N],
+ * edge_attr [B][N*(N-1)] and loc_true [B][N][To][3] (locs_out). Index arrays are device int32 and
+ * must be in range (the Python loader checks them). */
+int nonode_gather_batch(int S, int Tf, int N, int B, int I, int To, const float* loc, const float* vel,
                         const float* charges, const float* edge_attr_src, const int* idx, const int* frame0, const int* out_idx,
                         float* loc0, float* vel0, float* charges_out, float* edge_attr, float* loc_true,
                         void* stream);
+
+/* dst[b][0..K) = src[idx[b]][0..K) for b < B: whole samples of a device-resident split
+ * (SEGNO/dataset_nbody.py:82-86 __getitem__ + default_collate; one launch per array). src, dst
+ * 16-byte aligned; idx device int32 in [0, S). */
+int nonode_gather_rows(int S, long long K, int B, const float* src, const int* idx, float* dst, void* stream);
 
 
 /* ---- rollout metrics ---- */

@@ -21,7 +21,7 @@ SYMBOLS = (
     "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
     "nonode_egno_forward_train", "nonode_egno_backward_workspace_bytes", "nonode_egno_backward",
     "nonode_segno_train_state_bytes", "nonode_segno_forward_train", "nonode_segno_backward_workspace_bytes",
-    "nonode_segno_backward",
+    "nonode_segno_backward", "nonode_gather_rows",
     "nonode_egno_forward_train_frames", "nonode_egno_backward_frames",
     "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
     "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout", "nonode_sim_charged", "nonode_sim_gravity",
@@ -121,7 +121,8 @@ def lib():
     _d = ctypes.c_double
     L.nonode_sim_charged.argtypes = [_i] * 4 + [_d] * 3 + [_vp] * 6
     L.nonode_sim_gravity.argtypes = [_i] * 4 + [_d] * 3 + [_vp] * 7
-    L.nonode_gather_batch.argtypes = [_i] * 5 + [_vp] * 13
+    L.nonode_gather_batch.argtypes = [_i] * 6 + [_vp] * 13
+    L.nonode_gather_rows.argtypes = [_i, ctypes.c_longlong, _i, _vp, _vp, _vp, _vp]
     L.nonode_rollout_metrics.argtypes = [_i] * 3 + [_vp] * 5
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]

@@ -9,14 +9,14 @@
 namespace {
 
 struct GatherArgs {
-  int S, Tf, N, To;
+  int S, Tf, N, To, I;
   const float* loc; const float* vel;   // [S][Tf][N][3]
   const float* q;                       // [S][N]
   const float* ea_src;                  // [S][N*(N-1)] q_i q_j per sample
   const int* idx;                       // [B] sample of each batch row
-  const int* frame0;                    // [B] input frame
+  const int* frame0;                    // [B][I] input frames
   const int* out_idx;                   // [B][To] target frames
-  float* loc0; float* vel0;             // [B][N][3]
+  float* loc0; float* vel0;             // [B][I][N][3]
   float* q_out;                         // [B][N]
   float* edge_attr;                     // [B][N*(N-1)] = q_i q_j in (i, j != i) order
   float* loc_true;                      // [B][N][To][3]
@@ -28,10 +28,11 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(GatherArgs a) {
   const float* L = a.loc + (size_t)s * a.Tf * N * 3;
   const float* V = a.vel + (size_t)s * a.Tf * N * 3;
   const float* q = a.q + (size_t)s * N;
-  const int f0 = a.frame0[b];
-  for (int k = tid; k < N * 3; k += 256) {
-    a.loc0[(size_t)b * N * 3 + k] = L[(size_t)f0 * N * 3 + k];
-    a.vel0[(size_t)b * N * 3 + k] = V[(size_t)f0 * N * 3 + k];
+  for (int k = tid; k < a.I * N * 3; k += 256) {
+    const int i = k / (N * 3), r = k - i * N * 3;
+    const int f0 = a.frame0[(size_t)b * a.I + i];
+    a.loc0[(size_t)b * a.I * N * 3 + k] = L[(size_t)f0 * N * 3 + r];
+    a.vel0[(size_t)b * a.I * N * 3 + k] = V[(size_t)f0 * N * 3 + r];
   }
   for (int n = tid; n < N; n += 256) a.q_out[(size_t)b * N + n] = q[n];
   const int Nm1 = N - 1;
@@ -45,19 +46,44 @@ __global__ __launch_bounds__(256) void gather_batch_kernel(GatherArgs a) {
   }
 }
 
+// dst[b][k] = src[idx[b]][k], rows of K floats (float4 when K % 4 == 0)
+__global__ __launch_bounds__(256) void gather_rows_kernel(long long K, const float* src, const int* idx, float* dst) {
+  const int b = blockIdx.y;
+  const float* sr = src + (size_t)idx[b] * K;
+  float* dr = dst + (size_t)b * K;
+  const long long step = (long long)gridDim.x * 256;
+  if ((K & 3) == 0) {
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < K / 4; k += step)
+      reinterpret_cast<f4*>(dr)[k] = reinterpret_cast<const f4*>(sr)[k];
+  } else {
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < K; k += step) dr[k] = sr[k];
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
-int nonode_gather_batch(int S, int Tf, int N, int B, int To, const float* loc, const float* vel, const float* charges,
+int nonode_gather_rows(int S, long long K, int B, const float* src, const int* idx, float* dst, void* stream) {
+  if (S <= 0 || K <= 0 || B <= 0) return fail(NONODE_EINVAL, "gather_rows: S=%d K=%lld B=%d", S, K, B);
+  if (!src || !idx || !dst) return fail(NONODE_EINVAL, "gather_rows: null pointer");
+  if (((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) return fail(NONODE_EINVAL, "gather_rows: 16-byte alignment");
+  const long long per = (K & 3) == 0 ? K / 4 : K;
+  long long gx = (per + 255) / 256;
+  gx = gx < 64 ? gx : 64;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)gx, B), dim3(256), 0, (hipStream_t)stream, K, src, idx, dst);
+  return check_launch("gather_rows_kernel");
+}
+
+int nonode_gather_batch(int S, int Tf, int N, int B, int I, int To, const float* loc, const float* vel, const float* charges,
                         const float* edge_attr_src, const int* idx, const int* frame0, const int* out_idx, float* loc0, float* vel0,
                         float* charges_out, float* edge_attr, float* loc_true, void* stream) {
-  if (S <= 0 || Tf <= 0 || N < 2 || B <= 0 || To < 0)
-    return fail(NONODE_EINVAL, "gather_batch: S=%d Tf=%d N=%d B=%d To=%d", S, Tf, N, B, To);
+  if (S <= 0 || Tf <= 0 || N < 2 || B <= 0 || I < 1 || To < 0)
+    return fail(NONODE_EINVAL, "gather_batch: S=%d Tf=%d N=%d B=%d I=%d To=%d", S, Tf, N, B, I, To);
   if (!loc || !vel || !charges || !edge_attr_src || !idx || !frame0 || (To > 0 && (!out_idx || !loc_true)) || !loc0 || !vel0 ||
       !charges_out || !edge_attr)
     return fail(NONODE_EINVAL, "gather_batch: null pointer");
-  GatherArgs a{S, Tf, N, To, loc, vel, charges, edge_attr_src, idx, frame0, out_idx, loc0, vel0, charges_out, edge_attr, loc_true};
+  GatherArgs a{S, Tf, N, To, I, loc, vel, charges, edge_attr_src, idx, frame0, out_idx, loc0, vel0, charges_out, edge_attr, loc_true};
   hipLaunchKernelGGL(gather_batch_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("gather_batch_kernel");
 }

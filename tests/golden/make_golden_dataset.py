@@ -1,5 +1,8 @@
 """Generate tests/golden/nbody_tiny/ (.npy splits in the reference's on-disk format),
-tests/golden/dataset_items.npz (what the REFERENCE loader returns for them) and
+tests/golden/dataset_items.npz (what the REFERENCE loaders return for them: EGNO's
+NBodyDynamicsDataset with num_inputs = 1 and 3 (equispaced and varDT inputs), SEGNO's NBodyDataset
+(SEGNO/dataset_nbody.py:7-94) and the model inputs SEGNO's run_epoch builds from its batches,
+train_nbody.py:76-123, with num_inputs = 1 and 3) and
 tests/golden/metrics.npz (the reference's pearson_correlation_batch, utils.py:261-321, on
 synthetic prediction / truth pairs).
 
@@ -33,6 +36,9 @@ tg.utils.to_dense_batch = lambda x, b: (x, None)
 tg.data = types.ModuleType("torch_geometric.data")
 tg.data.Data = dict
 sys.modules.update({"torch_geometric": tg, "torch_geometric.utils": tg.utils, "torch_geometric.data": tg.data})
+wandb = types.ModuleType("wandb")
+wandb.log = lambda *a, **k: None
+sys.modules["wandb"] = wandb
 sys.path.insert(0, REF)
 sys.path.insert(0, os.path.join(REF, "EGNO", "simulation"))
 import synthetic_sim  # noqa: E402
@@ -74,6 +80,75 @@ def items(dataset):
     return d
 
 
+def items_multi(dataset, var_dt, seed):
+    """num_inputs = 3 items; varDT draws random_ascending_tensor (torch.randperm) per item."""
+    d = {}
+    torch.manual_seed(seed)
+    with contextlib.redirect_stdout(io.StringIO()):
+        ds = NBodyDynamicsDataset("train", data_dir=OUT, dataset=dataset, dataset_name="nbody_small", n_balls=5,
+                                  num_timesteps=10, num_inputs=3, traj_len=1, varDT=var_dt)
+    tag = f"{dataset}::multi{int(var_dt)}"
+    d[f"{tag}::seed"] = seed
+    for i in range(len(ds)):
+        loc, vel, ea, q, locs_out, f0, out_idx = ds[i]
+        for k, v in (("loc", loc), ("vel", vel), ("locs_out", locs_out), ("frame_0", f0), ("out_indices", out_idx)):
+            d[f"{tag}::{i}::{k}"] = v.numpy() if torch.is_tensor(v) else np.asarray(v)
+    return d
+
+
+def segno_items_and_inputs():
+    """SEGNO NBodyDataset items, and the inputs run_epoch (train_nbody.py:57-123) feeds the model
+    and the criterion for every batch of a non-shuffled DataLoader (batch_size 3, drop_last as
+    train_nbody.py:23 uses; the reference cannot featurise a short last batch), recorded with a
+    stub model."""
+    import types as _t
+    from torch.utils.data import DataLoader
+    sys.path.insert(0, os.path.join(REF, "SEGNO"))
+    import dataset_nbody  # noqa: E402
+    import train_nbody  # noqa: E402
+    d = {}
+    for dataset in ("charged", "gravity"):
+        ds = dataset_nbody.NBodyDataset(OUT, partition="train", dataset=dataset, dataset_size="small", n_balls=5)
+        d[f"segno_{dataset}::len"] = len(ds)
+        d[f"segno_{dataset}::start"] = ds.start
+        for i in range(len(ds)):
+            for k, v in zip(("loc", "vel", "edge_attr", "charges"), ds[i]):
+                d[f"segno_{dataset}::{i}::{k}"] = v.numpy()
+
+    class Rec(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.calls = []
+
+        def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
+            self.calls.append({"h": his, "x": x, "v": v, "edge_attr": edge_attr,
+                               "in_steps": in_steps if in_steps is not None else torch.zeros(0)})
+            return (x[:, -1] if x.dim() == 3 else x), his, v
+
+    for dataset in ("charged", "gravity"):
+        for ni, var_dt in ((1, False), (3, False), (3, True)):
+            ds = dataset_nbody.NBodyDataset(OUT, partition="train", dataset=dataset, dataset_size="small", n_balls=5)
+            rec, ends = Rec(), []
+
+            def crit(a, b):
+                ends.append(b)
+                return ((a - b) ** 2).mean()
+
+            args = _t.SimpleNamespace(device="cpu", varDT=var_dt, batch_size=3, num_inputs=ni, traj_len=1)
+            np.random.seed(7)
+            with contextlib.redirect_stdout(io.StringIO()):
+                train_nbody.run_epoch(rec, None, crit, 0, DataLoader(ds, batch_size=3, shuffle=False, drop_last=True), args,
+                                      backprop=False, num_timesteps=10)
+            tag = f"segno_{dataset}::in{ni}_{int(var_dt)}"
+            d[f"{tag}::np_seed"] = 7
+            d[f"{tag}::batches"] = len(rec.calls)
+            for k, c in enumerate(rec.calls):
+                for name, v in c.items():
+                    d[f"{tag}::{k}::{name}"] = v.detach().numpy()
+                d[f"{tag}::{k}::loc_end"] = ends[k].detach().numpy()
+    return d
+
+
 def metrics():
     g = torch.Generator().manual_seed(5)
     T, B, N = 20, 4, 5
@@ -92,5 +167,9 @@ if __name__ == "__main__":
     fx = {}
     fx.update(items("charged"))
     fx.update(items("gravity"))
+    for ds_name in ("charged", "gravity"):
+        fx.update(items_multi(ds_name, False, 11))
+        fx.update(items_multi(ds_name, True, 12))
+    fx.update(segno_items_and_inputs())
     np.savez_compressed(os.path.join(HERE, "dataset_items.npz"), **fx)
     print("wrote nbody_tiny/ and dataset_items.npz")

@@ -33,5 +33,35 @@ def test_max_samples_and_edges():
     assert len(ds) == 3 and ds.get_n_nodes() == 49
     r, c = ds.get_edges(2, 5)
     assert r.numel() == 2 * 20 and int(r[20]) == 5 and int(c[0]) == 1
-    with pytest.raises(NotImplementedError):
-        NBodyDynamicsDataset("train", data_dir=TINY, dataset="charged", n_balls=5, num_inputs=2)
+
+
+@pytest.mark.parametrize("dataset", ["charged", "gravity"])
+@pytest.mark.parametrize("var_dt", [False, True])
+def test_multi_input_items_equal_reference_loader(dataset, var_dt):
+    """num_inputs = 3 (dataset_simple.py:133-164): equispaced inputs, and varDT offsets drawn by
+    random_ascending_tensor in the reference's order (torch seeded as when recorded)."""
+    g = load_golden("dataset_items")
+    tag = f"{dataset}::multi{int(var_dt)}"
+    torch.manual_seed(int(g[f"{tag}::seed"]))
+    ds = NBodyDynamicsDataset("train", data_dir=TINY, dataset=dataset, dataset_name="nbody_small", n_balls=5,
+                              num_timesteps=10, num_inputs=3, varDT=var_dt)
+    for i in range(len(ds)):
+        loc, vel, _, _, locs_out, f0, oi = ds[i]
+        for k, v in (("loc", loc), ("vel", vel), ("locs_out", locs_out), ("frame_0", f0), ("out_indices", oi)):
+            want = g[f"{tag}::{i}::{k}"]
+            assert v.shape == want.shape and np.array_equal(v.numpy(), want), (tag, i, k)
+
+
+@pytest.mark.parametrize("dataset", ["charged", "gravity"])
+def test_segno_items_equal_reference_loader(dataset):
+    """SEGNO/dataset_nbody.py:7-94 items (whole trajectories, interaction-matrix edge features)."""
+    from no_node_comparison_amd.dataset import NBodyDataset
+    g = load_golden("dataset_items")
+    ds = NBodyDataset(TINY, partition="train", dataset=dataset, dataset_size="small", n_balls=5)
+    assert len(ds) == int(g[f"segno_{dataset}::len"]) and ds.start == int(g[f"segno_{dataset}::start"])
+    for i in range(len(ds)):
+        for k, v in zip(("loc", "vel", "edge_attr", "charges"), ds[i]):
+            want = g[f"segno_{dataset}::{i}::{k}"]
+            assert v.shape == want.shape and np.array_equal(v.numpy(), want), (dataset, i, k)
+    r, c = ds.get_edges(3, 5)
+    assert r.numel() == 60 and int(r[20]) == 5 and int(c[0]) == 1

@@ -1,4 +1,5 @@
-"""Device batches (nonode_gather_batch) equal the reference loader's items collated."""
+"""Device batches (nonode_gather_batch / nonode_gather_rows) equal the reference loaders' items collated, and
+segno_batch_inputs equals the model inputs the reference run_epoch builds."""
 import os
 
 import numpy as np
@@ -42,3 +43,79 @@ def test_prepare_inputs_on_device_batch():
                             q.cpu().numpy())
     for got, want in zip((x, v, eattr, nodes, lm), ref):
         np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("dataset,var_dt", [("charged", False), ("charged", True), ("gravity", True)])
+def test_multi_input_device_batches_equal_collated_items(dataset, var_dt):
+    """num_inputs = 3: loc / vel [B, 3, N, 3], frame_0 [B, 3]; with varDT the loader draws each
+    sample's input offsets in batch order, as the reference's __getitem__ calls do."""
+    from tests.conftest import load_golden
+    g = load_golden("dataset_items")
+    tag = f"{dataset}::multi{int(var_dt)}"
+    ds = NBodyDynamicsDataset("train", data_dir=TINY, dataset=dataset, n_balls=5, num_timesteps=10, num_inputs=3,
+                              varDT=var_dt)
+    torch.manual_seed(int(g[f"{tag}::seed"]))
+    dl = DeviceLoader(ds, batch_size=2)
+    i = 0
+    for batch in dl:
+        loc, vel, ea, q, lt, f0, oi = batch
+        assert loc.shape == (2, 3, 5, 3) and f0.shape == (2, 3)
+        for b in range(2):
+            for c, k in ((loc, "loc"), (vel, "vel"), (lt, "locs_out"), (f0, "frame_0"), (oi, "out_indices")):
+                want = g[f"{tag}::{i}::{k}"]
+                assert np.array_equal(c[b].cpu().numpy(), want.astype(c.cpu().numpy().dtype)), (i, k)
+            i += 1
+    assert i == len(ds)
+
+
+def test_device_loader_rejects_out_of_range_indices():
+    ds = NBodyDynamicsDataset("train", data_dir=TINY, dataset="charged", n_balls=5, num_timesteps=10)
+    dl = DeviceLoader(ds, batch_size=2)
+    with pytest.raises(IndexError):
+        dl.batch([0, len(ds)])
+    with pytest.raises(IndexError):
+        dl.batch([-1])
+
+
+@pytest.mark.parametrize("dataset", ["charged", "gravity"])
+def test_segno_device_batches_equal_collated_items(dataset):
+    from no_node_comparison_amd.dataset import NBodyDataset, SegnoDeviceLoader
+    ds = NBodyDataset(TINY, partition="train", dataset=dataset, dataset_size="small", n_balls=5)
+    dl = SegnoDeviceLoader(ds, batch_size=3, shuffle=True, generator=torch.Generator().manual_seed(1))
+    order = torch.randperm(len(ds), generator=torch.Generator().manual_seed(1))
+    seen = []
+    for k, batch in enumerate(dl):
+        idx = order[k * 3:(k + 1) * 3].tolist()
+        seen += idx
+        for c, got in enumerate(batch):
+            want = torch.stack([ds[i][c] for i in idx])
+            assert got.is_cuda and torch.equal(got.cpu(), want), c
+    assert sorted(seen) == list(range(len(ds)))
+    with pytest.raises(IndexError):
+        dl.batch([len(ds)])
+
+
+@pytest.mark.parametrize("dataset", ["charged", "gravity"])
+@pytest.mark.parametrize("ni,var_dt", [(1, False), (3, False), (3, True)])
+def test_segno_batch_inputs_equal_reference_run_epoch(dataset, ni, var_dt):
+    """segno_batch_inputs reproduces what the reference run_epoch feeds the model and the criterion
+    (train_nbody.py:76-123, recorded by make_golden_dataset.py with a stub model; numpy seeded as
+    there for the varDT gap draws)."""
+    from no_node_comparison_amd.dataset import NBodyDataset, SegnoDeviceLoader, segno_batch_inputs
+    from tests.conftest import load_golden
+    g = load_golden("dataset_items")
+    tag = f"segno_{dataset}::in{ni}_{int(var_dt)}"
+    ds = NBodyDataset(TINY, partition="train", dataset=dataset, dataset_size="small", n_balls=5)
+    dl = SegnoDeviceLoader(ds, batch_size=3, drop_last=True)
+    rng = np.random.RandomState(int(g[f"{tag}::np_seed"]))
+    n = 0
+    for k, batch in enumerate(dl):
+        h, loc, vel, ea, loc_end, in_steps, _ = segno_batch_inputs(batch, ds.start, 10, ni, var_dt, rng=rng)
+        for got, name in ((h, "h"), (loc, "x"), (vel, "v"), (ea, "edge_attr"), (loc_end, "loc_end")):
+            want = g[f"{tag}::{k}::{name}"]
+            assert tuple(got.shape) == want.shape, name
+            np.testing.assert_allclose(got.cpu().numpy(), want, rtol=2e-7, atol=1e-7, err_msg=name)
+        if ni > 1:
+            assert np.array_equal(in_steps.cpu().numpy(), g[f"{tag}::{k}::in_steps"])
+        n += 1
+    assert n == int(g[f"{tag}::batches"])
