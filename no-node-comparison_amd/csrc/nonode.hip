@@ -364,7 +364,7 @@ __device__ __forceinline__ void load_vp(f4 (&d)[4], const float* vp, int g) {
 // SiLU of the 16 ECL values, with the add / multiply as packed f32 ops (one wave per SIMD issues
 // a v_pk_* at the cost of a plain VALU op)
 #ifndef NONODE_PK_SILU
-#define NONODE_PK_SILU 1
+#define NONODE_PK_SILU 0   // packed f32 SiLU add / multiply: 1.8% slower beside the MFMAs (C2 layer 252 vs 247.5 us)
 #endif
 __device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
   if (!NONODE_PK_SILU) {
@@ -674,9 +674,18 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         mfma_h16(ap, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), xh, xl, lane);
         mfma_h16(aq, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), xh, xl, lane);
       }
+      // input-finiteness flag of the node (sX slot 3): the edge guard only recomputes pairs whose
+      // inputs are finite (a non-finite state, e.g. a diverged rollout, cannot be helped)
+      float sa = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sa += fabsf(ap[mt][q]) + fabsf(aq[mt][q]);
+      sa = group_sum(sa);
       if (valid) {
         store_ecl(sP + local * ROWP, ap, g);
         store_ecl(sQ + local * ROWP, aq, g);
+        if (g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;
       }
       return;
     }
@@ -697,7 +706,14 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     }
     mm64(acc, reinterpret_cast<const h8*>(blob + OFF_H16N + (isP ? H_WA : H_WB) * 4096),
          blob + (isP ? OFF_WA : OFF_WB), hin, lane);
+    float sa = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sa += fabsf(acc[mt][q]);
+    sa = group_sum(sa);
     if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
+    if (valid && !isP && g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;   // sender flag
   };
   auto load_sx = [&](const float* __restrict__ xI, int s0, int S) __attribute__((always_inline)) {
     for (int i = tid; i < S * 3; i += NW * 64) {
@@ -775,6 +791,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         const float* vFEAT = vFEAT_ + voff;
         const float* Prow = sP + rl * ROWP;            // re-read per unit (saves 16 live VGPRs)
         const float xr0 = sX[(sb + n) * 4 + 0], xr1 = sX[(sb + n) * 4 + 1], xr2 = sX[(sb + n) * 4 + 2];
+        const float xr3 = sX[(sb + n) * 4 + 3];   // the receiver's input-finiteness flag
         f4 msum[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) msum[mt] = f4{0.f, 0.f, 0.f, 0.f};
@@ -843,14 +860,15 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           // other unit's SiLU work.
           f4 pr[4];
           load_ecl(pr, Prow, g);                       // receiver projection, fixed for the segment
-          auto head2 = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2)
-              __attribute__((always_inline)) {
+          auto head2 = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2,
+                           bool& ok) __attribute__((always_inline)) {
             int j = n + k;
             j = (j >= N) ? j - N : j;
             const int sl = sb + j;
-            const float* xs = sX + sl * 4;
+            const f4 xs = *reinterpret_cast<const f4*>(sX + sl * 4);
             r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
             const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+            ok = xs[3] * xr3 != 0.f && __builtin_isfinite(d2);   // finite inputs: a guard recompute can help
             load_ecl(a, sQ + sl * ROWP, g);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
@@ -863,10 +881,10 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               for (int mo = 0; mo < 4; ++mo) a[mo] = mfma(wf[mo], bv, a[mo]);
             }
           };
-          auto edge_f = [&](f4 (&c1)[4], float r0, float r1, float r2, float& f0, float& f1, float& f2)
-              __attribute__((always_inline)) {
+          auto edge_f = [&](f4 (&c1)[4], float r0, float r1, float r2, float& f0, float& f1, float& f2,
+                            float& c) __attribute__((always_inline)) {
             silu_ecl(c1);
-            const float c = dot_r(c1, rWC2) + bc2;
+            c = dot_r(c1, rWC2) + bc2;
             f0 = r0 * c; f1 = r1 * c; f2 = r2 * c;
             if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
               f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -879,7 +897,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               __attribute__((always_inline)) {
             f4 a[4], c[4];
             float r0, r1, r2;
-            head2(k, ev, a, r0, r1, r2);
+            bool ok;
+            head2(k, ev, a, r0, r1, r2, ok);
             silu_ecl(a);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
@@ -888,7 +907,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
             mm64_scaled(c, wc1h, m, lane);
-            edge_f(c, r0, r1, r2, f0, f1, f2);
+            float cc;
+            edge_f(c, r0, r1, r2, f0, f1, f2, cc);
           };
           float e0[KF], e1[KF];
           fetch_ef(k, e0);
@@ -907,7 +927,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             float r00, r01, r02, r10, r11, r12;
             float f00, f01, f02, f10, f11, f12;
             f4 pm[4];
-            float gmax;
+            float cA, cB;   // coordinate-MLP outputs: non-finite iff an fp16 hi part overflowed
+            bool okA, okB;  // finite inputs (node flags, |r|^2)
             if constexpr (kStagger<VARIANT>) {
             // The two units run half a stage apart, so every MFMA block of one unit has the other
             // unit's VALU stage (gathers, SiLU, fp16 split) beside it in program order:
@@ -915,32 +936,28 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             // (one wave per SIMD has no other wave to fill the matrix-pipe shadow).
             {
               H16Frags fw2, fwc1;
-              head2(k, e0, a0, r00, r01, r02);
+              head2(k, e0, a0, r00, r01, r02, okA);
               STAMP(0);
               silu_ecl(a0);
-              gmax = amax_ecl(a0);
               h8 xh0[2], xl0[2], xh1[2], xl1[2];
               h16_split(a0, xh0, xl0);
               load_h16frags(fw2, w2l, lane);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) m0[mt] = rB2[mt];
               mfma_h16r(m0, fw2, xh0, xl0);                       // W2(A)
-              head2(k + 1, e1, a1, r10, r11, r12);                // | head + SiLU + split (B)
+              head2(k + 1, e1, a1, r10, r11, r12, okB);           // | head + SiLU + split (B)
               silu_ecl(a1);
-              gmax = fmaxf(gmax, amax_ecl(a1));
               h16_split(a1, xh1, xl1);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) m1[mt] = rB2[mt];
               mfma_h16r(m1, fw2, xh1, xl1);                       // W2(B)
               load_h16frags(fwc1, wc1l, lane);
               silu_ecl(m0);                                       // | SiLU + split (m_A)
-              gmax = fmaxf(gmax, amax_ecl(m0));
               h16_split(m0, xh0, xl0);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) a0[mt] = rBC1[mt];
               mfma_h16r(a0, fwc1, xh0, xl0);                      // Wc1(A)
               silu_ecl(m1);                                       // | SiLU + split (m_B)
-              gmax = fmaxf(gmax, amax_ecl(m1));
               h16_split(m1, xh1, xl1);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) {
@@ -948,17 +965,16 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
                 a1[mt] = rBC1[mt];
               }
               mfma_h16r(a1, fwc1, xh1, xl1);                      // Wc1(B)
-              edge_f(a0, r00, r01, r02, f00, f01, f02);           // | coord MLP (A)
+              edge_f(a0, r00, r01, r02, f00, f01, f02, cA);       // | coord MLP (A)
               STAMP(2);
-              edge_f(a1, r10, r11, r12, f10, f11, f12);
+              edge_f(a1, r10, r11, r12, f10, f11, f12, cB);
             }
             } else {
-            head2(k, e0, a0, r00, r01, r02);
-            head2(k + 1, e1, a1, r10, r11, r12);
+            head2(k, e0, a0, r00, r01, r02, okA);
+            head2(k + 1, e1, a1, r10, r11, r12, okB);
             STAMP(0);
             silu_ecl(a0);
             silu_ecl(a1);
-            gmax = fmaxf(amax_ecl(a0), amax_ecl(a1));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; }
             {
@@ -970,7 +986,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             STAMP(1);
             silu_ecl(m0);
             silu_ecl(m1);
-            gmax = fmaxf(gmax, fmaxf(amax_ecl(m0), amax_ecl(m1)));
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
               pm[mt] = m0[mt] + m1[mt];
@@ -984,10 +999,16 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
               mfma_h16x2(a0, a1, wc1l, mh0, ml0, mh1, ml1, lane);  // coord hidden: SiLU(Wc1 m + bc1)
             }
             STAMP(2);
-            edge_f(a0, r00, r01, r02, f00, f01, f02);
-            edge_f(a1, r10, r11, r12, f10, f11, f12);
+            edge_f(a0, r00, r01, r02, f00, f01, f02, cA);
+            edge_f(a1, r10, r11, r12, f10, f11, f12, cB);
             }
-            if (__builtin_expect(__any(gmax > H16_LIMIT), 0)) {
+            // Guard: an activation beyond the fp16 range (|x| > 65504: a diverged rollout) makes its
+            // hi part inf; inf x w (0 included) puts inf or NaN into every output channel of that
+            // product, hence into every later channel and into c. So a non-finite c from finite
+            // inputs flags exactly the pairs to recompute (column-scaled), at a few compares instead
+            // of 32 v_max3 per pair. Below 65504 the split keeps its 2^-22 relative accuracy.
+            const bool redo = (okA && !__builtin_isfinite(cA)) || (okB && !__builtin_isfinite(cB));
+            if (__builtin_expect(__any(redo), 0)) {
               f4 x0[4], x1[4];
               exact_unit(k, e0, x0, f00, f01, f02);
               exact_unit(k + 1, e1, x1, f10, f11, f12);
