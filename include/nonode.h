@@ -36,6 +36,12 @@ typedef enum {
 
 /* Variant of the shared E(n)-equivariant layer. */
 enum { NONODE_VARIANT_EGNO = 0, NONODE_VARIANT_SEGNO = 1 };
+/* Option bits OR-ed into the variant of nonode_pack_layer / nonode_pack_layer_bwd (stored in the
+ * blob, so every forward, backward and rollout entry that takes the blob follows them):
+ *  NORM_RADIAL: EGNO(norm=True): the radial edge input is F.normalize(|x_i - x_j|^2) over its one
+ *               element = s / max(s, 1e-12) (InvariantScalarNet, basic.py:136-141);
+ *  TANH_COORD:  SEGNO(tanh=True): the coordinate MLP ends in nn.Tanh (gcl.py:57-59). */
+enum { NONODE_LAYER_NORM_RADIAL = 0x100, NONODE_LAYER_TANH_COORD = 0x200 };
 
 const char* nonode_version(void);
 /* Thread-local message describing the last nonzero status. */
@@ -86,6 +92,8 @@ size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt);
  *   blobs[l]   (host array of device ptrs) packed layers from nonode_pack_layer(EGNO);
  *   tconv_blobs[l] (host array) time_conv_modules.l.t_conv.weights1 packed by nonode_pack_tconv;
  *   tconvx_w[l](host array) time_conv_x_modules.l.t_conv.weights1 [2][2][modes][2];
+ *   tconv_blobs = tconvx_w = NULL: EGNO(use_time_conv=False) (egno.py:99-107 skipped; loc_mean
+ *   and modes are then unused and loc_mean may be NULL);
  *   outputs x_out, v_out [T*B*N][3], h_out [T*B*N][64] (time-major, egno.py:89-96).
  * Limits: N >= 2, T <= 16, modes <= 9, time_emb_dim even <= 64, in_node <= 8.
  */

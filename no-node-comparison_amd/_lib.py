@@ -30,6 +30,9 @@ SYMBOLS = (
 
 VARIANT_EGNO = 0
 VARIANT_SEGNO = 1
+# option bits OR-ed into the pack variant (nonode.h NONODE_LAYER_*)
+LAYER_NORM_RADIAL = 0x100   # EGNO(norm=True), basic.py:140-141
+LAYER_TANH_COORD = 0x200    # SEGNO(tanh=True), gcl.py:57-59
 # profile_end() record kinds beyond the two layer variants (csrc/nonode.hip ProfScope)
 PROF_TCONV, PROF_TCONV_FIRST, PROF_SIM_CHARGED, PROF_SIM_GRAVITY, PROF_EDGE_BWD0, PROF_EDGE_BWD1 = 2, 3, 4, 5, 6, 7
 

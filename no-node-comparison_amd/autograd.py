@@ -24,7 +24,8 @@ class EGNOTrain(torch.autograd.Function):
         L = _lib.lib()
         T = model.num_timesteps
         dev = x.device
-        x, h, v, lm, ef, tt = _f32(x), _f32(h), _f32(v), _f32(loc_mean), _f32(edge_fea), _f32(t_out)
+        x, h, v, ef, tt = _f32(x), _f32(h), _f32(v), _f32(edge_fea), _f32(t_out)
+        lm = _f32(loc_mean) if loc_mean is not None else None   # unused without time convolutions
         emb_cols = model.time_emb_dim * (1 if t_in is None else 2)
         Bt = tt.shape[0]
         blobs, tblobs = model._packed()
@@ -37,12 +38,11 @@ class EGNOTrain(torch.autograd.Function):
         st_bytes = L.nonode_egno_train_state_bytes(B, N, T, model.n_layers, model.in_node_nf, emb_cols)
         state = torch.empty((st_bytes + 3) // 4, dtype=torch.float32, device=dev)
         P = ctypes.c_void_p * model.n_layers
-        tcx = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
+        tcw_p, tcx_p, _keep = model.tconv_arrays(tblobs)
         ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
         head = (B, N, T, model.n_layers, model.in_node_nf, model.in_edge_nf, model.time_emb_dim, model.num_modes, Bt,
                 _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef))
-        tail = (_lib.ptr(ew), _lib.ptr(eb), P(*[blobs[i].data_ptr() for i in range(model.n_layers)]),
-                P(*[tblobs[i].data_ptr() for i in range(model.n_layers)]), P(*[t.data_ptr() for t in tcx]),
+        tail = (_lib.ptr(ew), _lib.ptr(eb), P(*[blobs[i].data_ptr() for i in range(model.n_layers)]), tcw_p, tcx_p,
                 _lib.ptr(x_out), _lib.ptr(v_out), _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.ptr(ws), ws_bytes,
                 _lib.stream_of(x))
         if t_in is None:
@@ -70,10 +70,13 @@ class EGNOTrain(torch.autograd.Function):
             names = model.layer_param_names(i)
             lg[i] = _lib.LayerGrads(*[grads[nm].data_ptr() for nm in names])
         P = ctypes.c_void_p * nl
-        tw = [_f32(m.t_conv.weights1) for m in model.time_conv_modules]
-        txw = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
-        g_tc = P(*[grads[f"time_conv_modules.{i}.t_conv.weights1"].data_ptr() for i in range(nl)])
-        g_tcx = P(*[grads[f"time_conv_x_modules.{i}.t_conv.weights1"].data_ptr() for i in range(nl)])
+        tw_p = txw_p = g_tc = g_tcx = None   # use_time_conv=False: no TimeConv arrays
+        if model.use_time_conv:
+            tw = [_f32(m.t_conv.weights1) for m in model.time_conv_modules]
+            txw = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
+            tw_p, txw_p = P(*[t.data_ptr() for t in tw]), P(*[t.data_ptr() for t in txw])
+            g_tc = P(*[grads[f"time_conv_modules.{i}.t_conv.weights1"].data_ptr() for i in range(nl)])
+            g_tcx = P(*[grads[f"time_conv_x_modules.{i}.t_conv.weights1"].data_ptr() for i in range(nl)])
         ws_bytes = L.nonode_egno_backward_workspace_bytes(B, N, T, model.num_modes)
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
         gx = _f32(gx) if gx is not None else torch.zeros(T * B * N, 3, device=dev)
@@ -82,7 +85,7 @@ class EGNOTrain(torch.autograd.Function):
         head = (B, N, T, nl, model.in_node_nf, model.in_edge_nf, model.time_emb_dim)
         tail = (model.num_modes, Bt,
                 _lib.ptr(ctx.lm), _lib.ptr(ctx.ef), P(*[bblobs[i].data_ptr() for i in range(nl)]),
-                P(*[t.data_ptr() for t in tw]), P(*[t.data_ptr() for t in txw]), _lib.ptr(ctx.state),
+                tw_p, txw_p, _lib.ptr(ctx.state),
                 _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh), lg, g_tc, g_tcx,
                 _lib.ptr(grads["embedding.weight"]), _lib.ptr(grads["embedding.bias"]), _lib.ptr(ws), ws_bytes,
                 _lib.stream_of(gx))

@@ -70,7 +70,15 @@ enum : int {
 };
 enum : int { H_WA = 0, H_WB, H_WV1, H_WN1A, H_WN1B, H_WN2, H_COUNT };   // WN1A/B: h / message-sum columns
 enum : int { V_B2 = 0, V_BC1, V_WC2, V_B1, V_BV1, V_WV2, V_BN1, V_BN2, V_COUNT };
-constexpr int OFF_SCAL = OFF_VEC + V_COUNT * 64;  // [0] = coord b2, [1] = node_v b2
+constexpr int OFF_SCAL = OFF_VEC + V_COUNT * 64;  // [0] = coord b2, [1] = node_v b2, [SC_*] option flags
+// option flags (1.f / 0.f): radial input normalised (EGNO norm=True, basic.py:140-141); coordinate
+// MLP output through tanh (SEGNO tanh=True, gcl.py:57-59)
+constexpr int SC_NORM = 2, SC_TANH = 3;
+// F.normalize of the one-element radial feature: s / max(|s|, 1e-12) (s >= 0: 1 unless s < 1e-12)
+// (inf, NaN -> NaN as inf / inf and NaN / NaN in the reference)
+__device__ __forceinline__ float radial_norm(float s) {
+  return s < 1e-12f ? s * 1e12f : (__builtin_isfinite(s) ? 1.f : s - s);
+}
 static_assert(OFF_SCAL + 64 == OFF_H16, "blob layout");
 constexpr int BLOB_FLOATS = OFF_H16N + H_COUNT * 4096;
 constexpr float H16_LIMIT = 16384.f;   // |activation| above this takes the exact f32 MFMA path
@@ -445,6 +453,7 @@ struct PackArgs {
   const float* vw1; const float* vb1; const float* vw2; const float* vb2;  // may be null
   const float* nw1; const float* nb1; const float* nw2; const float* nb2;
   int ne;
+  int flags;   // NONODE_LAYER_* option bits (stored at OFF_SCAL + 2 / + 3)
   float* blob;
 };
 
@@ -520,7 +529,12 @@ __global__ void pack_kernel(PackArgs a) {
         B[OFF_VEC + dd] = val;
       } else if (d < 512 + V_COUNT * 64 + 64) {
         const int i = d - 512 - V_COUNT * 64;
-        B[OFF_SCAL + i] = (i == 0) ? a.cb2[0] : (i == 1 && a.vb2) ? a.vb2[0] : 0.f;
+        float val = 0.f;
+        if (i == 0) val = a.cb2[0];
+        else if (i == 1 && a.vb2) val = a.vb2[0];
+        else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
+        else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
+        B[OFF_SCAL + i] = val;
       }
       break;
   }
@@ -619,6 +633,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_FEAT)[tid];
   const float bc2 = p.blob[OFF_SCAL + 0];
   const float bv2 = p.blob[OFF_SCAL + 1];
+  const bool rnorm = p.blob[OFF_SCAL + SC_NORM] != 0.f;                        // wave-uniform
+  const bool ctanh = VARIANT == SEGNO && p.blob[OFF_SCAL + SC_TANH] != 0.f;    // wave-uniform
   const float* vFEAT_ = sV;
   const float* vB2_ = sV + 512 + V_B2 * 64;
   const float* vBC1_ = sV + 512 + V_BC1 * 64;
@@ -822,7 +838,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           const int sl = sb + j;
           const float* xs = sX + sl * 4;
           r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
-          const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+          float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+          if (rnorm) d2 = radial_norm(d2);
           f4 q4[4];
           load_ecl(q4, sQ + sl * ROWP, g);
           load_ecl(a, Prow, g);
@@ -839,7 +856,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         };
         auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
           silu_ecl(c1);
-          const float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2_, g)) + bc2;
+          float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2_, g)) + bc2;
+          if (ctanh) c = tanhf(c);
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
           if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
             f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -867,8 +885,9 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             const int sl = sb + j;
             const f4 xs = *reinterpret_cast<const f4*>(sX + sl * 4);
             r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
-            const float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+            float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
             ok = xs[3] * xr3 != 0.f && __builtin_isfinite(d2);   // finite inputs: a guard recompute can help
+            if (rnorm) d2 = radial_norm(d2);
             load_ecl(a, sQ + sl * ROWP, g);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
@@ -884,8 +903,9 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           auto edge_f = [&](f4 (&c1)[4], float r0, float r1, float r2, float& f0, float& f1, float& f2,
                             float& c) __attribute__((always_inline)) {
             silu_ecl(c1);
-            c = dot_r(c1, rWC2) + bc2;
-            f0 = r0 * c; f1 = r1 * c; f2 = r2 * c;
+            c = dot_r(c1, rWC2) + bc2;   // the guard tests c before the tanh (tanh(inf) = 1)
+            const float ct = ctanh ? tanhf(c) : c;
+            f0 = r0 * ct; f1 = r1 * ct; f2 = r2 * ct;
             if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
               f0 = fminf(fmaxf(f0, -100.f), 100.f);
               f1 = fminf(fmaxf(f1, -100.f), 100.f);
@@ -1559,6 +1579,31 @@ __global__ void embed_kernel(int n_nodes, int din, const float* in, const float*
   out[idx] = acc;
 }
 
+// ---- first-layer inputs without a TimeConv (training forward; EGNO use_time_conv=False) -----------
+// h0[t*BN + c] = emb_w[:, :din] h_in[c] + etab[c % Bt][t]   (egno.py:63-76; same arithmetic as
+// tconv_kernel<true>), and x, v replicated over T (egno.py:89-96)
+// frames = 1 (num_inputs > 1): h_in, x, v are per frame ([T*BN] rows) instead of replicated
+__global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, const float* emb_w, int emb_ld,
+                          const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr,
+                          int frames) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= BN * 64) return;
+  const int o = idx & 63, c = idx >> 6;
+  auto hin_part = [&](size_t r) {
+    float b = 0.f;
+    for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[r * din + k], b);
+    return b;
+  };
+  const float base = frames ? 0.f : hin_part((size_t)c);
+  const float* et = etab + (size_t)(c % Bt) * T * 64;
+  for (int t = 0; t < T; ++t) {
+    const size_t row = (size_t)t * BN + c;
+    const size_t src = frames ? row : (size_t)c;
+    h0[row * 64 + o] = et[t * 64 + o] + (frames ? hin_part(row) : base);
+    if (o < 3) { xr[row * 3 + o] = x[src * 3 + o]; vr[row * 3 + o] = v[src * 3 + o]; }
+  }
+}
+
 // ---- host-side launchers ----------------------------------------------------------------------
 // NONODE_XCD=0 turns off the XCD-aware tile / chunk order of the EGNO forward
 bool xcd_on() {
@@ -1694,11 +1739,19 @@ size_t nonode_layer_blob_floats(void) { return BLOB_FLOATS; }
 int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
                       float* blob, void* stream) {
   if (!w || !blob) return fail(NONODE_EINVAL, "pack_layer: null pointer");
+  const int flags = variant & ~0xff;
+  variant &= 0xff;
+  if (flags & ~(NONODE_LAYER_NORM_RADIAL | NONODE_LAYER_TANH_COORD))
+    return fail(NONODE_EINVAL, "pack_layer: unknown option bits 0x%x", flags);
   if (hidden != HID) return fail(NONODE_EUNSUPPORTED, "pack_layer: hidden=%d (only 64)", hidden);
   if (n_edge_feat < 0 || n_edge_feat > 4) return fail(NONODE_EUNSUPPORTED, "pack_layer: n_edge_feat=%d", n_edge_feat);
   if (!w->edge_w1 || !w->edge_b1 || !w->edge_w2 || !w->edge_b2 || !w->coord_w1 || !w->coord_b1 ||
       !w->coord_w2 || !w->coord_b2 || !w->node_w1 || !w->node_b1 || !w->node_w2 || !w->node_b2)
     return fail(NONODE_EINVAL, "pack_layer: missing weight pointer");
+  if ((flags & NONODE_LAYER_NORM_RADIAL) && variant != NONODE_VARIANT_EGNO)
+    return fail(NONODE_EINVAL, "pack_layer: NORM_RADIAL is an EGNO option");
+  if ((flags & NONODE_LAYER_TANH_COORD) && variant != NONODE_VARIANT_SEGNO)
+    return fail(NONODE_EINVAL, "pack_layer: TANH_COORD is a SEGNO option");
   if (variant == NONODE_VARIANT_EGNO && (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2))
     return fail(NONODE_EINVAL, "pack_layer: EGNO needs node_v_net weights");
   PackArgs a;
@@ -1713,6 +1766,7 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
   a.vw2 = egno ? w->vel_w2 : nullptr; a.vb2 = egno ? w->vel_b2 : nullptr;
   a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
   a.ne = n_edge_feat;
+  a.flags = flags;
   a.blob = blob;
   hipLaunchKernelGGL(pack_kernel, dim3(32, 16), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_kernel");
@@ -1791,7 +1845,9 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
     return fail(NONODE_EUNSUPPORTED,
                 "egno_forward: B=%d N=%d T=%d layers=%d in_node=%d modes=%d temb=%d Bt=%d", B, N, T,
                 n_layers, in_node, modes, time_emb_dim, Bt);
-  if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_blobs || !tconvx_w ||
+  // use_time_conv=False (egno.py:99-107 skipped): both TimeConv arrays null
+  const bool tc = tconv_blobs != nullptr;
+  if (!x || !h || !v || (tc && !loc_mean) || !t_out || !emb_w || !emb_b || !blobs || tc != (tconvx_w != nullptr) ||
       !x_out || !v_out || !h_out || !workspace)
     return fail(NONODE_EINVAL, "egno_forward: null pointer");
   if (workspace_bytes < nonode_egno_workspace_bytes(B, N, T, Bt))
@@ -1809,6 +1865,24 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
     hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim,
                        t_out, emb_w, emb_ld, emb_b, etab, t_in);
     if (int rc = check_launch("temb_kernel")) return rc;
+  }
+  if (!tc) {
+    // layer l reads buffer (L - l) & 1 and writes (L - 1 - l) & 1 of {h_out | x_out, hB | xB}, so the
+    // last layer writes h_out, x_out; v (unchanged by EGNN_Layer, basic.py:186) is replicated once
+    float* hb[2] = {h_out, hB};
+    float* xb[2] = {x_out, xB};
+    const int L = n_layers;
+    hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
+                       etab, x, v, hb[L & 1], xb[L & 1], v_out, frames);
+    if (int rc = check_launch("h0_kernel")) return rc;
+    for (int l = 0; l < L; ++l) {
+      const int i = (L - l) & 1, o = (L - 1 - l) & 1;
+      if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hb[i], xb[i], v_out, edge_fea,
+                                      blobs[l], 0.f, 1.f, 0, hb[o], xb[o], nullptr, s, 1, nullptr, nullptr, nullptr,
+                                      BN))
+        return rc;
+    }
+    return NONODE_OK;
   }
   for (int l = 0; l < n_layers; ++l) {
     TconvArgs a{};

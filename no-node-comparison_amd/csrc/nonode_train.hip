@@ -44,7 +44,7 @@ enum : int {
   BOFF_VEC = 66048,     // vectors (vp order), BV_* below
 };
 enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
-constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2
+constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2, [SC_*] option flags
 // fp16 hi/lo fragments (pack_h16 layout, unscaled) of the four 64x64 edge matrices: the edge
 // backward's forward recompute (W2, Wc1) and its transposed products (W2^T, Wc1^T) run fp16x3
 constexpr int BOFF_H16 = BOFF_SCAL + 64;
@@ -118,7 +118,12 @@ __global__ void pack_bwd_kernel(PackArgs a) {
         B[BOFF_VEC + dd] = val;
       } else if (d < 512 + BV_COUNT * 64 + 64) {
         const int i = d - 512 - BV_COUNT * 64;
-        B[BOFF_SCAL + i] = (i == 0) ? a.cb2[0] : (i == 1 && a.vb2) ? a.vb2[0] : 0.f;
+        float val = 0.f;
+        if (i == 0) val = a.cb2[0];
+        else if (i == 1 && a.vb2) val = a.vb2[0];
+        else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
+        else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
+        B[BOFF_SCAL + i] = val;
       }
       break;
   }
@@ -218,31 +223,7 @@ __device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
 }
 
-// ---- training-forward helpers -----------------------------------------------------------------
-// h0[t*BN + c] = emb_w[:, :din] h_in[c] + etab[c % Bt][t]   (egno.py:63-76; same arithmetic as
-// tconv_kernel<true>), and x, v replicated over T (egno.py:89-96)
-// frames = 1 (num_inputs > 1): h_in, x, v are per frame ([T*BN] rows) instead of replicated
-__global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, const float* emb_w, int emb_ld,
-                          const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr,
-                          int frames) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= BN * 64) return;
-  const int o = idx & 63, c = idx >> 6;
-  auto hin_part = [&](size_t r) {
-    float b = 0.f;
-    for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[r * din + k], b);
-    return b;
-  };
-  const float base = frames ? 0.f : hin_part((size_t)c);
-  const float* et = etab + (size_t)(c % Bt) * T * 64;
-  for (int t = 0; t < T; ++t) {
-    const size_t row = (size_t)t * BN + c;
-    const size_t src = frames ? row : (size_t)c;
-    h0[row * 64 + o] = et[t * 64 + o] + (frames ? hin_part(row) : base);
-    if (o < 3) { xr[row * 3 + o] = x[src * 3 + o]; vr[row * 3 + o] = v[src * 3 + o]; }
-  }
-}
-
+// ---- training-forward helpers (h0_kernel: nonode.hip) ----------------------------------------
 // emb_in[t*BN + c] = [h_in[c], temb(t_out[c % Bt][t])]  (the embedding Linear's input rows)
 // rows [h_in | temb(t_out)], or [h_in | temb(t_in) | temb(t_out)] when t_in != null (egno.py:77-79)
 __global__ void emb_in_kernel(int BN, int T, int din, int dim, int Bt, const float* hin, const float* t_out,
@@ -544,6 +525,8 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   float* myGX = sGX + wave * p.s_max * 4;
   const float* bb = p.bb;
   const float bc2 = bb[BOFF_SCAL + 0];
+  const bool rnorm = bb[BOFF_SCAL + SC_NORM] != 0.f;   // EGNO norm=True (basic.py:140-141)
+  const bool ctanh = bb[BOFF_SCAL + SC_TANH] != 0.f;   // SEGNO tanh=True (gcl.py:57-59)
   const float* wW2 = bb + BOFF_W2;
   const float* wWc1 = bb + BOFF_WC1;
   {
@@ -644,7 +627,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       const float s2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
       const float* efp = p.ef + (((size_t)(gr % p.ef_mod) * N + n) * Nm1 + jj) * NE;
       float fe[NF];
-      fe[0] = s2;
+      fe[0] = rnorm ? radial_norm(s2) : s2;
 #pragma unroll
       for (int kk = 0; kk < NE; ++kk) fe[1 + kk] = efp[kk];
       float ev[2];
@@ -707,6 +690,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         f4 c1[4];
         silu_keep(z3, sg3, c1);
         c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
+        if (ctanh) c = tanhf(c);
       }
       // reverse: f = r c (SEGNO: clamp(r c, +-100) per edge)
       float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
@@ -715,7 +699,8 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         gF1 = fabsf(r1 * c) <= 100.f ? gF1 : 0.f;
         gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
       }
-      const float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
+      float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
+      if (ctanh) gc *= 1.f - c * c;   // through the tanh: gc is the gradient of the MLP output
       float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
       // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
       f4 gz3[4];
@@ -754,7 +739,8 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
       if (!(p.dbg & 8)) wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
       // s = |r|^2 input column
-      const float gs = dot_vp(gz1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64, g);
+      float gs = dot_vp(gz1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64, g);
+      if (rnorm) gs = s2 < 1e-12f ? gs * 1e12f : 0.f;   // d normalize(s) / ds: 1 / eps below eps, else 0
       gr0 = fmaf(2.f * gs, r0, gr0);
       gr1 = fmaf(2.f * gs, r1, gr1);
       gr2 = fmaf(2.f * gs, r2, gr2);
@@ -1454,6 +1440,13 @@ size_t nonode_bwd_blob_floats(void) { return BBLOB_FLOATS; }
 int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat, float* bblob,
                           void* stream) {
   if (!w || !bblob) return fail(NONODE_EINVAL, "pack_layer_bwd: null pointer");
+  const int flags = variant & ~0xff;
+  variant &= 0xff;
+  if (flags & ~(NONODE_LAYER_NORM_RADIAL | NONODE_LAYER_TANH_COORD))
+    return fail(NONODE_EINVAL, "pack_layer_bwd: unknown option bits 0x%x", flags);
+  if (((flags & NONODE_LAYER_NORM_RADIAL) && variant != NONODE_VARIANT_EGNO) ||
+      ((flags & NONODE_LAYER_TANH_COORD) && variant != NONODE_VARIANT_SEGNO))
+    return fail(NONODE_EINVAL, "pack_layer_bwd: NORM_RADIAL is an EGNO option, TANH_COORD a SEGNO one");
   if (hidden != HID || n_edge_feat < 0 || n_edge_feat > 4)
     return fail(NONODE_EUNSUPPORTED, "pack_layer_bwd: hidden=%d n_edge_feat=%d", hidden, n_edge_feat);
   const bool egno = variant == NONODE_VARIANT_EGNO;
@@ -1470,6 +1463,7 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   a.vw2 = egno ? w->vel_w2 : nullptr; a.vb2 = egno ? w->vel_b2 : nullptr;
   a.nw1 = w->node_w1; a.nb1 = w->node_b1; a.nw2 = w->node_w2; a.nb2 = w->node_b2;
   a.ne = n_edge_feat;
+  a.flags = flags;
   a.blob = bblob;
   hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 20), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_bwd_kernel");
@@ -1494,7 +1488,8 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
       modes > MMAX_T || time_emb_dim < 4 || time_emb_dim > 64 || (time_emb_dim & 1) || Bt <= 0 || (B * N) % Bt)
     return fail(NONODE_EUNSUPPORTED, "egno_forward_train: B=%d N=%d T=%d modes=%d (training: modes <= %d)", B, N, T,
                 modes, MMAX_T);
-  if (!x || !h || !v || !loc_mean || !t_out || !emb_w || !emb_b || !blobs || !tconv_blobs || !tconvx_w ||
+  const bool tc = tconv_blobs != nullptr;   // false: use_time_conv=False (both TimeConv arrays null)
+  if (!x || !h || !v || (tc && !loc_mean) || !t_out || !emb_w || !emb_b || !blobs || tc != (tconvx_w != nullptr) ||
       !x_out || !v_out || !h_out || !state || !workspace)
     return fail(NONODE_EINVAL, "egno_forward_train: null pointer");
   const int emb_cols = (t_in ? 2 : 1) * time_emb_dim;   // time-embedding columns of the embedding Linear
@@ -1525,11 +1520,15 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
   for (int l = 0; l < L; ++l) {
     TconvArgs a{};
     a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
-    a.wp = tconv_blobs[l]; a.wx = tconvx_w[l]; a.frames = frames;
     a.h = st.hs + l * n * 64; a.x = st.xs + l * n * 3; a.v = st.vs + l * n * 3; a.lm = loc_mean;
-    a.h_out = st.he + l * n * 64; a.x_out = st.xe + l * n * 3; a.v_out = st.ve + l * n * 3;
-    a.mask_out = st.mask + (size_t)l * T * ((BN + 15) / 16) * 16;
-    if (int rc = launch_tconv(false, a, s)) return rc;
+    if (tc) {
+      a.wp = tconv_blobs[l]; a.wx = tconvx_w[l]; a.frames = frames;
+      a.h_out = st.he + l * n * 64; a.x_out = st.xe + l * n * 3; a.v_out = st.ve + l * n * 3;
+      a.mask_out = st.mask + (size_t)l * T * ((BN + 15) / 16) * 16;
+      if (int rc = launch_tconv(false, a, s)) return rc;
+    } else {   // the layer reads its saved inputs directly (the backward does the same)
+      a.h_out = st.hs + l * n * 64; a.x_out = st.xs + l * n * 3; a.v_out = st.vs + l * n * 3;
+    }
     if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, a.h_out, a.x_out, a.v_out, edge_fea, blobs[l], 0.f, 1.f,
                                     0, st.hs + (l + 1) * n * 64, st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
                                     st.Ms + l * n * 64, st.Fs + l * n * 4))
@@ -1588,7 +1587,9 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
   if (B <= 0 || N < 2 || T <= 0 || T > TMAX || n_layers < 1 || modes < 1 || modes > MMAX_T || Bt <= 0 ||
       n_edge_feat < 0 || n_edge_feat > 4)
     return fail(NONODE_EUNSUPPORTED, "egno_backward: B=%d N=%d T=%d", B, N, T);
-  if (!loc_mean || !bblobs || !tconv_w || !tconvx_w || !state || !g_x || !layer_grads || !g_tconv || !g_tconvx ||
+  const bool tc = tconv_w != nullptr;   // false: use_time_conv=False (every TimeConv array null)
+  if ((tc && (!loc_mean || !tconvx_w || !g_tconv || !g_tconvx)) ||
+      (!tc && (tconvx_w || g_tconv || g_tconvx)) || !bblobs || !state || !g_x || !layer_grads ||
       !g_emb_w || !g_emb_b || !workspace || (n_edge_feat > 0 && !edge_fea))
     return fail(NONODE_EINVAL, "egno_backward: null pointer");
   const int M = effective_modes(T, modes);
@@ -1612,9 +1613,9 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
   const int ld1 = 2 * HID + 1 + ne;
   for (int l = L - 1; l >= 0; --l) {
     const nonode_layer_grads& lg = layer_grads[l];
-    const float* he = st.he + l * n * 64;
-    const float* xe = st.xe + l * n * 3;
-    const float* ve = st.ve + l * n * 3;
+    const float* he = (tc ? st.he : st.hs) + l * n * 64;
+    const float* xe = (tc ? st.xe : st.xs) + l * n * 3;
+    const float* ve = (tc ? st.ve : st.vs) + l * n * 3;
     const float* bb = bblobs[l];
     // ---- EGNN_Layer reverse ----
     NodeBwdArgs na;
@@ -1668,8 +1669,17 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     if (int rc = gemm(w.op_gz, 64, 64, st.Ms + l * n * 64, 64, 64, (long long)n, lg.node_w1, 128, HID, nullptr))
       return rc;
     if (int rc = gemm(gh, 64, 64, w.op_z, 64, 64, (long long)n, lg.node_w2, 64, 0, lg.node_b2)) return rc;
-    // ---- TimeConv_x reverse: x, v of the layer's TimeConv input ----
     const int nxt = cur ^ 1;
+    if (!tc) {   // no TimeConv: the layer-input gradients are the next (earlier) layer's output gradients
+      hipMemcpyAsync(w.gx[nxt], w.gxe, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+      hipMemcpyAsync(w.gv[nxt], w.gve, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+      hipMemcpyAsync(w.gh[nxt], w.ghe, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+      if (int rc = check_launch("egno_backward copies")) return rc;
+      cur = nxt;
+      gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
+      continue;
+    }
+    // ---- TimeConv_x reverse: x, v of the layer's TimeConv input ----
     hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes,
                        st.xs + l * n * 3, st.vs + l * n * 3, loc_mean, w.gxe, w.gve, tconvx_w[l], w.gx[nxt],
                        w.gv[nxt], w.xpart, frames);

@@ -36,7 +36,8 @@ class _InvariantEdgeNet(nn.Module):
 
 
 class EGNNLayerParams(nn.Module):
-    """Parameters of one EGNN_Layer (basic.py:147-165); compute lives in the fused HIP kernel."""
+    """Parameters of one EGNN_Layer (basic.py:147-165); compute lives in the fused HIP kernel.
+    with_v=False has no node_v_net (basic.py:156-160)."""
 
     def __init__(self, in_edge_nf, hidden_nf, with_v=True):
         super().__init__()
@@ -76,9 +77,11 @@ def num_modes_for(num_timesteps, num_modes):
 class EGNO(nn.Module):
     """EGNO neural operator (egno.py:8-111) — drop-in, MI355X kernels underneath.
 
-    Supported configuration (the one model_confs.yaml:1-17 and main.py:133-134 build):
-    with_v=True, flat=False, norm=False, use_time_conv=True, hidden_nf=64, SiLU activation, any
-    num_inputs. Anything else raises NotImplementedError at construction.
+    Supported: hidden_nf=64, SiLU activation, any num_inputs, norm (the radial input normalised,
+    basic.py:140-141), use_time_conv (False: no TimeConv modules, egno.py:27-33, 99-107 skipped).
+    with_v=False builds the reference's module tree (no node_v_net) but, as in the reference, cannot
+    run forward (egno.py:95 / basic.py:180-181 need v and node_v_net). flat=True (BaseMLP widened
+    to 4*hidden with Tanh, basic.py:39-41) raises NotImplementedError at construction.
     """
 
     def __init__(self, n_layers, in_node_nf, in_edge_nf, hidden_nf, activation=nn.SiLU(), device='cpu',
@@ -88,14 +91,8 @@ class EGNO(nn.Module):
         unsupported = []
         if num_inputs < 1:
             unsupported.append(f"num_inputs={num_inputs}")
-        if not with_v:
-            unsupported.append("with_v=False")
         if flat:
             unsupported.append("flat=True")
-        if norm:
-            unsupported.append("norm=True")
-        if not use_time_conv:
-            unsupported.append("use_time_conv=False")
         if hidden_nf != 64:
             unsupported.append(f"hidden_nf={hidden_nf}")
         if not isinstance(activation, nn.SiLU):
@@ -109,6 +106,7 @@ class EGNO(nn.Module):
         self.varDT = varDT
         self.n_layers = n_layers
         self.with_v = with_v
+        self.norm = norm
         self.hidden_nf = hidden_nf
         self.in_node_nf = in_node_nf
         self.in_edge_nf = in_edge_nf
@@ -124,21 +122,26 @@ class EGNO(nn.Module):
         self.embedding = nn.Linear(in_node_nf + (2 if num_inputs > 1 else 1) * time_emb_dim, hidden_nf)
         for _ in range(n_layers):
             self.layers.append(EGNNLayerParams(in_edge_nf, hidden_nf, with_v))
-        self.time_conv_modules = nn.ModuleList()
-        self.time_conv_x_modules = nn.ModuleList()
-        for _ in range(n_layers):
-            self.time_conv_modules.append(_TimeConvParams(hidden_nf, hidden_nf, modes, 1.0 / (hidden_nf * hidden_nf)))
-            self.time_conv_x_modules.append(_TimeConvParams(2, 2, modes, 0.1))
+        if use_time_conv:
+            self.time_conv_modules = nn.ModuleList()
+            self.time_conv_x_modules = nn.ModuleList()
+            for _ in range(n_layers):
+                self.time_conv_modules.append(_TimeConvParams(hidden_nf, hidden_nf, modes,
+                                                              1.0 / (hidden_nf * hidden_nf)))
+                self.time_conv_x_modules.append(_TimeConvParams(2, 2, modes, 0.1))
         self._blobs = None
         self._blob_key = None
         self.to(device)
 
     # ---- packed weights (re-packed whenever a parameter changed in place) ----
+    def _pack_variant(self):
+        return _lib.VARIANT_EGNO | (_lib.LAYER_NORM_RADIAL if self.norm else 0)
+
     def _packed(self):
-        """Packed kernel weights (layer blobs, TimeConv blobs), rebuilt whenever a parameter
-        changed in place (optimizer step) or moved."""
+        """Packed kernel weights (layer blobs, TimeConv blobs or None without time convolutions),
+        rebuilt whenever a parameter changed in place (optimizer step) or moved."""
         params = [p for l in self.layers for p in l.parameters()] + \
-            [m.t_conv.weights1 for m in self.time_conv_modules]
+            ([m.t_conv.weights1 for m in self.time_conv_modules] if self.use_time_conv else [])
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._blobs is not None and key == self._blob_key:
             return self._blobs
@@ -147,17 +150,28 @@ class EGNO(nn.Module):
         dev = self.embedding.weight.device
         blobs = torch.empty(self.n_layers, n, dtype=torch.float32, device=dev)
         tblobs = torch.empty(self.n_layers, L.nonode_tconv_blob_floats(self.num_modes), dtype=torch.float32,
-                             device=dev)
+                             device=dev) if self.use_time_conv else None
         stream = _lib.stream_of(blobs)
         for i, layer in enumerate(self.layers):
             w = layer.weight_struct()
-            _lib.check(L.nonode_pack_layer(ctypes.byref(w), _lib.VARIANT_EGNO, self.hidden_nf,
+            _lib.check(L.nonode_pack_layer(ctypes.byref(w), self._pack_variant(), self.hidden_nf,
                                            self.in_edge_nf, _lib.ptr(blobs[i]), stream))
+            if not self.use_time_conv:
+                continue
             tw = self.time_conv_modules[i].t_conv.weights1.detach().float().contiguous()
             _lib.check(L.nonode_pack_tconv(_lib.ptr(tw), self.num_modes, self.num_timesteps, _lib.ptr(tblobs[i]),
                                            stream))
         self._blobs, self._blob_key = (blobs, tblobs), key
         return self._blobs
+
+    def tconv_arrays(self, tblobs):
+        """(tconv_blobs, tconvx_w) host pointer arrays for the C ABI plus the tensors they point
+        into (keep them alive for the call); (None, None, []) without time convolutions."""
+        if not self.use_time_conv:
+            return None, None, []
+        P = ctypes.c_void_p * self.n_layers
+        tcx = [m.t_conv.weights1.detach().to(torch.float32).contiguous() for m in self.time_conv_x_modules]
+        return (P(*[tblobs[i].data_ptr() for i in range(self.n_layers)]), P(*[t.data_ptr() for t in tcx]), tcx)
 
     def layer_param_names(self, i):
         """Parameter names of layer i in nonode_layer_weights / nonode_layer_grads field order."""
@@ -177,7 +191,7 @@ class EGNO(nn.Module):
         stream = _lib.stream_of(bb)
         for i, layer in enumerate(self.layers):
             w = layer.weight_struct()
-            _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), _lib.VARIANT_EGNO, self.hidden_nf, self.in_edge_nf,
+            _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), self._pack_variant(), self.hidden_nf, self.in_edge_nf,
                                                _lib.ptr(bb[i]), stream))
         self._bblobs, self._bblob_key = bb, key
         return bb
@@ -186,7 +200,10 @@ class EGNO(nn.Module):
         """egno.py:37-111. x, v, loc_mean: [BN, 3]; h: [BN, in_node_nf]; edge_index: 2 x [E]
         (fully connected, the dataset's edge order); edge_fea: [E, in_edge_nf];
         timesteps_out: [B, T]. Returns (x, v, h) of shapes [T*BN, 3], [T*BN, 3], [T*BN, 64]."""
-        if v is None or loc_mean is None:
+        if not self.with_v:
+            raise TypeError("EGNO(with_v=False) has no node_v_net: the reference forward fails on it too "
+                            "(v.repeat at egno.py:95 for v=None, node_v_net(h) at basic.py:180-181 otherwise)")
+        if v is None or (loc_mean is None and self.use_time_conv):
             raise ValueError("EGNO.forward needs v and loc_mean (the time convolution stacks "
                              "x - loc_mean with v, egno.py:103-105)")
         if self.num_inputs > 1:
@@ -239,7 +256,7 @@ class EGNO(nn.Module):
             raise ValueError(f"edge_fea must be [{I}, {E}, {self.in_edge_nf}], got {tuple(edge_fea.shape)}")
         fidx = torch.tensor(self.frame_inputs(T), device=x.device)
         f32 = lambda t: t.detach().to(torch.float32)  # noqa: E731
-        per_frame = lambda t: f32(t)[fidx].reshape(T * t.shape[1], t.shape[2]).contiguous()  # noqa: E731
+        per_frame = lambda t: None if t is None else f32(t)[fidx].reshape(T * t.shape[1], t.shape[2]).contiguous()  # noqa: E731,E501
         with torch.no_grad():
             xf, hf, vf, lmf, eff = (per_frame(t) for t in (x, h, v, loc_mean, edge_fea))
             t_in = f32(timesteps_in)[:, fidx].contiguous()
@@ -265,14 +282,13 @@ class EGNO(nn.Module):
 
     @torch.no_grad()
     def _forward_kernels(self, x, h, edge_fea, v, loc_mean, t_out, B, N):
-        f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
+        f32 = lambda t: None if t is None else t.detach().to(torch.float32).contiguous()  # noqa: E731
         x, h, v, lm, ef = f32(x), f32(h), f32(v), f32(loc_mean), f32(edge_fea)
         return self._launch_forward(_lib.lib().nonode_egno_forward, B, N, x, h, v, lm, ef, self._t_out_f32(t_out))
 
     def _launch_forward(self, entry, B, N, x, h, v, lm, ef, tt, t_in=None):
         """nonode_egno_forward (single input) or nonode_egno_forward_frames (t_in given)."""
         T = self.num_timesteps
-        f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
         blobs, tblobs = self._packed()
         dev = x.device
         n = T * B * N
@@ -284,9 +300,8 @@ class EGNO(nn.Module):
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
         P = ctypes.c_void_p * self.n_layers
         blob_p = P(*[blobs[i].data_ptr() for i in range(self.n_layers)])
-        tcx = [f32(m.t_conv.weights1) for m in self.time_conv_x_modules]
-        tcw_p = P(*[tblobs[i].data_ptr() for i in range(self.n_layers)])
-        tcx_p = P(*[t.data_ptr() for t in tcx])
+        tcw_p, tcx_p, _keep = self.tconv_arrays(tblobs)
+        f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
         ew, eb = f32(self.embedding.weight), f32(self.embedding.bias)
         tail = (_lib.ptr(ew), _lib.ptr(eb), blob_p, tcw_p, tcx_p, _lib.ptr(x_out), _lib.ptr(v_out),
                 _lib.ptr(h_out), _lib.ptr(ws), ws_bytes, _lib.stream_of(x))

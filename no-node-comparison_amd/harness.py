@@ -161,14 +161,13 @@ def egno_rollout(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean
     ti = timesteps_in.reshape(-1).to(torch.int32).contiguous() if timesteps_in is not None else None
     eo = _f32(edge_attr_o).reshape(E, -1)
     q = _f32(charges).reshape(-1) if charges is not None else None
-    x, h, v, lm, ef = _f32(loc), _f32(nodes), _f32(vel), _f32(loc_mean), _f32(edge_attr)
+    x, h, v, ef = _f32(loc), _f32(nodes), _f32(vel), _f32(edge_attr)
+    lm = _f32(loc_mean) if loc_mean is not None else None   # unused without time convolutions
     blobs, tblobs = model._packed()
     L = _lib.lib()
     P = ctypes.c_void_p * model.n_layers
-    tcx = [_f32(m.t_conv.weights1) for m in model.time_conv_x_modules]
     blob_p = P(*[blobs[i].data_ptr() for i in range(model.n_layers)])
-    tcw_p = P(*[tblobs[i].data_ptr() for i in range(model.n_layers)])
-    tcx_p = P(*[t.data_ptr() for t in tcx])
+    tcw_p, tcx_p, _keep = model.tconv_arrays(tblobs)
     ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
     preds = torch.empty(traj_len * T, BN, 3, device=dev)
     en_all = torch.empty(traj_len * T, B, device=dev) if energy_dataset is not None else None

@@ -24,7 +24,7 @@ from .graph import check_full_graph
 class GCLParams(nn.Module):
     """Parameters of SEGNO_GCL (gcl.py:26-69) in its registration and RNG order."""
 
-    def __init__(self, input_nf, output_nf, hidden_nf, edges_in_d=0, act_fn=nn.SiLU()):
+    def __init__(self, input_nf, output_nf, hidden_nf, edges_in_d=0, act_fn=nn.SiLU(), tanh=False):
         super().__init__()
         self.edge_mlp = nn.Sequential(nn.Linear(2 * input_nf + 1 + edges_in_d, hidden_nf), act_fn,
                                       nn.Linear(hidden_nf, hidden_nf), act_fn)
@@ -32,7 +32,11 @@ class GCLParams(nn.Module):
                                       nn.Linear(hidden_nf, output_nf))
         layer = nn.Linear(hidden_nf, 1, bias=True)
         torch.nn.init.xavier_uniform_(layer.weight, gain=0.001)
-        self.coord_mlp = nn.Sequential(nn.Linear(hidden_nf, hidden_nf), act_fn, layer)
+        # tanh=True appends nn.Tanh (gcl.py:57-59): no parameters, same state_dict keys; the
+        # reference's coords_range (a plain tensor, never used in forward) is kept for fidelity
+        self.coord_mlp = nn.Sequential(nn.Linear(hidden_nf, hidden_nf), act_fn, layer, *([nn.Tanh()] if tanh else []))
+        if tanh:
+            self.coords_range = torch.ones(1) * 3
         # coord_mlp_vel exists in the reference state_dict but is never used in forward
         self.coord_mlp_vel = nn.Sequential(nn.Linear(input_nf, hidden_nf), act_fn, nn.Linear(hidden_nf, 1))
 
@@ -46,8 +50,9 @@ class GCLParams(nn.Module):
 class SEGNO(nn.Module):
     """SEGNO neural ODE (model.py:6-102) — drop-in, MI355X kernels underneath.
 
-    Supported: SiLU, tanh=False, norm_diff=False, hidden_nf=64, in_edge_nf <= 4; single input
-    (x [BN, 3]) or several (x [BN, I, 3] with in_steps, multiple_agg 'sum' / 'attn').
+    Supported: SiLU, hidden_nf=64, in_edge_nf <= 4, tanh (coordinate MLP output through tanh,
+    gcl.py:57-59), norm_diff (stored, unused in the reference's forward, gcl.py:32,63); single
+    input (x [BN, 3]) or several (x [BN, I, 3] with in_steps, multiple_agg 'sum' / 'attn').
     """
 
     def __init__(self, in_node_nf, in_edge_nf, hidden_nf, device='cpu', act_fn=nn.SiLU(), n_layers=4,
@@ -57,10 +62,6 @@ class SEGNO(nn.Module):
         unsupported = []
         if hidden_nf != 64:
             unsupported.append(f"hidden_nf={hidden_nf}")
-        if tanh:
-            unsupported.append("tanh=True")
-        if norm_diff:
-            unsupported.append("norm_diff=True")
         if not isinstance(act_fn, nn.SiLU):
             unsupported.append(f"act_fn={act_fn}")
         if in_edge_nf > 4 or in_node_nf > 8:
@@ -84,7 +85,9 @@ class SEGNO(nn.Module):
         self.invariant = invariant
         self.norm_vel = norm_vel
         self.sigmoid = nn.Sigmoid()
-        self.module = GCLParams(hidden_nf, hidden_nf, hidden_nf, edges_in_d=in_edge_nf, act_fn=act_fn)
+        self.module = GCLParams(hidden_nf, hidden_nf, hidden_nf, edges_in_d=in_edge_nf, act_fn=act_fn, tanh=tanh)
+        self.tanh = tanh
+        self.norm_diff = norm_diff
         self.coords_weight = coords_weight
         self.recurrent = recurrent
         self.in_node_nf = in_node_nf
@@ -113,10 +116,13 @@ class SEGNO(nn.Module):
         L = _lib.lib()
         bb = torch.empty(L.nonode_bwd_blob_floats(), dtype=torch.float32, device=self.embedding.weight.device)
         w = self.module.weight_struct()
-        _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), _lib.VARIANT_SEGNO, self.hidden_nf, self.in_edge_nf,
+        _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), self._pack_variant(), self.hidden_nf, self.in_edge_nf,
                                            _lib.ptr(bb), _lib.stream_of(bb)))
         self._bblob, self._bblob_key = bb, key
         return bb
+
+    def _pack_variant(self):
+        return _lib.VARIANT_SEGNO | (_lib.LAYER_TANH_COORD if self.tanh else 0)
 
     def _training(self):
         return self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
@@ -129,7 +135,7 @@ class SEGNO(nn.Module):
         L = _lib.lib()
         blob = torch.empty(L.nonode_layer_blob_floats(), dtype=torch.float32, device=self.embedding.weight.device)
         w = self.module.weight_struct()
-        _lib.check(L.nonode_pack_layer(ctypes.byref(w), _lib.VARIANT_SEGNO, self.hidden_nf, self.in_edge_nf,
+        _lib.check(L.nonode_pack_layer(ctypes.byref(w), self._pack_variant(), self.hidden_nf, self.in_edge_nf,
                                        _lib.ptr(blob), _lib.stream_of(blob)))
         self._blob, self._blob_key = blob, key
         return blob

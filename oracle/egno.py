@@ -75,14 +75,22 @@ def aggregate(message, row, n_node, aggr):
     return out
 
 
-def egnn_layer(p, prefix, x, h, row, col, edge_fea, v):
-    """EGNN_Layer.forward (basic.py:167-186), with_v=True, norm=False, flat=False.
+def radial_normalize(s):
+    """F.normalize(s, p=2, dim=-1) of the one-element Gram row (basic.py:140-141): s / max(|s|, 1e-12)."""
+    return s / np.maximum(np.abs(s), np.asarray(1e-12, dtype=s.dtype))
+
+
+def egnn_layer(p, prefix, x, h, row, col, edge_fea, v, norm=False):
+    """EGNN_Layer.forward (basic.py:167-186), with_v=True, flat=False; norm normalises the radial
+    input (basic.py:140-141).
 
     Edge-MLP input order is [|r|^2, h_i, h_j, e] (InvariantScalarNet basic.py:136-143
     + hij = cat(h[row], h[col], edge_fea) at basic.py:170).
     """
     rij = x[row] - x[col]
     s = np.sum(rij * rij, axis=-1, keepdims=True)          # Gram of one vector: [E, 1]
+    if norm:
+        s = radial_normalize(s)
     inp = np.concatenate([s, h[row], h[col], edge_fea], axis=-1)
     m = base_mlp(inp, p, prefix + ".edge_message_net.scalar_net", last_act=True)
     c = base_mlp(m, p, prefix + ".coord_net")
@@ -95,8 +103,8 @@ def egnn_layer(p, prefix, x, h, row, col, edge_fea, v):
 
 
 def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=10,
-                 hidden=64, time_emb_dim=32, capture=None):
-    """EGNO.forward (egno.py:37-111) for num_inputs == 1.
+                 hidden=64, time_emb_dim=32, capture=None, norm=False, use_time_conv=True):
+    """EGNO.forward (egno.py:37-111) for num_inputs == 1 (use_time_conv=False skips egno.py:99-107).
 
     x, v, loc_mean: [BN, 3]; h: [BN, in_node]; row/col: [E]; edge_fea: [E, in_edge];
     t_out: [Bt, T]. Returns (x, v, h) with T-major rows (t*BN + node).
@@ -117,9 +125,12 @@ def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=
     col_t = np.tile(col, T) + offs_e
     xx = np.tile(x, (T, 1))
     vv = np.tile(v, (T, 1))
-    lm = np.tile(loc_mean, (T, 1))
+    lm = np.tile(loc_mean, (T, 1)) if use_time_conv else None
     ef = np.tile(edge_fea, (T, 1))
     for i in range(n_layers):
+        if not use_time_conv:
+            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
+            continue
         hh = time_conv(hh.reshape(T, BN, hidden), p[f"time_conv_modules.{i}.t_conv.weights1"])
         hh = hh.reshape(T * BN, hidden)
         X = np.stack([xx - lm, vv], axis=-1).reshape(T, BN, 3, 2)
@@ -128,7 +139,7 @@ def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=
         vv = X[..., 1].reshape(T * BN, 3)
         if capture is not None:
             capture[f"tconv{i}"] = (hh, xx, vv)
-        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
         if capture is not None:
             capture[f"layer{i}"] = (xx, vv, hh)
     return xx, vv, hh
@@ -142,7 +153,7 @@ def frame_inputs(num_inputs, T):
 
 
 def egno_forward_multi(p, x, h, row, col, edge_fea, v, loc_mean, t_in, t_out, n_layers=4, T=10,
-                       hidden=64, time_emb_dim=32):
+                       hidden=64, time_emb_dim=32, norm=False, use_time_conv=True):
     """EGNO.forward (egno.py:37-111) for num_inputs = I > 1.
 
     x, v, loc_mean: [I, BN, 3]; h: [I, BN, in_node]; edge_fea: [I, E, in_edge]; t_in: [Bt, I];
@@ -166,16 +177,19 @@ def egno_forward_multi(p, x, h, row, col, edge_fea, v, loc_mean, t_in, t_out, n_
     col_t = np.tile(col, T) + offs_e
     xx = x[f].reshape(T * BN, 3)
     vv = v[f].reshape(T * BN, 3)
-    lm = loc_mean[f].reshape(T * BN, 3)
+    lm = loc_mean[f].reshape(T * BN, 3) if use_time_conv else None
     ef = edge_fea[f].reshape(T * E, -1)
     for i in range(n_layers):
+        if not use_time_conv:
+            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
+            continue
         hh = time_conv(hh.reshape(T, BN, hidden), p[f"time_conv_modules.{i}.t_conv.weights1"])
         hh = hh.reshape(T * BN, hidden)
         X = np.stack([xx - lm, vv], axis=-1).reshape(T, BN, 3, 2)
         X = time_conv_x(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
         xx = X[..., 0].reshape(T * BN, 3) + lm
         vv = X[..., 1].reshape(T * BN, 3)
-        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
     return xx, vv, hh
 
 

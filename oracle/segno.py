@@ -28,13 +28,16 @@ def segment_mean(data, seg, n):
 
 
 def gcl_forward(p, h, row, col, x, v, edge_attr, n_layers, recurrent=True,
-                coords_weight=1.0, dense_mean=False):
-    """SEGNO_GCL.forward (gcl.py:111-119) with attention=False, tanh=False, node_attr=None."""
+                coords_weight=1.0, dense_mean=False, tanh=False):
+    """SEGNO_GCL.forward (gcl.py:111-119) with attention=False, node_attr=None; tanh: the
+    coordinate MLP ends in nn.Tanh (gcl.py:57-59)."""
     diff = x[row] - x[col]                                   # coord2radial gcl.py:104-109
     radial = np.sum(diff ** 2, axis=1, keepdims=True)
     inp = np.concatenate([h[row], h[col], radial, edge_attr], axis=1)   # gcl.py:78
     m = silu(linear(silu(linear(inp, p, "module.edge_mlp.0")), p, "module.edge_mlp.2"))
     c = linear(silu(linear(m, p, "module.coord_mlp.0")), p, "module.coord_mlp.2")
+    if tanh:
+        c = np.tanh(c)
     trans = np.clip(diff * c, -100, 100)                      # gcl.py:97-102
     agg = segment_mean_dense(trans, row) if dense_mean else segment_mean(trans, row, x.shape[0])
     agg = agg * coords_weight

@@ -57,10 +57,13 @@ def _scatter(msg, row, n, mean):
     return out
 
 
-def egnn_layer(p, pre, x, h, row, col, ef, v):
-    """EGNN_Layer.forward (basic.py:167-186): with_v, norm=False, flat=False."""
+def egnn_layer(p, pre, x, h, row, col, ef, v, norm=False):
+    """EGNN_Layer.forward (basic.py:167-186): with_v, flat=False; norm: F.normalize of the radial
+    input (basic.py:140-141)."""
     rij = x[row] - x[col]
     s = (rij * rij).sum(-1, keepdim=True)                         # InvariantScalarNet Gram (basic.py:136-143)
+    if norm:
+        s = F.normalize(s, p=2, dim=-1)
     m = _mlp(torch.cat([s, h[row], h[col], ef], -1), p, pre + ".edge_message_net.scalar_net", last_act=True)
     f = rij * _mlp(m, p, pre + ".coord_net")
     x = x + _mlp(h, p, pre + ".node_v_net") * v + _scatter(f, row, x.shape[0], True).clamp(-100, 100)
@@ -68,8 +71,10 @@ def egnn_layer(p, pre, x, h, row, col, ef, v):
     return x, v, h
 
 
-def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hidden=64, time_emb_dim=32):
-    """EGNO.forward (egno.py:37-111), num_inputs == 1. Returns (x, v, h), T-major rows."""
+def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hidden=64, time_emb_dim=32,
+                 norm=False, use_time_conv=True):
+    """EGNO.forward (egno.py:37-111), num_inputs == 1. Returns (x, v, h), T-major rows.
+    use_time_conv=False skips egno.py:99-107."""
     BN, E = h.shape[0], row.shape[0]
     temb = timestep_embedding(t_out, time_emb_dim)                     # [Bt, T, Ht]
     Bt = temb.shape[0]
@@ -77,15 +82,19 @@ def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hi
     hh = _lin(torch.cat([h[None].expand(T, -1, -1), temb], -1).reshape(T * BN, -1), p, "embedding")
     off = (torch.arange(T) * BN).repeat_interleave(E)                  # egno.py:89-96
     row_t, col_t = row.repeat(T) + off, col.repeat(T) + off
-    xx, vv, lm, eft = x.repeat(T, 1), v.repeat(T, 1), loc_mean.repeat(T, 1), ef.repeat(T, 1)
+    xx, vv, eft = x.repeat(T, 1), v.repeat(T, 1), ef.repeat(T, 1)
+    lm = loc_mean.repeat(T, 1) if use_time_conv else None
     for i in range(n_layers):
+        if not use_time_conv:
+            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm)
+            continue
         h3 = hh.reshape(T, BN, hidden)
         hh = (h3 + F.leaky_relu(_spectral(h3, p[f"time_conv_modules.{i}.t_conv.weights1"]))).reshape(T * BN, hidden)
         X = torch.stack([xx - lm, vv], -1).reshape(T, BN, 3, 2)
         X = X + _spectral(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
         xx = X[..., 0].reshape(T * BN, 3) + lm
         vv = X[..., 1].reshape(T * BN, 3)
-        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm)
     return xx, vv, hh
 
 
@@ -97,13 +106,14 @@ def segment_mean_dense(data, seg):
     return F.normalize(M, p=1, dim=1) @ data
 
 
-def gcl(p, h, row, col, x, v, ea, n_sub, recurrent=True, coords_weight=1.0, dense_mean=True):
-    """SEGNO_GCL.forward (gcl.py:111-119), attention off, tanh off."""
+def gcl(p, h, row, col, x, v, ea, n_sub, recurrent=True, coords_weight=1.0, dense_mean=True, tanh=False):
+    """SEGNO_GCL.forward (gcl.py:111-119), attention off; tanh: coord_mlp ends in nn.Tanh (gcl.py:57-59)."""
     diff = x[row] - x[col]
     radial = (diff ** 2).sum(1, keepdim=True)                          # coord2radial gcl.py:104-109
     m = F.silu(_lin(F.silu(_lin(torch.cat([h[row], h[col], radial, ea], 1), p, "module.edge_mlp.0")),
                     p, "module.edge_mlp.2"))
-    trans = (diff * _lin(F.silu(_lin(m, p, "module.coord_mlp.0")), p, "module.coord_mlp.2")).clamp(-100, 100)
+    c = _lin(F.silu(_lin(m, p, "module.coord_mlp.0")), p, "module.coord_mlp.2")
+    trans = (diff * (torch.tanh(c) if tanh else c)).clamp(-100, 100)
     agg = segment_mean_dense(trans, row) if dense_mean else _scatter(trans, row, x.shape[0], True)
     v = v + agg * coords_weight / n_sub
     x = x + v / n_sub
@@ -112,12 +122,12 @@ def gcl(p, h, row, col, x, v, ea, n_sub, recurrent=True, coords_weight=1.0, dens
     return (h + out if recurrent else out), x, v
 
 
-def segno_forward_step(p, his, x, row, col, v, ea, T=10, dense_mean=True, recurrent=True):
+def segno_forward_step(p, his, x, row, col, v, ea, T=10, dense_mean=True, recurrent=True, tanh=False):
     """SEGNO embedding (model.py:73) + forward_step (model.py:95-102): T substeps, dt = 1/T.
     Returns (x, h, v)."""
     h = _lin(his, p, "embedding")
     for _ in range(T):
-        h, x, v = gcl(p, h, row, col, x, v, ea, T, recurrent=recurrent, dense_mean=dense_mean)
+        h, x, v = gcl(p, h, row, col, x, v, ea, T, recurrent=recurrent, dense_mean=dense_mean, tanh=tanh)
     return x, h, v
 
 

@@ -35,6 +35,14 @@ What each fixture pins (reference file:line):
   segno_grad.npz      one SEGNO training step of run_epoch (train_nbody.py:150-178, num_inputs=1)
                       routed through forward_step (model.py:95-102, the integrator): criterion =
                       nn.MSELoss (train_nbody.py:31), loss and every parameter gradient, T=10.
+  egno_norm.npz       EGNO(norm=True) (InvariantScalarNet's F.normalize of the radial input,
+                      basic.py:140-141) at B=2,N=5,T=10, one pair of coincident nodes (radial
+                      below the 1e-12 eps), seed-2 weights: forward + one training step's gradients.
+  egno_notc.npz       EGNO(use_time_conv=False) (no TimeConv modules, egno.py:27-33, 99-107 skipped),
+                      seed-3 weights recorded right after construction: forward + gradients.
+  segno_tanh.npz      SEGNO(tanh=True, norm_diff=True) (coord_mlp ends in nn.Tanh, gcl.py:57-59;
+                      norm_diff is stored and unused), seed-4 weights: forward_step T=10 + one
+                      training step's gradients through it.
   init_seed0.npz      state_dicts produced by EGNO(...)/SEGNO(...) right after
                       torch.manual_seed(0) (RNG-consumption order of the constructors).
 """
@@ -538,7 +546,99 @@ def make_segno_multi(B=2, N=5, T=10, I=3):
         "out::loc_preds": _np(preds), "out::energies": _np(energies), "raw::charges": _np(charges)})
 
 
+def _egno_opt_case(B, N, seed):
+    """prepare_inputs (main_simulation_simple_no.py:311-339) on reference ChargedParticlesSim frames."""
+    loc_all, vel_all, q = charged_trajectories(B, N, seed=seed)
+    start = 30
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start]))
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start]))
+    eao = edge_attr_o(q).reshape(-1, 1)
+    edges = full_edges(B, N)
+    loc_p, vel_p, edge_attr, nodes, loc_mean = egno_main.prepare_inputs(loc, vel, eao, edges, N, 1, torch.tensor(q))
+    return loc_all, start, edges, loc_p, vel_p, edge_attr, nodes, loc_mean
+
+
+def _egno_opt(name, seed, B=2, N=5, T=10, coincide=False, **opts):
+    loc_all, start, edges, x, v, ea, nodes, lm = _egno_opt_case(B, N, 46 + seed)
+    if coincide:   # node 1 of graph 0 on top of node 0 with its velocity: radial 0 < eps on edges
+        x, v = x.clone(), v.clone()   # (0, 1), (1, 0) through the TimeConvs into layer 0
+        x[1] = x[0]
+        v[1] = v[0]
+        nodes = nodes.clone()
+        nodes[1, 0] = nodes[0, 0]
+        r, c = edges
+        ea = ea.clone()
+        ea[:, 1] = ((x[r] - x[c]) ** 2).sum(1)
+    t_out = torch.arange(1, T + 1).repeat(B, 1)
+    t_in = torch.zeros(B, dtype=torch.long)
+    torch.manual_seed(seed)
+    model = EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
+                 num_timesteps=T, time_emb_dim=32, **opts)
+    fx = dict(_sd(model))
+    model.eval()
+    with torch.no_grad():
+        xo, vo, ho = model(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_in=t_in, timesteps_out=t_out)
+    model.train()
+    model.zero_grad()
+    loc_true = torch.tensor(loc_all[:, start + 1:start + 1 + T]).transpose(1, 2)   # [B, N, T, 3]
+    xp, _, _ = model(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_in=t_in, timesteps_out=t_out)
+    xp = _to_dense_batch(xp.reshape(T, -1, 3).transpose(0, 1), torch.arange(B).repeat_interleave(N))[0]
+    loss = torch.nn.MSELoss(reduction="none")(xp, loc_true).mean((0, 1, 3)).mean()   # :267-277
+    loss.backward()
+    fx.update({"cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T),
+               "in::x": _np(x), "in::h": _np(nodes), "in::v": _np(v), "in::loc_mean": _np(lm),
+               "in::edge_attr": _np(ea), "in::row": _np(edges[0]), "in::col": _np(edges[1]),
+               "in::t_out": _np(t_out), "in::loc_true": _np(loc_true),
+               "out::x": _np(xo), "out::v": _np(vo), "out::h": _np(ho), "out::loss": np.array(float(loss))})
+    for k, p in model.named_parameters():
+        fx["grad::" + k] = _np(p.grad) if p.grad is not None else np.zeros(tuple(p.shape), np.float32)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **fx)
+
+
+def make_segno_tanh(B=2, N=5, T=10, seed=4):
+    loc_all, vel_all, q = charged_trajectories(B, N, seed=50)
+    start = 20
+    edges = full_edges(B, N)
+    rows, cols = edges
+    loc = torch.tensor(np.ascontiguousarray(loc_all[:, start])).reshape(-1, 3)
+    vel = torch.tensor(np.ascontiguousarray(vel_all[:, start])).reshape(-1, 3)
+    loc_end = torch.tensor(np.ascontiguousarray(loc_all[:, start + T])).reshape(-1, 3)
+    charges = torch.tensor(q).reshape(-1, 1)
+    h = torch.sqrt(torch.sum(vel ** 2, dim=1)).unsqueeze(-1)                     # train_nbody.py:121
+    edge_attr = torch.cat([charges[rows] * charges[cols],
+                           torch.sum((loc[rows] - loc[cols]) ** 2, 1).unsqueeze(1)], 1)   # :123
+    torch.manual_seed(seed)
+    model = SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True,
+                  norm_diff=True, tanh=True, device="cpu", varDT=False, multiple_agg=None)
+    fx = dict(_sd(model))
+    edge_index = torch.stack(edges)
+    model.train()
+    model.zero_grad()
+    hh = model.embedding(h)
+    x_pred, h_pred, v_pred = model.forward_step(hh, loc, edge_index, vel, edge_attr, T=T)
+    loss = torch.nn.MSELoss()(x_pred, loc_end)
+    loss.backward()
+    fx.update({"cfg::B": np.array(B), "cfg::N": np.array(N), "cfg::T": np.array(T),
+               "in::x": _np(loc), "in::v": _np(vel), "in::his": _np(h), "in::edge_attr": _np(edge_attr),
+               "in::row": _np(rows), "in::col": _np(cols), "in::loc_end": _np(loc_end),
+               "out::x": _np(x_pred), "out::h": _np(h_pred), "out::v": _np(v_pred),
+               "out::loss": np.array(float(loss))})
+    for k, p in model.named_parameters():
+        if p.grad is not None:
+            fx["grad::" + k] = _np(p.grad)
+    np.savez_compressed(os.path.join(HERE, "segno_tanh.npz"), **fx)
+
+
+def make_options():
+    _egno_opt("egno_norm", 2, coincide=True, norm=True)
+    _egno_opt("egno_notc", 3, use_time_conv=False)
+    make_segno_tanh()
+
+
 if __name__ == "__main__":
+    if sys.argv[1:] == ["options"]:
+        make_options()
+        sys.exit(0)
     if sys.argv[1:] == ["segno_multi"]:
         make_segno_multi()
         sys.exit(0)

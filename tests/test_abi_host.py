@@ -106,7 +106,9 @@ def test_unsupported_configs_raise():
     # num_inputs > 1 is supported (inference): the embedding takes both time embeddings (egno.py:12-16)
     assert _egno_ctor(num_inputs=3).embedding.weight.shape == (64, 2 + 2 * 32)
     with pytest.raises(NotImplementedError):
-        pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, tanh=True)
+        _egno_ctor(flat=True)
+    with pytest.raises(NotImplementedError):
+        pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=32)
     with pytest.raises(ValueError):
         pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, multiple_agg="max")
 

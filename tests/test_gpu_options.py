@@ -1,0 +1,206 @@
+"""GPU parity of the reference constructor options (tests/test_options.py pins the oracle side):
+EGNO norm=True (radial input normalised, basic.py:140-141), EGNO use_time_conv=False
+(egno.py:27-33, 99-107 skipped), SEGNO tanh=True (coord_mlp ends in nn.Tanh, gcl.py:57-59) --
+forward and training gradients through the HIP kernels.
+
+Bars (max-norm relative): 1e-5 against the reference's own outputs / autograd gradients
+(egno_norm / egno_notc / segno_tanh fixtures) and against float64 references on other shapes.
+"""
+import numpy as np
+import pytest
+import torch
+
+import no_node_comparison_amd as pkg
+from oracle import egno as oe
+from oracle import torch_ref as tr
+from tests.conftest import check_rel, load_golden, params_of
+from tests.test_gpu_parity import DEV, _dev, _egno_case
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+OPTS = {"egno_norm": dict(norm=True), "egno_notc": dict(use_time_conv=False)}
+
+
+def _egno(opts, sd=None, seed=0, T=10, num_inputs=1):
+    torch.manual_seed(seed)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2, num_timesteps=T,
+                 time_emb_dim=32, num_inputs=num_inputs, device=DEV, **opts)
+    if sd is not None:
+        m.load_state_dict({k: torch.tensor(v) for k, v in sd.items()})
+    return m
+
+
+def _run(m, inp):
+    return m(inp["x"], inp["h"], [inp["row"], inp["col"]], inp["edge_fea"], v=inp["v"], loc_mean=inp["loc_mean"],
+             timesteps_out=inp["t_out"])
+
+
+def _golden_inputs(fx):
+    inp = {k: _dev(fx["in::" + k]) for k in ("x", "h", "row", "col", "edge_attr", "v", "loc_mean", "t_out")}
+    inp["edge_fea"] = inp.pop("edge_attr")
+    return inp
+
+
+@pytest.mark.parametrize("name", sorted(OPTS))
+def test_egno_option_forward_and_gradients_match_reference_golden(name):
+    fx = load_golden(name)
+    B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
+    m = _egno(OPTS[name], params_of(fx)).eval()
+    inp = _golden_inputs(fx)
+    with torch.no_grad():
+        x, v, h = _run(m, inp)
+    check_rel(f"{name} x", x.cpu(), fx["out::x"], TOL)
+    check_rel(f"{name} v", v.cpu(), fx["out::v"], TOL)
+    check_rel(f"{name} h", h.cpu(), fx["out::h"], TOL)
+    m.train()
+    m.zero_grad(set_to_none=True)
+    x, _, _ = _run(m, inp)
+    pred = x.reshape(T, B, N, 3).permute(1, 2, 0, 3)
+    loss = ((pred - _dev(fx["in::loc_true"])) ** 2).mean((0, 1, 3)).mean()
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(float(loss.detach()) - float(fx["out::loss"])) <= 1e-5 * abs(float(fx["out::loss"]))
+    for k, p in m.named_parameters():
+        ref = fx["grad::" + k]
+        if np.abs(ref).max() == 0:
+            assert p.grad is None or float(p.grad.abs().max()) <= 1e-6, k
+        else:
+            check_rel(f"{name} grad {k}", p.grad, ref, TOL)
+
+
+@pytest.mark.parametrize("name", sorted(OPTS))
+@pytest.mark.parametrize("B,N", [(64, 20), (3, 7)])
+def test_egno_option_forward_matches_f64_oracle(name, B, N):
+    T = 10
+    m = _egno(OPTS[name], seed=B + N).eval()
+    case = _egno_case(B, N, T, seed=N + 1)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    f64 = {k: (v.astype(np.float64) if k not in ("row", "col", "t_out") else v) for k, v in case.items()}
+    xr, vr, hr = oe.egno_forward(p, **f64, T=T, **OPTS[name])
+    with torch.no_grad():
+        x, v, h = _run(m, {k: _dev(val) for k, val in case.items()})
+    check_rel("x", x.cpu(), xr, TOL)
+    check_rel("v", v.cpu(), vr, TOL)
+    check_rel("h", h.cpu(), hr, TOL)
+
+
+@pytest.mark.parametrize("name", sorted(OPTS))
+def test_egno_option_gradients_match_f64_autograd(name):
+    B, N, T = 6, 20, 10
+    m = _egno(OPTS[name], seed=7).train()
+    case = _egno_case(B, N, T, seed=9)
+    target = np.random.default_rng(3).standard_normal((B, N, T, 3)).astype(np.float32)
+    m.zero_grad(set_to_none=True)
+    x, _, _ = _run(m, {k: _dev(v) for k, v in case.items()})
+    loss = ((x.reshape(T, B, N, 3).permute(1, 2, 0, 3) - _dev(target)) ** 2).mean((0, 1, 3)).mean()
+    loss.backward()
+    torch.cuda.synchronize()
+    dt = torch.float64
+    p = {k: v.detach().cpu().to(dt).requires_grad_(True) for k, v in m.state_dict().items()}
+    t = {k: torch.tensor(v).to(dt) if v.dtype.kind == "f" else torch.tensor(v) for k, v in case.items()}
+    xr, _, _ = tr.egno_forward(p, t["x"], t["h"], t["row"], t["col"], t["edge_fea"], t["v"], t["loc_mean"],
+                               t["t_out"], T=T, **OPTS[name])
+    lr = ((xr.reshape(T, B, N, 3).permute(1, 2, 0, 3) - torch.tensor(target).to(dt)) ** 2).mean((0, 1, 3)).mean()
+    lr.backward()
+    assert abs(float(loss.detach()) - float(lr.detach())) <= 1e-5 * abs(float(lr.detach()))
+    for k, q in m.named_parameters():
+        ref = p[k].grad
+        if ref is None or float(ref.abs().max()) == 0:
+            assert q.grad is None or float(q.grad.abs().max()) <= 1e-6, k
+            continue
+        check_rel(f"{name} grad {k}", q.grad, ref, TOL)
+
+
+def test_egno_no_time_conv_multi_input_matches_oracle():
+    """use_time_conv=False with num_inputs = 3 (egno.py:44-96 without the TimeConvs)."""
+    B, N, T, I = 2, 6, 10, 3
+    m = _egno(OPTS["egno_notc"], seed=21, num_inputs=I).eval()
+    rng = np.random.default_rng(4)
+    x = rng.standard_normal((I, B * N, 3)).astype(np.float32)
+    v = rng.standard_normal((I, B * N, 3)).astype(np.float32) * 0.5
+    h = np.concatenate([np.linalg.norm(v, axis=-1, keepdims=True), np.ones((I, B * N, 1), np.float32)], -1)
+    row, col = tr.full_edges(B, N)
+    ea = rng.standard_normal((I, B * N * (N - 1), 2)).astype(np.float32)
+    t_in = np.tile(np.array([-2.0, -1.0, 0.0], np.float32), (B, 1))
+    t_out = np.tile(np.arange(1, T + 1, dtype=np.float32), (B, 1))
+    p = {k: q.detach().cpu().numpy().astype(np.float64) for k, q in m.state_dict().items()}
+    xr, vr, hr = oe.egno_forward_multi(p, x.astype(np.float64), h.astype(np.float64), row.numpy(), col.numpy(),
+                                       ea.astype(np.float64), v.astype(np.float64), None, t_in, t_out, T=T,
+                                       use_time_conv=False)
+    with torch.no_grad():
+        xo, vo, ho = m(_dev(x), _dev(h), [_dev(row), _dev(col)], _dev(ea), v=_dev(v), loc_mean=None,
+                       timesteps_in=_dev(t_in), timesteps_out=_dev(t_out))
+    check_rel("x", xo.cpu(), xr, TOL)
+    check_rel("v", vo.cpu(), vr, TOL)
+    check_rel("h", ho.cpu(), hr, TOL)
+
+
+def test_egno_no_time_conv_rollout_first_segment_is_the_forward():
+    """rollout_fn (main_simulation_simple_no.py:342-384) through the native driver with
+    use_time_conv=False: segment 0 is exactly the model's forward."""
+    B, N, T = 4, 20, 10
+    m = _egno(OPTS["egno_notc"], seed=5).eval()
+    case = _egno_case(B, N, T, seed=6)
+    inp = {k: _dev(v) for k, v in case.items()}
+    loc_p = inp["x"]
+    with torch.no_grad():
+        x, _, _ = _run(m, inp)
+        t_full = _dev(np.tile(np.arange(1, 2 * T + 1), (B, 1)))
+        preds, _, _ = pkg.harness.egno_rollout(m, inp["h"], loc_p, [inp["row"], inp["col"]], inp["v"],
+                                               inp["edge_fea"][:, :1].contiguous(), inp["edge_fea"], None, N, 2, B,
+                                               charges=inp["h"][:, 1:2].contiguous(), num_steps=T,
+                                               timesteps_out=t_full)
+    torch.cuda.synchronize()
+    assert torch.equal(preds[:T].reshape(-1, 3), x)
+    assert bool(torch.isfinite(preds).all())
+
+
+@pytest.mark.parametrize("B,N,T", [(2, 5, 10), (16, 20, 10)])
+def test_segno_tanh_matches_golden_and_f64(B, N, T):
+    fx = load_golden("segno_tanh")
+    torch.manual_seed(4)
+    m = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=8, recurrent=True, tanh=True, norm_diff=True,
+                  device=DEV)
+    if (B, N) == (int(fx["cfg::B"]), int(fx["cfg::N"])):
+        m.load_state_dict({k: torch.tensor(v) for k, v in params_of(fx).items()})
+        his, x, v, ea = (torch.tensor(fx[k]) for k in ("in::his", "in::x", "in::v", "in::edge_attr"))
+        r, c = torch.tensor(fx["in::row"]), torch.tensor(fx["in::col"])
+        target = torch.tensor(fx["in::loc_end"])
+    else:
+        g = torch.Generator().manual_seed(B)
+        x = torch.randn(B * N, 3, generator=g) * 1.5
+        v = torch.randn(B * N, 3, generator=g) * 0.5
+        q = torch.randint(0, 2, (B * N, 1), generator=g).float() * 2 - 1
+        r, c = tr.full_edges(B, N)
+        ea = torch.cat([q[r] * q[c], ((x[r] - x[c]) ** 2).sum(1, keepdim=True)], 1)
+        his = v.norm(dim=1, keepdim=True)
+        target = x + 0.3 * v
+    m.train()
+    m.zero_grad(set_to_none=True)
+    xo, ho, vo = m(_dev(his), _dev(x), [_dev(r), _dev(c)], _dev(v), _dev(ea), T=T)
+    loss = torch.nn.functional.mse_loss(xo, _dev(target))
+    loss.backward()
+    torch.cuda.synchronize()
+    dt = torch.float64
+    p = {k: q.detach().cpu().to(dt).requires_grad_(True) for k, q in m.state_dict().items()}
+    xr, hr, vr = tr.segno_forward_step(p, his.to(dt), x.to(dt), r, c, v.to(dt), ea.to(dt), T=T, dense_mean=False,
+                                       tanh=True)
+    lr = torch.nn.functional.mse_loss(xr, target.to(dt))
+    lr.backward()
+    check_rel("x", xo, xr.detach(), TOL)
+    check_rel("h", ho, hr.detach(), TOL)
+    check_rel("v", vo, vr.detach(), TOL)
+    if (B, N) == (int(fx["cfg::B"]), int(fx["cfg::N"])):
+        check_rel("x vs reference", xo, fx["out::x"], TOL)
+        assert abs(float(loss.detach()) - float(fx["out::loss"])) <= 1e-5 * abs(float(fx["out::loss"]))
+    n = 0
+    for k, q in m.named_parameters():
+        ref = p[k].grad
+        if ref is None or float(ref.abs().max()) == 0:
+            assert q.grad is None or float(q.grad.abs().max()) == 0, k
+            continue
+        n += 1
+        check_rel(f"tanh grad {k}", q.grad, ref, TOL)
+        if (B, N) == (int(fx["cfg::B"]), int(fx["cfg::N"])):
+            check_rel(f"tanh grad {k} vs reference", q.grad, fx["grad::" + k], TOL)
+    assert n == 14
