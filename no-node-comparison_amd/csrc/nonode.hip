@@ -613,9 +613,14 @@ size_t layer_lds_floats(int ct, int s_rows) {
 // budget), two units per iteration.
 // NW = 4: one wave per SIMD (512-register budget), two units per iteration; NW = 8: two waves per
 // SIMD (256 registers each), one unit per iteration, fragments and biases read from LDS.
-template <int VARIANT, int KF, int NW>
-__global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
+// OPT: the variant's constructor option (EGNO norm=True: radial input normalised; SEGNO tanh=True:
+// coordinate output through tanh), compiled into its own copy of the body so the default path's
+// hot loop carries no per-edge select; the kernel picks the copy once from the blob's flag.
+template <int VARIANT, int KF, int NW, bool OPT>
+__device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   constexpr bool PAIR = NW == 4;
+  constexpr bool rnorm = OPT && VARIANT == EGNO;    // basic.py:140-141
+  constexpr bool ctanh = OPT && VARIANT == SEGNO;   // gcl.py:57-59
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
@@ -633,8 +638,6 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
     reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_FEAT)[tid];
   const float bc2 = p.blob[OFF_SCAL + 0];
   const float bv2 = p.blob[OFF_SCAL + 1];
-  const bool rnorm = p.blob[OFF_SCAL + SC_NORM] != 0.f;                        // wave-uniform
-  const bool ctanh = VARIANT == SEGNO && p.blob[OFF_SCAL + SC_TANH] != 0.f;    // wave-uniform
   const float* vFEAT_ = sV;
   const float* vB2_ = sV + 512 + V_B2 * 64;
   const float* vBC1_ = sV + 512 + V_BC1 * 64;
@@ -839,7 +842,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
           const float* xs = sX + sl * 4;
           r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
           float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
-          if (rnorm) d2 = radial_norm(d2);
+          if constexpr (rnorm) d2 = radial_norm(d2);
           f4 q4[4];
           load_ecl(q4, sQ + sl * ROWP, g);
           load_ecl(a, Prow, g);
@@ -857,7 +860,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
         auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
           silu_ecl(c1);
           float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2_, g)) + bc2;
-          if (ctanh) c = tanhf(c);
+          if constexpr (ctanh) c = tanhf(c);
           float f0 = r0 * c, f1 = r1 * c, f2 = r2 * c;
           if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
             f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -887,7 +890,7 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
             r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
             float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
             ok = xs[3] * xr3 != 0.f && __builtin_isfinite(d2);   // finite inputs: a guard recompute can help
-            if (rnorm) d2 = radial_norm(d2);
+            if constexpr (rnorm) d2 = radial_norm(d2);
             load_ecl(a, sQ + sl * ROWP, g);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
@@ -904,7 +907,8 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
                             float& c) __attribute__((always_inline)) {
             silu_ecl(c1);
             c = dot_r(c1, rWC2) + bc2;   // the guard tests c before the tanh (tanh(inf) = 1)
-            const float ct = ctanh ? tanhf(c) : c;
+            float ct = c;
+            if constexpr (ctanh) ct = tanhf(c);
             f0 = r0 * ct; f1 = r1 * ct; f2 = r2 * ct;
             if (VARIANT == SEGNO) {   // gcl.py:99-100 clamps every edge's translation
               f0 = fminf(fmaxf(f0, -100.f), 100.f);
@@ -1250,6 +1254,14 @@ __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
   }
   }
   STAMP_FLUSH
+}
+
+template <int VARIANT, int KF, int NW>
+__global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
+  if (p.blob[OFF_SCAL + (VARIANT == SEGNO ? SC_TANH : SC_NORM)] != 0.f)   // wave-uniform
+    egnn_layer_body<VARIANT, KF, NW, true>(p);
+  else
+    egnn_layer_body<VARIANT, KF, NW, false>(p);
 }
 
 // ---- temporal spectral layers -----------------------------------------------------------------

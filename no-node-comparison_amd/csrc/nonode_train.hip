@@ -501,8 +501,11 @@ __device__ __forceinline__ float edge_sum16(float v) {
 // Two launches per layer (register budget: one wave cannot hold both 64x64 accumulators next to the
 // per-edge working set): PASS 0 recomputes the edge up to gz3 and accumulates dWc1, dbc1, dwc2,
 // dbc2; PASS 1 does the whole reverse pass with dW2, db2, the W1 scalar columns and GA / GB / GX.
-template <int NE, int PASS>
-__global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
+// OPT: 1 = EGNO norm=True (radial input normalised, basic.py:140-141), 2 = SEGNO tanh=True (coordinate
+// output through tanh, gcl.py:57-59); each its own copy of the body (no per-edge select by default)
+template <int NE, int PASS, int OPT>
+__device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
+  constexpr bool rnorm = OPT == 1, ctanh = OPT == 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NW = 4;
   constexpr int NF = 1 + NE;   // scalar inputs of edge W1: |r|^2, e_0 .. e_{NE-1}
@@ -525,8 +528,6 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   float* myGX = sGX + wave * p.s_max * 4;
   const float* bb = p.bb;
   const float bc2 = bb[BOFF_SCAL + 0];
-  const bool rnorm = bb[BOFF_SCAL + SC_NORM] != 0.f;   // EGNO norm=True (basic.py:140-141)
-  const bool ctanh = bb[BOFF_SCAL + SC_TANH] != 0.f;   // SEGNO tanh=True (gcl.py:57-59)
   const float* wW2 = bb + BOFF_W2;
   const float* wWc1 = bb + BOFF_WC1;
   {
@@ -627,7 +628,8 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       const float s2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
       const float* efp = p.ef + (((size_t)(gr % p.ef_mod) * N + n) * Nm1 + jj) * NE;
       float fe[NF];
-      fe[0] = rnorm ? radial_norm(s2) : s2;
+      fe[0] = s2;
+      if constexpr (rnorm) fe[0] = radial_norm(s2);
 #pragma unroll
       for (int kk = 0; kk < NE; ++kk) fe[1 + kk] = efp[kk];
       float ev[2];
@@ -690,7 +692,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         f4 c1[4];
         silu_keep(z3, sg3, c1);
         c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
-        if (ctanh) c = tanhf(c);
+        if constexpr (ctanh) c = tanhf(c);
       }
       // reverse: f = r c (SEGNO: clamp(r c, +-100) per edge)
       float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
@@ -700,7 +702,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
         gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
       }
       float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
-      if (ctanh) gc *= 1.f - c * c;   // through the tanh: gc is the gradient of the MLP output
+      if constexpr (ctanh) gc *= 1.f - c * c;   // through the tanh: gc is the gradient of the MLP output
       float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
       // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
       f4 gz3[4];
@@ -740,7 +742,7 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
       if (!(p.dbg & 8)) wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
       // s = |r|^2 input column
       float gs = dot_vp(gz1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64, g);
-      if (rnorm) gs = s2 < 1e-12f ? gs * 1e12f : 0.f;   // d normalize(s) / ds: 1 / eps below eps, else 0
+      if constexpr (rnorm) gs = s2 < 1e-12f ? gs * 1e12f : 0.f;   // d normalize(s) / ds: 1 / eps below eps, else 0
       gr0 = fmaf(2.f * gs, r0, gr0);
       gr1 = fmaf(2.f * gs, r1, gr1);
       gr2 = fmaf(2.f * gs, r2, gr2);
@@ -832,6 +834,13 @@ __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   float* dst = p.wpart + (size_t)blockIdx.x * EW_STRIDE;
   block_partial(smem, dst, PASS == 0 ? EW_WC1 : EW_W2, PASS == 1 ? EW_WC1 : EW_WC2 + 65);
   if (PASS == 1) block_partial(smem, dst, EW_FEAT, EW_FEAT + 64 * (NF + 1));
+}
+
+template <int NE, int PASS>
+__global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
+  if (p.bb[BOFF_SCAL + SC_NORM] != 0.f) edge_bwd_body<NE, PASS, 1>(p);        // wave-uniform
+  else if (p.bb[BOFF_SCAL + SC_TANH] != 0.f) edge_bwd_body<NE, PASS, 2>(p);
+  else edge_bwd_body<NE, PASS, 0>(p);
 }
 // per-pass chunk size (tiles per LDS chunk) and dynamic LDS bytes
 int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_max_out, size_t* lds_out) {
