@@ -255,23 +255,58 @@ struct NodeBwdArgs {
   const float* bb;                                                   // backward blob
   float* gv; float* gF; float* gM; float* ghp;                       // outputs
   float* op_gt; float* op_t; float* op_gphi; float* op_z; float* op_gz;   // GEMM operands
+  float* GB; float* GX;                                              // zeroed for the edge backward
 };
 
-__global__ __launch_bounds__(256) void node_bwd_kernel(NodeBwdArgs p) {
+// Persistent: one workgroup (8 waves, two per SIMD) per CU stages the six node-side fragment
+// matrices in LDS once (112 KB: WV1, WN1, WV1^T, WN2^T, WN1^T h / m columns) and its waves walk
+// 16-node tiles. (One tile per wave with the fragments read from L2 moved ~128 KB of fragments per
+// 16 nodes: 92 us per C4 layer, L2-bound.) Also zeroes the edge backward's GB / GX rows.
+constexpr int NB_WAVES = 8;
+constexpr int NB_LDS_FLOATS = (BOFF_WN1 + 8192 - BOFF_WV1) + (BOFF_WN1TM + 4096 - BOFF_WV1T);   // 28672
+__global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
-  const int tile = blockIdx.x * 4 + wave;
+  {
+    const float* bb = p.bb;
+    constexpr int n1 = BOFF_WN1 + 8192 - BOFF_WV1, n2 = BOFF_WN1TM + 4096 - BOFF_WV1T;
+    const f4* s1 = reinterpret_cast<const f4*>(bb + BOFF_WV1);
+    const f4* s2 = reinterpret_cast<const f4*>(bb + BOFF_WV1T);
+    for (int i = threadIdx.x; i < n1 / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem)[i] = s1[i];
+    for (int i = threadIdx.x; i < n2 / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem + n1)[i] = s2[i];
+  }
+  __syncthreads();
+  const float* sWV1_ = smem;                                  // [BOFF_WV1, BOFF_WN1 + 8192) staged
+  const float* sWN1_ = smem + (BOFF_WN1 - BOFF_WV1);
+  const float* sT = smem + (BOFF_WN1 + 8192 - BOFF_WV1);    // [BOFF_WV1T, BOFF_WN1TM + 4096) staged
+  const float* sWV1T_ = sT;
+  const float* sWN2T_ = sT + (BOFF_WN2T - BOFF_WV1T);
+  const float* sWN1TH_ = sT + (BOFF_WN1TH - BOFF_WV1T);
+  const float* sWN1TM_ = sT + (BOFF_WN1TM - BOFF_WV1T);
+  const int ntile = (p.n + 15) >> 4;
+#pragma unroll 1
+  for (int tile = blockIdx.x * NB_WAVES + wave; tile < ntile; tile += gridDim.x * NB_WAVES) {
+  // loop-invariant weight reads stay in the loop (hoisted, the bias vectors and fragments would
+  // pin registers across the tiles and spill): opaque zero offset
+  int off = 0;
+  asm volatile("" : "+v"(off));
+  const float* bb = p.bb + off;
+  const float* sWV1 = sWV1_ + off;
+  const float* sWN1 = sWN1_ + off;
+  const float* sWV1T = sWV1T_ + off;
+  const float* sWN2T = sWN2T_ + off;
+  const float* sWN1TH = sWN1TH_ + off;
+  const float* sWN1TM = sWN1TM_ + off;
   const int r0 = tile * 16;
-  if (r0 >= p.n) return;
   const int r = min(r0 + e, p.n - 1);
   const bool valid = r0 + e < p.n;
-  const float* bb = p.bb;
   f4 hr[4], Mr[4];
   load_ecl(hr, p.h + (size_t)r * HID, g);
   load_ecl(Mr, p.M + (size_t)r * HID, g);
   // phi_v(h) = wv2 . SiLU(WV1 h + bv1) + bv2
   f4 tp[4];
   load_vp(tp, bb + BOFF_VEC + BV_BV1 * 64, g);
-  mfma_dense<4>(tp, bb + BOFF_WV1, hr, lane);
+  mfma_dense<4>(tp, sWV1, hr, lane);
   f4 t[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) t[mt] = tp[mt];
@@ -294,14 +329,14 @@ __global__ __launch_bounds__(256) void node_bwd_kernel(NodeBwdArgs p) {
   mul_dsilu(gt, tp);
   f4 gh[4];
   zero4(gh);
-  mfma_dense<4>(gh, bb + BOFF_WV1T, gt, lane);
+  mfma_dense<4>(gh, sWV1T, gt, lane);
   // node MLP: z = SiLU(WN1 [h, M] + bn1), h' = WN2 z + bn2
   f4 in8[8];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
   f4 zp[4];
   load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
-  mfma_dense<8>(zp, bb + BOFF_WN1, in8, lane);
+  mfma_dense<8>(zp, sWN1, in8, lane);
   f4 z[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
@@ -309,12 +344,12 @@ __global__ __launch_bounds__(256) void node_bwd_kernel(NodeBwdArgs p) {
   f4 gho[4], gz[4];
   load_ecl(gho, p.gho + (size_t)r * HID, g);
   zero4(gz);
-  mfma_dense<4>(gz, bb + BOFF_WN2T, gho, lane);
+  mfma_dense<4>(gz, sWN2T, gho, lane);
   mul_dsilu(gz, zp);
-  mfma_dense<4>(gh, bb + BOFF_WN1TH, gz, lane);
+  mfma_dense<4>(gh, sWN1TH, gz, lane);
   f4 gM[4];
   zero4(gM);
-  mfma_dense<4>(gM, bb + BOFF_WN1TM, gz, lane);
+  mfma_dense<4>(gM, sWN1TM, gz, lane);
   if (valid) {
     const size_t o = (size_t)r * HID;
     store_ecl(p.ghp + o, gh, g);
@@ -323,14 +358,29 @@ __global__ __launch_bounds__(256) void node_bwd_kernel(NodeBwdArgs p) {
     store_ecl(p.op_t + o, t, g);
     store_ecl(p.op_z + o, z, g);
     store_ecl(p.op_gz + o, gz, g);
+    const f4 z4[4] = {};
+    store_ecl(p.GB + o, z4, g);                          // the edge backward's sender sums start at 0
     if (g == 0) {
       p.gv[(size_t)r * 3 + 0] = p.gvo[(size_t)r * 3 + 0] + phi * gx0;
       p.gv[(size_t)r * 3 + 1] = p.gvo[(size_t)r * 3 + 1] + phi * gx1;
       p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
       *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
+      *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = f4{0.f, 0.f, 0.f, 0.f};
       p.op_gphi[r] = gphi;
     }
   }
+  }
+}
+
+int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s) {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hipFuncSetAttribute((const void*)node_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, NB_LDS_FLOATS * 4);
+  });
+  const int want = (ntile + NB_WAVES - 1) / NB_WAVES;
+  const int G = want < num_cus() ? want : num_cus();
+  hipLaunchKernelGGL(node_bwd_kernel, dim3(G), dim3(NB_WAVES * 64), NB_LDS_FLOATS * 4, s, a);
+  return check_launch("node_bwd_kernel");
 }
 
 // ---- edge backward (basic.py:107-144, 167-173 reversed) ----------------------------------------
@@ -559,6 +609,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   const int nend = (int)(((long long)(blockIdx.x + 1) * p.n_graphs) / G) * N;
   const int ntw = (nend - nb + 15) >> 4;
   const int nch = (ntw + p.ct - 1) / p.ct;
+  STAMP_DECL   // diagnostic section stamps (NONODE_STAMP builds): PASS 1 slots 0-12, PASS 0 13-15
   for (int ci = 0; ci < nch; ++ci) {
     const int c0 = (ci * ntw) / nch;
     const int ctc = ((ci + 1) * ntw) / nch - c0;
@@ -604,7 +655,9 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         }
       }
     }
+    STAMP(PASS ? 8 : 14);
     __syncthreads();
+    STAMP(PASS ? 9 : 14);
     // ---- B: one unit (16 edges: receivers of a tile x sender offset k) at a time ----
     const int U = ctc * Nm1;
     for (int u = wave; u < U; u += NW) {
@@ -661,6 +714,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       bool bigA;
       {
         f4 a[4];
+        STAMP(PASS ? 0 : 13);
         silu_keep(z1, sg1, a);
         bigA = __any(amax_ecl(a) > H16_LIMIT);
         load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
@@ -676,6 +730,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       bool bigM;
       {
         f4 m[4];
+        STAMP(PASS ? 1 : 13);
         silu_keep(z2, sg2, m);
         bigM = __any(amax_ecl(m) > H16_LIMIT);
         load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
@@ -690,6 +745,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       float c;
       {
         f4 c1[4];
+        STAMP(PASS ? 2 : 13);
         silu_keep(z3, sg3, c1);
         c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
         if constexpr (ctanh) c = tanhf(c);
@@ -719,13 +775,16 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
         sGC += gc;
+        STAMP(15);
         continue;
       }
+      STAMP(3);
       // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m)
       f4 gz2[4];
       load_ecl(gz2, sGM + rl * ROWP, g);
       if (!rvalid) zero4(gz2);
       if (!(p.dbg & 32)) mm64_cs(gz2, hWc1T, gz3, lane);
+      STAMP(4);
       mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
       // dW2 += gz2 (x) a ; db2 += gz2
       if (!(p.dbg & 4)) {
@@ -734,9 +793,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
         wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA);
       }
+      STAMP(5);
       f4 gz1[4];
       zero4(gz1);
       if (!(p.dbg & 64)) mm64_cs(gz1, hW2T, gz2, lane);
+      STAMP(6);
       mul_dsilu_s(gz1, z1, sg1);                 // a = SiLU(z1)
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
       if (!(p.dbg & 8)) wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
@@ -768,8 +829,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           *xs -= f4{gr0, gr1, gr2, 0.f};
         }
       }
+      STAMP(7);
     }
+    STAMP(PASS ? 7 : 15);
     __syncthreads();
+    STAMP(PASS ? 10 : 14);
     if (PASS == 0 || (p.dbg & 16)) continue;
     // ---- C: write the chunk's sums (senders can be shared with the next chunk: atomics) ----
     // (the four wave-private tables added in wave order)
@@ -791,6 +855,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       atomicAdd(p.GX + (size_t)(s0 + sl) * 4 + d, ((sGX[o] + sGX[st + o]) + sGX[2 * st + o]) + sGX[3 * st + o]);
     }
     __syncthreads();
+    STAMP(11);
   }
   // ---- D: weight-gradient partials: each wave's to LDS, then one per block (waves added in order) ----
   __syncthreads();   // the last chunk's tables are dead: reuse the LDS
@@ -834,6 +899,8 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   float* dst = p.wpart + (size_t)blockIdx.x * EW_STRIDE;
   block_partial(smem, dst, PASS == 0 ? EW_WC1 : EW_W2, PASS == 1 ? EW_WC1 : EW_WC2 + 65);
   if (PASS == 1) block_partial(smem, dst, EW_FEAT, EW_FEAT + 64 * (NF + 1));
+  STAMP(12);
+  STAMP_FLUSH
 }
 
 template <int NE, int PASS>
@@ -1101,6 +1168,28 @@ __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
 
 // dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
 // strided partial lanes, combined in a fixed order (deterministic).
+// the TimeConv_x weight gradient from rows_reduce's per-slice sums [nb][io][MMAX_T][2]: one block adds
+// the slices in order and writes g_tconvx [2][2][Mfull][2] whole (modes >= M zero), replacing a
+// memset and four copies
+__global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int nb, int M, int Mfull, float* dst) {
+  __shared__ float red[8][33];
+  constexpr int cnt = 2 * 2 * MMAX_T * 2;
+  const int o = threadIdx.x & 31, lanei = threadIdx.x >> 5;
+  float s = 0.f;
+  for (int r = lanei; r < nb; r += 8) s += part[(size_t)r * cnt + o];
+  red[lanei][o] = s;
+  __syncthreads();
+  for (int d = threadIdx.x; d < 4 * Mfull * 2; d += 256) {
+    const int io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
+    float v = 0.f;
+    if (m < M) {
+      const int k = (io * MMAX_T + m) * 2 + c;
+      for (int q = 0; q < 8; ++q) v += red[q][k];
+    }
+    dst[d] = v;
+  }
+}
+
 __global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst) {
   __shared__ float red[4][64];
   const int per = M * 2 * 4096;
@@ -1190,9 +1279,8 @@ __global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* 
 // for channel 4 il + t; the epilogue maps the accumulator back.
 constexpr int GEMM_UNR = 8;
 template <bool V4>
-__global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__ G, int ldg, int M,
-                                                       const float* __restrict__ A, int lda, int N, long long K,
-                                                       long long kslice, float* partial) {
+__device__ __forceinline__ void gemm_tn_body(const float* __restrict__ G, int ldg, int M, const float* __restrict__ A,
+                                             int lda, int N, long long K, long long kslice, float* partial) {
   const int lane = threadIdx.x & 63, il = lane & 15, kr = lane >> 4;
   const long long gw = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const long long k0 = gw * kslice, k1 = min(K, k0 + kslice);
@@ -1294,16 +1382,38 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
   float* dst = partial + (size_t)blockIdx.x * NO;
   for (int o = threadIdx.x; o < NO; o += 256) dst[o] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
 }
+template <bool V4>
+__global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__ G, int ldg, int M,
+                                                       const float* __restrict__ A, int lda, int N, long long K,
+                                                       long long kslice, float* partial) {
+  gemm_tn_body<V4>(G, ldg, M, A, lda, N, K, kslice, partial);
+}
+
+// Several 64x64 weight-gradient GEMMs over the same K rows in one launch (blockIdx.y = GEMM): their
+// waves are in flight together, which hides the row-load latency a single small GEMM exposes, and
+// one launch replaces several. GEMM j writes its block partials at partial + j * pstride.
+constexpr int GEMM_BATCH_MAX = 6;
+struct GemmBatchArgs {
+  const float* G[GEMM_BATCH_MAX]; const float* A[GEMM_BATCH_MAX];
+  int ldg[GEMM_BATCH_MAX], lda[GEMM_BATCH_MAX];
+  long long K, kslice, pstride;
+  float* partial;
+};
+__global__ __launch_bounds__(256) void gemm_tn_batch(GemmBatchArgs a) {
+  const int j = blockIdx.y;
+  gemm_tn_body<true>(a.G[j], a.ldg[j], 64, a.A[j], a.lda[j], 64, a.K, a.kslice, a.partial + (size_t)j * a.pstride);
+}
 
 // dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
 // partial[b][i][N]. 256 threads = 16 outputs x 16 strided partial sums, combined in a fixed order
 // (deterministic).
 // (columns j >= split go to col1 + (j - split) instead: the [s | ... | e] blocks of edge W1)
-__global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld,
-                                                   int col0, int cs, float* bias, int accumulate, float scale,
-                                                   int split, int col1, long long pstride) {
+__device__ __forceinline__ void gemm_reduce_body(const float* partial, int nblk, int M, int N, float* dst, int ld,
+                                                 int col0, int cs, float* bias, int accumulate, float scale,
+                                                 int split, int col1, long long pstride) {
   __shared__ float red[16][17];
   const int NO = M * (N + 1);
+  if ((int)blockIdx.x * 16 >= NO) return;   // whole block (a batch's grid covers its largest job)
   const int ol = threadIdx.x & 15, part = threadIdx.x >> 4;
   const int o = blockIdx.x * 16 + ol;
   // eight independent partial sums per thread (a fixed tree: deterministic), so the loads of a
@@ -1330,6 +1440,36 @@ __global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nbl
   } else if (bias) {
     bias[i] = accumulate ? bias[i] + s : s;
   }
+}
+__global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld,
+                                                   int col0, int cs, float* bias, int accumulate, float scale,
+                                                   int split, int col1, long long pstride) {
+  gemm_reduce_body(partial, nblk, M, N, dst, ld, col0, cs, bias, accumulate, scale, split, col1, pstride);
+}
+// a batch of reductions in one launch (blockIdx.y = job)
+struct ReduceJob {
+  const float* partial; int nblk, M, N; float* dst; int ld, col0, cs; float* bias; int accumulate; float scale;
+  int split, col1; long long pstride;
+};
+constexpr int REDUCE_BATCH_MAX = 12;
+struct ReduceBatchArgs { ReduceJob j[REDUCE_BATCH_MAX]; };
+__global__ __launch_bounds__(256) void gemm_reduce_batch(ReduceBatchArgs a) {
+  const ReduceJob& r = a.j[blockIdx.y];
+  gemm_reduce_body(r.partial, r.nblk, r.M, r.N, r.dst, r.ld, r.col0, r.cs, r.bias, r.accumulate, r.scale, r.split,
+                   r.col1, r.pstride);
+}
+int launch_reduce_batch(const ReduceJob* jobs, int count, hipStream_t s) {
+  if (count <= 0) return NONODE_OK;
+  if (count > REDUCE_BATCH_MAX) return fail(NONODE_EINVAL, "reduce batch of %d", count);
+  ReduceBatchArgs a{};
+  int gx = 1;
+  for (int i = 0; i < count; ++i) {
+    a.j[i] = jobs[i];
+    const int NO = jobs[i].M * (jobs[i].N + 1);
+    gx = (NO + 15) / 16 > gx ? (NO + 15) / 16 : gx;
+  }
+  hipLaunchKernelGGL(gemm_reduce_batch, dim3(gx, count), dim3(256), 0, s, a);
+  return check_launch("gemm_reduce_batch");
 }
 
 // out[blk][o] = sum over this block's row slice of part[rows][cnt] (cnt <= 32): 256 threads =
@@ -1384,6 +1524,36 @@ struct Gemm {
                        cs, bias, accumulate, scale, split, col1, (long long)NO);
     return check_launch("gemm_reduce");
   }
+  // count 64x64 GEMMs C_j = sum_k G_j[k] (x) A_j[k] over the same K rows in one launch (gemm_tn_batch);
+  // their reductions are appended to red[] (*nred) for one launch_reduce_batch by the caller
+  struct Job { const float* G; int ldg; const float* A; int lda; float* dst; int ld, col0; float* bias; int accumulate; };
+  int batch(const Job* jobs, int count, long long K, ReduceJob* red, int* nred) const {
+    if (count > GEMM_BATCH_MAX) return fail(NONODE_EINVAL, "gemm batch of %d", count);
+    if (K <= 0) return NONODE_OK;
+    GemmBatchArgs a{};
+    for (int j = 0; j < count; ++j) {
+      const Job& b = jobs[j];
+      if (b.ldg % 4 || b.lda % 4 || ((uintptr_t)b.G & 15) || ((uintptr_t)b.A & 15))
+        return fail(NONODE_EINVAL, "gemm batch: unaligned operand");
+      a.G[j] = b.G; a.A[j] = b.A; a.ldg[j] = b.ldg; a.lda[j] = b.lda;
+    }
+    long long waves = (K + 31) / 32;
+    if (waves > max_waves) waves = max_waves;
+    long long kslice = (K + waves - 1) / waves;
+    kslice = (kslice + 4 * GEMM_UNR - 1) / (4 * GEMM_UNR) * (4 * GEMM_UNR);
+    waves = (K + kslice - 1) / kslice;
+    const int nblk = (int)((waves + 3) / 4);
+    constexpr int NO = 64 * 65;
+    a.K = K; a.kslice = kslice; a.pstride = (long long)nblk * NO; a.partial = partial;
+    hipLaunchKernelGGL(gemm_tn_batch, dim3(nblk, count), dim3(256), 0, s, a);
+    if (int rc = check_launch("gemm_tn_batch")) return rc;
+    for (int j = 0; j < count; ++j) {
+      const Job& b = jobs[j];
+      red[(*nred)++] = ReduceJob{partial + (size_t)j * a.pstride, nblk, 64, 64, b.dst, b.ld, b.col0, 1, b.bias,
+                                 b.accumulate, 1.f, 1 << 30, 0, (long long)NO};
+    }
+    return NONODE_OK;
+  }
 };
 
 // ---- state layout of the training forward ---------------------------------------------------------
@@ -1435,7 +1605,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take(BN * 3 * 2 * 2 * MMAX_T * 2);
-  w.partial = take((size_t)(GEMM_MAX_WAVES + 4) * 64 * 65);
+  w.partial = take((size_t)GEMM_BATCH_MAX * (GEMM_MAX_WAVES / 4 + 1) * 64 * 65);   // gemm_tn_batch partials
   w.floats = tot;
   return w;
 }
@@ -1526,27 +1696,31 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
                        time_emb_dim, Bt, h, t_out, st.emb_in, t_in, frames);
     if (int rc = check_launch("emb_in_kernel")) return rc;
   }
+  // EGNN_Layer leaves v unchanged (basic.py:186): layer l's input v is TimeConv_x's output ve[l - 1]
+  // (vs[0] without time convolutions); the last layer writes x_out, h_out directly
   for (int l = 0; l < L; ++l) {
     TconvArgs a{};
     a.BN = BN; a.T = T; a.M = effective_modes(T, modes); a.Mfull = modes;
-    a.h = st.hs + l * n * 64; a.x = st.xs + l * n * 3; a.v = st.vs + l * n * 3; a.lm = loc_mean;
+    a.h = st.hs + l * n * 64; a.x = st.xs + l * n * 3; a.lm = loc_mean;
+    a.v = (l > 0 && tc) ? st.ve + (l - 1) * n * 3 : st.vs;
+    const float *hin, *xin, *vin;
     if (tc) {
       a.wp = tconv_blobs[l]; a.wx = tconvx_w[l]; a.frames = frames;
       a.h_out = st.he + l * n * 64; a.x_out = st.xe + l * n * 3; a.v_out = st.ve + l * n * 3;
       a.mask_out = st.mask + (size_t)l * T * ((BN + 15) / 16) * 16;
       if (int rc = launch_tconv(false, a, s)) return rc;
+      hin = a.h_out; xin = a.x_out; vin = a.v_out;
     } else {   // the layer reads its saved inputs directly (the backward does the same)
-      a.h_out = st.hs + l * n * 64; a.x_out = st.xs + l * n * 3; a.v_out = st.vs + l * n * 3;
+      hin = a.h; xin = a.x; vin = a.v;
     }
-    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, a.h_out, a.x_out, a.v_out, edge_fea, blobs[l], 0.f, 1.f,
-                                    0, st.hs + (l + 1) * n * 64, st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
+    const bool last = l == L - 1;
+    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hin, xin, vin, edge_fea, blobs[l], 0.f,
+                                    1.f, 0, last ? h_out : st.hs + (l + 1) * n * 64,
+                                    last ? x_out : st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
                                     st.Ms + l * n * 64, st.Fs + l * n * 4))
       return rc;
-    hipMemcpyAsync(st.vs + (l + 1) * n * 3, a.v_out, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   }
-  hipMemcpyAsync(x_out, st.xs + L * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  hipMemcpyAsync(v_out, st.vs + L * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  hipMemcpyAsync(h_out, st.hs + L * n * 64, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  hipMemcpyAsync(v_out, tc ? st.ve + (L - 1) * n * 3 : st.vs, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   return check_launch("egno_forward_train copies");
 }
 }  // namespace
@@ -1611,20 +1785,20 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
   TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, emb_cols);
   BwdWs w = bwd_ws(workspace, B, N, T, M);
   Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
+  ReduceJob rjobs[REDUCE_BATCH_MAX];
+  int nred = 0;
   // grads of the final outputs
-  float *gx = w.gx[0], *gv = w.gv[0], *gh = w.gh[0];
-  hipMemcpyAsync(gx, g_x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  if (g_v) hipMemcpyAsync(gv, g_v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  else hipMemsetAsync(gv, 0, n * 3 * sizeof(float), s);
-  if (g_h) hipMemcpyAsync(gh, g_h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  else hipMemsetAsync(gh, 0, n * 64 * sizeof(float), s);
+  // (read in place: the reverse pass only reads the output gradients of a layer)
+  const float *gx = g_x, *gv = g_v, *gh = g_h;
+  if (!g_v) { hipMemsetAsync(w.gv[0], 0, n * 3 * sizeof(float), s); gv = w.gv[0]; }
+  if (!g_h) { hipMemsetAsync(w.gh[0], 0, n * 64 * sizeof(float), s); gh = w.gh[0]; }
   int cur = 0;
   const int ld1 = 2 * HID + 1 + ne;
   for (int l = L - 1; l >= 0; --l) {
     const nonode_layer_grads& lg = layer_grads[l];
     const float* he = (tc ? st.he : st.hs) + l * n * 64;
     const float* xe = (tc ? st.xe : st.xs) + l * n * 3;
-    const float* ve = (tc ? st.ve : st.vs) + l * n * 3;
+    const float* ve = tc ? st.ve + l * n * 3 : st.vs;   // v is unchanged by every layer
     const float* bb = bblobs[l];
     // ---- EGNN_Layer reverse ----
     NodeBwdArgs na;
@@ -1633,10 +1807,8 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     na.gv = w.gve; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp;
     na.op_gt = w.op_gt; na.op_t = w.op_t; na.op_gphi = w.op_gphi; na.op_z = w.op_z; na.op_gz = w.op_gz;
     const int ntile = (int)((n + 15) / 16);
-    hipLaunchKernelGGL(node_bwd_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, na);
-    if (int rc = check_launch("node_bwd_kernel")) return rc;
-    hipMemsetAsync(w.GB, 0, n * 64 * sizeof(float), s);
-    hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
+    na.GB = w.GB; na.GX = w.GX;
+    if (int rc = launch_node_bwd(na, ntile, s)) return rc;
     {
       const int n_graphs = T * B;
       int G = num_cus();
@@ -1650,34 +1822,39 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
       ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
       ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
-      // edge-level weight gradients: fixed-order sums of the G*4 wave partials
+      // edge-level weight gradients: fixed-order sums of the G block partials (launched with the
+      // node-level GEMMs' reductions below)
       const int nparts = G;   // one partial per block
       const int nf = 1 + ne;
       auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int split, int col1) {
-        const int NO = M_ * (N_ + 1);
-        hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, w.wpart + off, nparts, M_, N_, dst,
-                           ld, 0, 1, bias, 0, 1.f, split, col1, (long long)EW_STRIDE);
-        return check_launch("gemm_reduce(edge)");
+        rjobs[nred++] = ReduceJob{w.wpart + off, nparts, M_, N_, dst, ld, 0, 1, bias, 0, 1.f, split, col1,
+                                  (long long)EW_STRIDE};
       };
-      if (int rc = red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 1 << 30, 0)) return rc;
-      if (int rc = red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 1 << 30, 0)) return rc;
-      if (int rc = red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 1 << 30, 0)) return rc;
+      red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 1 << 30, 0);
+      red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 1 << 30, 0);
+      red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 1 << 30, 0);
       // edge Linear 1 scalar columns [s | e] (EGNO order [s, h_i, h_j, e], basic.py:152-154, 170)
-      if (int rc = red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1)) return rc;
+      red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1);
     }
     hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, (int)n, w.ghp, w.GA, w.GB, gx,
                        w.GX, bb, w.ghe, w.gxe);
     if (int rc = check_launch("node_post_kernel")) return rc;
-    // ---- node-level weight gradients of this layer ----
+    // ---- node-level weight gradients of this layer: six 64x64 GEMMs in one launch, their and the
+    // edge-level reductions in another ----
     // edge Linear 1 h_i / h_j blocks; its bias gradient sum_e gz1 = sum_i GA_i comes with the h_i block
-    if (int rc = gemm(w.GA, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1, lg.edge_b1)) return rc;
-    if (int rc = gemm(w.GB, 64, 64, he, 64, 64, (long long)n, lg.edge_w1, ld1, 1 + HID, nullptr)) return rc;
-    if (int rc = gemm(w.op_gt, 64, 64, he, 64, 64, (long long)n, lg.vel_w1, 64, 0, lg.vel_b1)) return rc;
+    {
+      const Gemm::Job jobs[6] = {
+          {w.GA, 64, he, 64, lg.edge_w1, ld1, 1, lg.edge_b1, 0},
+          {w.GB, 64, he, 64, lg.edge_w1, ld1, 1 + HID, nullptr, 0},
+          {w.op_gt, 64, he, 64, lg.vel_w1, 64, 0, lg.vel_b1, 0},
+          {w.op_gz, 64, he, 64, lg.node_w1, 128, 0, lg.node_b1, 0},
+          {w.op_gz, 64, st.Ms + l * n * 64, 64, lg.node_w1, 128, HID, nullptr, 0},
+          {gh, 64, w.op_z, 64, lg.node_w2, 64, 0, lg.node_b2, 0}};
+      if (int rc = gemm.batch(jobs, 6, (long long)n, rjobs, &nred)) return rc;
+      if (int rc = launch_reduce_batch(rjobs, nred, s)) return rc;
+      nred = 0;
+    }
     if (int rc = gemm(w.op_gphi, 1, 1, w.op_t, 64, 64, (long long)n, lg.vel_w2, 64, 0, lg.vel_b2)) return rc;
-    if (int rc = gemm(w.op_gz, 64, 64, he, 64, 64, (long long)n, lg.node_w1, 128, 0, lg.node_b1)) return rc;
-    if (int rc = gemm(w.op_gz, 64, 64, st.Ms + l * n * 64, 64, 64, (long long)n, lg.node_w1, 128, HID, nullptr))
-      return rc;
-    if (int rc = gemm(gh, 64, 64, w.op_z, 64, 64, (long long)n, lg.node_w2, 64, 0, lg.node_b2)) return rc;
     const int nxt = cur ^ 1;
     if (!tc) {   // no TimeConv: the layer-input gradients are the next (earlier) layer's output gradients
       hipMemcpyAsync(w.gx[nxt], w.gxe, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -1690,23 +1867,19 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     }
     // ---- TimeConv_x reverse: x, v of the layer's TimeConv input ----
     hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes,
-                       st.xs + l * n * 3, st.vs + l * n * 3, loc_mean, w.gxe, w.gve, tconvx_w[l], w.gx[nxt],
+                       st.xs + l * n * 3, l > 0 ? st.ve + (l - 1) * n * 3 : st.vs, loc_mean, w.gxe, w.gve, tconvx_w[l], w.gx[nxt],
                        w.gv[nxt], w.xpart, frames);
     if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
     {
-      // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M stay zero)
-      hipMemsetAsync(g_tconvx[l], 0, 2 * 2 * modes * 2 * sizeof(float), s);
+      // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M zero)
       float* tmp = w.partial;
       const int cnt = 2 * 2 * MMAX_T * 2;
       const long long rows = (long long)BN * 3, slice = 256;
       const int nb = (int)((rows + slice - 1) / slice);
       hipLaunchKernelGGL(rows_reduce, dim3(nb), dim3(256), 0, s, w.xpart, rows, cnt, slice, tmp + 64);
       if (int rc = check_launch("rows_reduce")) return rc;
-      hipLaunchKernelGGL(rows_reduce, dim3(1), dim3(256), 0, s, tmp + 64, (long long)nb, cnt, (long long)nb, tmp);
-      if (int rc = check_launch("rows_reduce")) return rc;
-      for (int io = 0; io < 4; ++io)
-        hipMemcpyAsync(g_tconvx[l] + io * modes * 2, tmp + io * MMAX_T * 2, M * 2 * sizeof(float),
-                       hipMemcpyDeviceToDevice, s);
+      hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, tmp + 64, nb, M, modes, g_tconvx[l]);
+      if (int rc = check_launch("tconvx_grad_finish")) return rc;
     }
     // ---- TimeConv reverse: h of the layer's TimeConv input ----
     {
@@ -1721,7 +1894,7 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
       TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;
       TG = ta.ntiles < TG ? ta.ntiles : TG;
       if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
-      hipMemsetAsync(g_tconv[l], 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);
+      if (modes > M) hipMemsetAsync(g_tconv[l], 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
       hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 + 63) / 64), dim3(256), 0, s, w.tpart, TG, M, modes,
                          g_tconv[l]);
       if (int rc = check_launch("tconv_wgrad_reduce")) return rc;
