@@ -74,12 +74,16 @@ __global__ __launch_bounds__(1024) void sim_charged_kernel(SimChargedArgs a) {
     if (act) {
       double F[3] = {0.0, 0.0, 0.0};
       const double ni = sn[o + i];
+      // branch-free over j (the self pair adds an exact 0, fill_diagonal(forces_size, 0)), so the
+      // compiler can overlap the divide / sqrt chains of consecutive senders; the sums keep the
+      // reference's j order
+#pragma unroll 4
       for (int j = 0; j < N; ++j) {
-        if (j == i) continue;   // fill_diagonal(forces_size, 0)
+        const bool self = j == i;
         const double xj0 = sx[0][o + j], xj1 = sx[1][o + j], xj2 = sx[2][o + j];
         const double dot = dadd(dadd(dmul(x[0], xj0), dmul(x[1], xj1)), dmul(x[2], xj2));
-        const double l2 = dsub(dadd(ni, sn[o + j]), dmul(2.0, dot));
-        const double fs = dmul(a.strength, qi * sq[o + j]) / dmul(l2, sqrt(l2));
+        const double l2 = self ? 1.0 : dsub(dadd(ni, sn[o + j]), dmul(2.0, dot));
+        const double fs = self ? 0.0 : dmul(a.strength, qi * sq[o + j]) / dmul(l2, sqrt(l2));
         F[0] = dadd(F[0], dmul(fs, dsub(x[0], xj0)));
         F[1] = dadd(F[1], dmul(fs, dsub(x[1], xj1)));
         F[2] = dadd(F[2], dmul(fs, dsub(x[2], xj2)));
@@ -138,6 +142,7 @@ __global__ __launch_bounds__(1024) void sim_gravity_kernel(SimGravityArgs a) {
     __syncthreads();
     if (act) {
       double A[3] = {0.0, 0.0, 0.0};
+#pragma unroll 4
       for (int j = 0; j < N; ++j) {
         const double dx = dsub(sx[0][o + j], x[0]), dy = dsub(sx[1][o + j], x[1]), dz = dsub(sx[2][o + j], x[2]);
         const double r2 = dadd(dadd(dadd(dmul(dx, dx), dmul(dy, dy)), dmul(dz, dz)), a.soft2);
