@@ -34,6 +34,11 @@ typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
 // Pair loop with unit B's VALU stages placed beside unit A's MFMA blocks: SEGNO only (there it fits
 // the register file; for EGNO it spills and slows the guard path)
+// W2 / Wc1 fp16 fragments of the EGNO pair loop held in registers for a whole tile segment
+// instead of re-read from LDS per pair (C2 layer 243.6 -> 241.9 us)
+#ifndef NONODE_FRAG_REG
+#define NONODE_FRAG_REG 1
+#endif
 #ifndef NONODE_STAGGER_EGNO
 #define NONODE_STAGGER_EGNO 0
 #endif
@@ -937,6 +942,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
           float e0[KF], e1[KF];
           fetch_ef(k, e0);
           fetch_ef(min(k + 1, k_hi), e1);
+#if NONODE_FRAG_REG
+          H16Frags rw2, rwc1;   // W2 / Wc1 fragments held in registers for the segment
+          load_h16frags(rw2, w2h, lane);
+          load_h16frags(rwc1, wc1h, lane);
+#endif
 #pragma unroll 1
           for (; k + 1 <= k_hi; k += 2) {
             float n0[KF], n1[KF];
@@ -1005,7 +1015,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               h8 ah0[2], al0[2], ah1[2], al1[2];
               h16_split(a0, ah0, al0);
               h16_split(a1, ah1, al1);
+#if NONODE_FRAG_REG
+              mfma_h16r2(m0, m1, rw2, ah0, al0, ah1, al1);
+#else
               mfma_h16x2(m0, m1, w2l, ah0, al0, ah1, al1, lane);   // m = SiLU(W2 a + b2)
+#endif
             }
             STAMP(1);
             silu_ecl(m0);
@@ -1020,7 +1034,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               h8 mh0[2], ml0[2], mh1[2], ml1[2];
               h16_split(m0, mh0, ml0);
               h16_split(m1, mh1, ml1);
+#if NONODE_FRAG_REG
+              mfma_h16r2(a0, a1, rwc1, mh0, ml0, mh1, ml1);
+#else
               mfma_h16x2(a0, a1, wc1l, mh0, ml0, mh1, ml1, lane);  // coord hidden: SiLU(Wc1 m + bc1)
+#endif
             }
             STAMP(2);
             edge_f(a0, r00, r01, r02, f00, f01, f02, cA);
@@ -1045,6 +1063,94 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
 #pragma unroll
             for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }
             STAMP(3);
+          }
+        }
+        if constexpr (!PAIR) {
+          // Two waves per SIMD, one unit (16 edges) per iteration, fragments and biases from LDS. The
+          // body is one basic block as in the pair loop: the fp16x3 path always runs, and a
+          // non-finite coordinate output from finite inputs sends the unit to the column-scaled
+          // recompute before its sums are committed.
+          auto head1 = [&](int k, const float (&ev)[KF], f4 (&a)[4], float& r0, float& r1, float& r2,
+                           bool& ok) __attribute__((always_inline)) {
+            int j = n + k;
+            j = (j >= N) ? j - N : j;
+            const int sl = sb + j;
+            const f4 xs = *reinterpret_cast<const f4*>(sX + sl * 4);
+            r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
+            float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+            ok = xs[3] * xr3 != 0.f && __builtin_isfinite(d2);
+            if constexpr (rnorm) d2 = radial_norm(d2);
+            f4 q4[4];
+            load_ecl(q4, sQ + sl * ROWP, g);
+            load_ecl(a, Prow, g);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) a[mt] += q4[mt];
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) {
+              const int fi = 4 * kf + g;
+              const float bv = (fi == 0) ? d2 : ((fi - 1 < p.ne) ? ev[kf] : 0.f);
+              const f4 wf = *reinterpret_cast<const f4*>(vFEAT + kf * 256 + lane * 4);
+#pragma unroll
+              for (int mo = 0; mo < 4; ++mo) a[mo] = mfma(wf[mo], bv, a[mo]);
+            }
+          };
+          auto coord1 = [&](f4 (&c1)[4], const float* wc2, float r0, float r1, float r2, float& f0, float& f1,
+                            float& f2, float& c) __attribute__((always_inline)) {
+            silu_ecl(c1);
+            c = dot_vp(c1, wc2, g) + bc2;   // tested before the tanh (tanh(inf) = 1)
+            float ct = c;
+            if constexpr (ctanh) ct = tanhf(c);
+            f0 = r0 * ct; f1 = r1 * ct; f2 = r2 * ct;
+            if (VARIANT == SEGNO) {   // gcl.py:99-100
+              f0 = fminf(fmaxf(f0, -100.f), 100.f);
+              f1 = fminf(fmaxf(f1, -100.f), 100.f);
+              f2 = fminf(fmaxf(f2, -100.f), 100.f);
+            }
+          };
+          float e0[KF];
+          fetch_ef(min(k, k_hi), e0);
+#pragma unroll 1
+          for (; k <= k_hi; ++k) {
+            float en[KF];
+            fetch_ef(min(k + 1, k_hi), en);
+            int loff = 0;
+            asm volatile("" : "+v"(loff));   // fragment / bias reads stay in the loop
+            const h8* w2l = w2h + loff;
+            const h8* wc1l = wc1h + loff;
+            f4 a[4], m[4];
+            float r0, r1, r2, f0, f1, f2, c;
+            bool ok;
+            head1(k, e0, a, r0, r1, r2, ok);
+            silu_ecl(a);
+            load_vp(m, vB2_ + loff, g);
+            {
+              h8 ah[2], al[2];
+              h16_split(a, ah, al);
+              mfma_h16(m, w2l, ah, al, lane);   // m = SiLU(W2 a + b2)
+            }
+            silu_ecl(m);
+            load_vp(a, vBC1_ + loff, g);
+            {
+              h8 mh[2], ml[2];
+              h16_split(m, mh, ml);
+              mfma_h16(a, wc1l, mh, ml, lane);  // SiLU(Wc1 m + bc1)
+            }
+            coord1(a, vWC2_ + loff, r0, r1, r2, f0, f1, f2, c);
+            if (__builtin_expect(__any(ok && !__builtin_isfinite(c)), 0)) {
+              head1(k, e0, a, r0, r1, r2, ok);
+              silu_ecl(a);
+              load_vp(m, vB2_, g);
+              mm64_scaled(m, w2h, a, lane);
+              silu_ecl(m);
+              load_vp(a, vBC1_, g);
+              mm64_scaled(a, wc1h, m, lane);
+              coord1(a, vWC2_, r0, r1, r2, f0, f1, f2, c);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
+            fs0 += f0; fs1 += f1; fs2 += f2;
+#pragma unroll
+            for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
           }
         }
         // One unit (16 edges) per iteration; the next unit's edge inputs are in flight meanwhile.
