@@ -32,17 +32,6 @@ typedef float f8 __attribute__((ext_vector_type(8)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
-// Pair loop with unit B's VALU stages placed beside unit A's MFMA blocks: SEGNO only (there it fits
-// the register file; for EGNO it spills and slows the guard path)
-// W2 / Wc1 fp16 fragments of the EGNO pair loop held in registers for a whole tile segment
-// instead of re-read from LDS per pair (C2 layer 243.6 -> 241.9 us)
-#ifndef NONODE_FRAG_REG
-#define NONODE_FRAG_REG 1
-#endif
-#ifndef NONODE_STAGGER_EGNO
-#define NONODE_STAGGER_EGNO 0
-#endif
-template <int VARIANT> constexpr bool kStagger = VARIANT == 1 || NONODE_STAGGER_EGNO;
 // tconv_kernel h stream cache policy: bit 0 = nontemporal loads, bit 1 = nontemporal stores
 #ifndef NONODE_TC_NT
 #define NONODE_TC_NT 0
@@ -314,18 +303,17 @@ __device__ __forceinline__ void load_h16frags(H16Frags& f, const h8* wf, int lan
       f.lo[s][mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
     }
 }
-__device__ __forceinline__ void mfma_h16r(f4 (&acc)[4], const H16Frags& f, const h8 (&xh)[2], const h8 (&xl)[2]) {
+// keep fragments in AGPRs: the MFMAs read them as their A operand directly (a plain hoist leaves
+// them in AGPRs too, but copies them back with v_accvgpr_read before every use)
+__device__ __forceinline__ void pin_agpr(H16Frags& f) {
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.lo[s][mo], xh[s], acc[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xl[s], acc[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xh[s], acc[mo]);
-  }
+    for (int mo = 0; mo < 4; ++mo) {
+      asm volatile("" : "+a"(f.hi[s][mo]));
+      asm volatile("" : "+a"(f.lo[s][mo]));
+    }
 }
-
 // two edge units through register-resident fragments, the two chains interleaved
 __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H16Frags& f, const h8 (&x0h)[2],
                                            const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2]) {
@@ -340,27 +328,21 @@ __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H
   }
 }
 
-// two edge units through one 64x64 layer: acc0 += W x0, acc1 += W x1 (48 MFMAs, 8 chains)
-__device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
-                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2],
-                                           int lane) {
+// f4 sum as four plain v_add_f32: the backend would emit two v_pk_add_f32, which cost more than the
+// plain ops they replace when issued beside MFMAs (MI355X_MICROARCH.md constants table)
+#ifndef NONODE_SCALAR_ADD
+#define NONODE_SCALAR_ADD 1
+#endif
+__device__ __forceinline__ f4 add4(f4 a, f4 b) {
+#if NONODE_SCALAR_ADD
+  f4 r;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    h8 ah[4], al[4];
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) {
-      ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
-      al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
-    }
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(al[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(al[mo], x1h[s], acc1[mo]); }
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1l[s], acc1[mo]); }
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1h[s], acc1[mo]); }
-  }
+  for (int q = 0; q < 4; ++q) asm("v_add_f32 %0, %1, %2" : "=v"(r[q]) : "v"(a[q]), "v"(b[q]));
+  return r;
+#else
+  return a + b;
+#endif
 }
-
 __device__ __forceinline__ void load_ecl(f4 (&d)[4], const float* row, int g) {
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) d[mt] = *reinterpret_cast<const f4*>(row + 16 * mt + 4 * g);
@@ -374,29 +356,13 @@ __device__ __forceinline__ void load_vp(f4 (&d)[4], const float* vp, int g) {
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) d[mt] = *reinterpret_cast<const f4*>(vp + 16 * g + 4 * mt);
 }
-// SiLU of the 16 ECL values, with the add / multiply as packed f32 ops (one wave per SIMD issues
-// a v_pk_* at the cost of a plain VALU op)
-#ifndef NONODE_PK_SILU
-#define NONODE_PK_SILU 0   // packed f32 SiLU add / multiply: 1.8% slower beside the MFMAs (C2 layer 252 vs 247.5 us)
-#endif
+// SiLU of the 16 ECL values (plain f32 add / multiply: packed v_pk_* ops issued beside the MFMAs
+// measured 1.8% slower, C2 layer 252 vs 247.5 us)
 __device__ __forceinline__ void silu_ecl(f4 (&a)[4]) {
-  if (!NONODE_PK_SILU) {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) a[mt][q] = silu(a[mt][q]);
-    return;
-  }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-    for (int q = 0; q < 4; q += 2) {
-      const f2 z = {a[mt][q], a[mt][q + 1]};
-      const f2 d = f2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.0f;
-      const f2 y = z * f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-      a[mt][q] = y.x;
-      a[mt][q + 1] = y.y;
-    }
+    for (int q = 0; q < 4; ++q) a[mt][q] = silu(a[mt][q]);
 }
 // sum over the 4 lane groups (lanes e, e+16, e+32, e+48): the full 64-channel dot product
 // (gfx950 permlane swaps: v + v^32 and then v + v^16 without an LDS round trip)
@@ -898,7 +864,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             if constexpr (rnorm) d2 = radial_norm(d2);
             load_ecl(a, sQ + sl * ROWP, g);
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) a[mt] += pr[mt];
+            for (int mt = 0; mt < 4; ++mt) a[mt] = add4(a[mt], pr[mt]);
 #pragma unroll
             for (int kf = 0; kf < KF; ++kf) {
               const int fi = 4 * kf + g;
@@ -921,6 +887,13 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               f2 = fminf(fmaxf(f2, -100.f), 100.f);
             }
           };
+          // W2 / Wc1 fp16 fragments held for the whole tile segment in AGPRs, which the MFMAs read as
+          // their A operand directly (no LDS re-read per pair, no accvgpr copies)
+          H16Frags rw2, rwc1;
+          load_h16frags(rw2, w2h, lane);
+          load_h16frags(rwc1, wc1h, lane);
+          pin_agpr(rw2);
+          pin_agpr(rwc1);
           // recomputation of one unit with column-scaled fp16x3 products (the guard path)
           auto exact_unit = [&](int k, const float (&ev)[KF], f4 (&m)[4], float& f0, float& f1, float& f2)
               __attribute__((always_inline)) {
@@ -942,68 +915,17 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
           float e0[KF], e1[KF];
           fetch_ef(k, e0);
           fetch_ef(min(k + 1, k_hi), e1);
-#if NONODE_FRAG_REG
-          H16Frags rw2, rwc1;   // W2 / Wc1 fragments held in registers for the segment
-          load_h16frags(rw2, w2h, lane);
-          load_h16frags(rwc1, wc1h, lane);
-#endif
 #pragma unroll 1
           for (; k + 1 <= k_hi; k += 2) {
             float n0[KF], n1[KF];
             fetch_ef(min(k + 2, k_hi), n0);
             fetch_ef(min(k + 3, k_hi), n1);
-            // fragment reads stay in the loop (LICM would pin 128 VGPRs of loop-invariant weights)
-            int foff = 0;
-            asm volatile("" : "+v"(foff));
-            const h8* w2l = w2h + foff;
-            const h8* wc1l = wc1h + foff;
             f4 a0[4], a1[4], m0[4], m1[4];
             float r00, r01, r02, r10, r11, r12;
             float f00, f01, f02, f10, f11, f12;
             f4 pm[4];
             float cA, cB;   // coordinate-MLP outputs: non-finite iff an fp16 hi part overflowed
             bool okA, okB;  // finite inputs (node flags, |r|^2)
-            if constexpr (kStagger<VARIANT>) {
-            // The two units run half a stage apart, so every MFMA block of one unit has the other
-            // unit's VALU stage (gathers, SiLU, fp16 split) beside it in program order:
-            //   W2(A) | head+SiLU(B) ;  W2(B) | SiLU(m_A) ;  Wc1(A) | SiLU(m_B) ;  Wc1(B) | coord(A)
-            // (one wave per SIMD has no other wave to fill the matrix-pipe shadow).
-            {
-              H16Frags fw2, fwc1;
-              head2(k, e0, a0, r00, r01, r02, okA);
-              STAMP(0);
-              silu_ecl(a0);
-              h8 xh0[2], xl0[2], xh1[2], xl1[2];
-              h16_split(a0, xh0, xl0);
-              load_h16frags(fw2, w2l, lane);
-#pragma unroll
-              for (int mt = 0; mt < 4; ++mt) m0[mt] = rB2[mt];
-              mfma_h16r(m0, fw2, xh0, xl0);                       // W2(A)
-              head2(k + 1, e1, a1, r10, r11, r12, okB);           // | head + SiLU + split (B)
-              silu_ecl(a1);
-              h16_split(a1, xh1, xl1);
-#pragma unroll
-              for (int mt = 0; mt < 4; ++mt) m1[mt] = rB2[mt];
-              mfma_h16r(m1, fw2, xh1, xl1);                       // W2(B)
-              load_h16frags(fwc1, wc1l, lane);
-              silu_ecl(m0);                                       // | SiLU + split (m_A)
-              h16_split(m0, xh0, xl0);
-#pragma unroll
-              for (int mt = 0; mt < 4; ++mt) a0[mt] = rBC1[mt];
-              mfma_h16r(a0, fwc1, xh0, xl0);                      // Wc1(A)
-              silu_ecl(m1);                                       // | SiLU + split (m_B)
-              h16_split(m1, xh1, xl1);
-#pragma unroll
-              for (int mt = 0; mt < 4; ++mt) {
-                pm[mt] = m0[mt] + m1[mt];
-                a1[mt] = rBC1[mt];
-              }
-              mfma_h16r(a1, fwc1, xh1, xl1);                      // Wc1(B)
-              edge_f(a0, r00, r01, r02, f00, f01, f02, cA);       // | coord MLP (A)
-              STAMP(2);
-              edge_f(a1, r10, r11, r12, f10, f11, f12, cB);
-            }
-            } else {
             head2(k, e0, a0, r00, r01, r02, okA);
             head2(k + 1, e1, a1, r10, r11, r12, okB);
             STAMP(0);
@@ -1015,18 +937,14 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               h8 ah0[2], al0[2], ah1[2], al1[2];
               h16_split(a0, ah0, al0);
               h16_split(a1, ah1, al1);
-#if NONODE_FRAG_REG
               mfma_h16r2(m0, m1, rw2, ah0, al0, ah1, al1);
-#else
-              mfma_h16x2(m0, m1, w2l, ah0, al0, ah1, al1, lane);   // m = SiLU(W2 a + b2)
-#endif
             }
             STAMP(1);
             silu_ecl(m0);
             silu_ecl(m1);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) {
-              pm[mt] = m0[mt] + m1[mt];
+              pm[mt] = add4(m0[mt], m1[mt]);
               a0[mt] = rBC1[mt];
               a1[mt] = rBC1[mt];
             }
@@ -1034,16 +952,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               h8 mh0[2], ml0[2], mh1[2], ml1[2];
               h16_split(m0, mh0, ml0);
               h16_split(m1, mh1, ml1);
-#if NONODE_FRAG_REG
               mfma_h16r2(a0, a1, rwc1, mh0, ml0, mh1, ml1);
-#else
-              mfma_h16x2(a0, a1, wc1l, mh0, ml0, mh1, ml1, lane);  // coord hidden: SiLU(Wc1 m + bc1)
-#endif
             }
             STAMP(2);
             edge_f(a0, r00, r01, r02, f00, f01, f02, cA);
             edge_f(a1, r10, r11, r12, f10, f11, f12, cB);
-            }
             // Guard: an activation beyond the fp16 range (|x| > 65504: a diverged rollout) makes its
             // hi part inf; inf x w (0 included) puts inf or NaN into every output channel of that
             // product, hence into every later channel and into c. So a non-finite c from finite
@@ -1058,7 +971,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               for (int mt = 0; mt < 4; ++mt) pm[mt] = x0[mt] + x1[mt];
             }
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) msum[mt] += pm[mt];
+            for (int mt = 0; mt < 4; ++mt) msum[mt] = add4(msum[mt], pm[mt]);
             fs0 += f00 + f10; fs1 += f01 + f11; fs2 += f02 + f12;
 #pragma unroll
             for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; }

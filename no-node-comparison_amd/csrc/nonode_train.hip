@@ -415,8 +415,6 @@ struct EdgeBwdArgs {
   const float* gF; const float* gM;
   float* GA; float* GB; float* GX;                                    // per node (GB, GX atomically)
   float* wpart;                                                       // [grid * 4][EW_STRIDE]
-  int dbg;   // ablation bits (timing only, NONODE_EBDBG): 1 GA/GB atomics, 2 GX atomics, 4 wgrad,
-             // 8 feat wgrad, 16 phase C, 32 Wc1^T, 64 W2^T
 };
 
 // PASS 1 sums GA (per receiver), GB (per sender) and GX in WAVE-PRIVATE LDS tables by plain
@@ -783,11 +781,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       f4 gz2[4];
       load_ecl(gz2, sGM + rl * ROWP, g);
       if (!rvalid) zero4(gz2);
-      if (!(p.dbg & 32)) mm64_cs(gz2, hWc1T, gz3, lane);
+      mm64_cs(gz2, hWc1T, gz3, lane);
       STAMP(4);
       mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
       // dW2 += gz2 (x) a ; db2 += gz2
-      if (!(p.dbg & 4)) {
+      {
         f4 a[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
@@ -796,11 +794,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       STAMP(5);
       f4 gz1[4];
       zero4(gz1);
-      if (!(p.dbg & 64)) mm64_cs(gz1, hW2T, gz2, lane);
+      mm64_cs(gz1, hW2T, gz2, lane);
       STAMP(6);
       mul_dsilu_s(gz1, z1, sg1);                 // a = SiLU(z1)
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
-      if (!(p.dbg & 8)) wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
+      wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
       // s = |r|^2 input column
       float gs = dot_vp(gz1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64, g);
       if constexpr (rnorm) gs = s2 < 1e-12f ? gs * 1e12f : 0.f;   // d normalize(s) / ds: 1 / eps below eps, else 0
@@ -809,7 +807,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       gr2 = fmaf(2.f * gs, r2, gr2);
       if (rvalid) {
         // per-receiver / per-sender sums of gz1 (the W_A h_i and W_B h_j inputs) and x terms
-        if (!(p.dbg & 1)) {
+        {
           f4 t[4];
           load_ecl(t, myGA + rl * ROWP, g);
 #pragma unroll
@@ -820,7 +818,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
           store_ecl(myGB + sl * ROWP, t, g);
         }
-        if (g == 0 && !(p.dbg & 2)) {
+        if (g == 0) {
           // receiver rows first, then sender rows (a receiver of one lane can be the sender of another)
           f4* xr = reinterpret_cast<f4*>(myGX + rls * 4);
           *xr += f4{gr0, gr1, gr2, 0.f};
@@ -834,7 +832,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
     STAMP(PASS ? 7 : 15);
     __syncthreads();
     STAMP(PASS ? 10 : 14);
-    if (PASS == 0 || (p.dbg & 16)) continue;
+    if (PASS == 0) continue;
     // ---- C: write the chunk's sums (senders can be shared with the next chunk: atomics) ----
     // (the four wave-private tables added in wave order)
     for (int i = tid; i < ctc * 16 * HID; i += NW * 64) {
@@ -1815,8 +1813,6 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
       G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
       G = n_graphs < G ? n_graphs : G;
       EdgeBwdArgs ea;
-      static const int ebdbg = getenv("NONODE_EBDBG") ? atoi(getenv("NONODE_EBDBG")) : 0;
-      ea.dbg = ebdbg;
       ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = frames ? T * B : B; ea.ct = 0; ea.s_max = 0;
       ea.segno = 0;
       ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
@@ -2128,7 +2124,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
       G = B < G ? B : G;
       EdgeBwdArgs ea;
-      ea.dbg = 0; ea.segno = 1;
+      ea.segno = 1;
       ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
       ea.h = hs; ea.x = st.xs + t * n * 3; ea.ef = ne ? edge_attr : bblob; ea.bb = bblob; ea.gF = w.gF;
       ea.gM = w.gM; ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
