@@ -402,6 +402,28 @@ __device__ __forceinline__ float group_max(float v) {
 // path): every column (edge) is scaled by 2^-s, s >= 0 the smallest shift that brings its largest
 // |value| below 2^13, before the fp16x3 split, and the product is scaled back by 2^s. Both scalings
 // are exact, so the result keeps the fp16x3 path's ~2^-22 relative accuracy at any magnitude.
+// the same with the fragments in registers (the pair loop's AGPR-resident W2 / Wc1)
+__device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const H16Frags& f, const f4 (&x)[4]) {
+  const float cmax = group_max(amax_ecl(x));
+  const int s = max(__builtin_amdgcn_frexp_expf(cmax) - 13, 0);
+  const float dn = __uint_as_float((unsigned)(127 - s) << 23), up = __uint_as_float((unsigned)(127 + min(s, 127)) << 23);
+  f4 xs[4], t[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { xs[mt] = x[mt] * dn; t[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
+  h8 xh[2], xl[2];
+  h16_split(xs, xh, xl);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.lo[k][mo], xh[k], t[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.hi[k][mo], xl[k], t[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.hi[k][mo], xh[k], t[mo]);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) acc[mt] += t[mt] * up;
+}
 __device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const h8* wh, const f4 (&x)[4], int lane) {
   const float cmax = group_max(amax_ecl(x));
   const int s = max(__builtin_amdgcn_frexp_expf(cmax) - 13, 0);
@@ -904,11 +926,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             silu_ecl(a);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
-            mm64_scaled(m, w2h, a, lane);
+            mm64_scaled(m, rw2, a);
             silu_ecl(m);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
-            mm64_scaled(c, wc1h, m, lane);
+            mm64_scaled(c, rwc1, m);
             float cc;
             edge_f(c, r0, r1, r2, f0, f1, f2, cc);
           };
