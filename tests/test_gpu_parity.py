@@ -14,6 +14,7 @@ import no_node_comparison_amd as pkg
 from oracle import egno as oe
 from oracle import harness as oh
 from oracle import segno as osg
+from oracle import torch_ref as tr
 from tests.conftest import check_rel, load_golden, maxnorm_rel, params_of
 
 pytestmark = pytest.mark.gpu
@@ -236,6 +237,66 @@ def test_egno_mode_and_frame_bounds_match_oracle(T, modes):
     check_rel("x", x.cpu(), xr, TOL)
     check_rel("v", v.cpu(), vr, TOL)
     check_rel("h", h.cpu(), hr, TOL)
+
+
+@pytest.mark.parametrize("B,N,scale", [(2, 20, 3e4), (1, 70, 1e4)])
+def test_egno_guard_path_matches_oracle(B, N, scale):
+    """Edge features scaled so the edge-feature part of every layer's first Linear reaches ~2e5: the
+    SiLU(pre) activations leave the fp16 range, so units take the column-scaled guard recompute, in
+    the paired 4-wave loop (N = 20) and in the 8-wave single-unit loop (N = 70, N >= 64). Outputs
+    grow to ~1e13 / ~1e17 and stay inside the f32 range."""
+    T = 10
+    m = _egno(T=T, seed=B * 7 + N)
+    case = _egno_case(B, N, T, seed=N + 1)
+    case["edge_fea"] = (case["edge_fea"] * scale).astype(np.float32)
+    p = _sd_np(m)
+    # the guard really triggers: a first-layer pre-activation exceeds the fp16 range
+    w1 = p["layers.0.edge_message_net.scalar_net.mlp.0.weight"][:, -2:]
+    assert float(np.abs(case["edge_fea"].astype(np.float64) @ w1.T).max()) > 2 * 65504.0
+    xr, vr, hr = oe.egno_forward(p, **{k: (v.astype(np.float64) if k not in ("row", "col", "t_out") else v)
+                                       for k, v in case.items()}, T=T)
+    assert np.isfinite(xr).all() and np.isfinite(hr).all()
+    # inputs this large are ill-conditioned in fp32 itself: the reference's own ops in fp32
+    # (oracle/torch_ref.py) are up to ~1.4e-5 from float64 at N = 70; the bar is 1e-5 or twice that
+    # fp32 floor, whichever is larger
+    p32 = {k: torch.tensor(v, dtype=torch.float32) for k, v in p.items()}
+    t = lambda a: torch.tensor(np.ascontiguousarray(a))  # noqa: E731
+    with torch.no_grad():
+        f32 = tr.egno_forward(p32, t(case["x"]).float(), t(case["h"]).float(), t(case["row"]).long(),
+                              t(case["col"]).long(), t(case["edge_fea"]).float(), t(case["v"]).float(),
+                              t(case["loc_mean"]).float(), t(case["t_out"]).float(), T=T)
+        x, v, h = m(_dev(case["x"]), _dev(case["h"]), [_dev(case["row"]), _dev(case["col"])], _dev(case["edge_fea"]),
+                    v=_dev(case["v"]), loc_mean=_dev(case["loc_mean"]), timesteps_out=_dev(case["t_out"]))
+    for name, out, f, ref in (("x", x, f32[0], xr), ("v", v, f32[1], vr), ("h", h, f32[2], hr)):
+        check_rel(f"guard N={N} {name}", out.cpu(), ref, max(TOL, 2 * maxnorm_rel(f.numpy(), ref)))
+
+
+@pytest.mark.parametrize("B,N,scale", [(3, 20, 300.0), (1, 64, 60.0), (1, 70, 60.0)])
+def test_segno_guard_path_matches_oracle(B, N, scale):
+    """SEGNO with scaled positions (|r|^2 also enters as an edge feature): guard recompute in both
+    loops against the oracle."""
+    T = 4
+    m = _segno(seed=N + 3)
+    loc, vel, q = synthetic_charged(B, N, seed=N)
+    r, c = oh.full_edges(B, N)
+    x = loc.reshape(-1, 3).numpy().astype(np.float64) * scale
+    v = vel.reshape(-1, 3).numpy().astype(np.float64)
+    qq = q.reshape(-1, 1).numpy()
+    ea = np.concatenate([qq[r] * qq[c], ((x[r] - x[c]) ** 2).sum(1, keepdims=True)], 1)
+    assert float(ea[:, 1].max()) > 65504.0
+    his = np.sqrt((v ** 2).sum(1, keepdims=True))
+    p = _sd_np(m)
+    xr, hr, vr = osg.forward(p, his, x, r, c, v, ea, T=T, bug_compat=False)
+    assert np.isfinite(xr).all() and np.isfinite(hr).all()
+    p32 = {k: torch.tensor(w, dtype=torch.float32) for k, w in p.items()}
+    f = lambda a: torch.tensor(np.ascontiguousarray(a)).float()  # noqa: E731
+    with torch.no_grad():
+        f32 = tr.segno_forward_step(p32, f(his), f(x), torch.tensor(r).long(), torch.tensor(c).long(), f(v), f(ea), T=T)
+        xo, ho, vo = m(_dev(his.astype(np.float32)), _dev(x.astype(np.float32)), [_dev(r), _dev(c)],
+                       _dev(v.astype(np.float32)), _dev(ea.astype(np.float32)), T=T)
+    # bar: 1e-5 or twice the reference ops' own fp32 error on these inputs, whichever is larger
+    for name, out, g, ref in (("xo", xo, f32[0], xr), ("vo", vo, f32[2], vr), ("ho", ho, f32[1], hr)):
+        check_rel(f"segno guard N={N} {name}", out.cpu(), ref, max(TOL, 2 * maxnorm_rel(g.numpy(), ref)))
 
 
 @pytest.mark.parametrize("B,N,T", [(1, 2, 3), (4, 5, 10), (9, 20, 10), (2, 60, 7), (1, 150, 2)])
