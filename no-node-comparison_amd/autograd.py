@@ -54,11 +54,16 @@ class EGNOTrain(torch.autograd.Function):
         ctx.model, ctx.B, ctx.N, ctx.Bt = model, B, N, Bt
         ctx.state, ctx.lm, ctx.ef = state, lm, ef
         ctx.n_params = len(params)
+        # the backward repacks the parameters' current values: saving them lets autograd's version
+        # check raise if any was modified in place between forward and backward (e.g. an optimizer
+        # step before a second backward), instead of returning gradients for the wrong weights
+        ctx.save_for_backward(*params)
         return x_out, v_out, h_out
 
     @staticmethod
     def backward(ctx, gx, gv, gh):
         model, B, N, Bt = ctx.model, ctx.B, ctx.N, ctx.Bt
+        _ = ctx.saved_tensors   # raises if a parameter changed in place since the forward
         L = _lib.lib()
         T = model.num_timesteps
         dev = ctx.state.device
@@ -129,11 +134,13 @@ class SEGNOStepTrain(torch.autograd.Function):
                                                 _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.stream_of(x)))
         ctx.model, ctx.T, ctx.B, ctx.N = model, T, B, N
         ctx.state, ctx.ea = state, ea
+        ctx.save_for_backward(*params)   # version check of the parameters (see EGNOTrain.forward)
         return x_out, h_out, v_out
 
     @staticmethod
     def backward(ctx, gx, gh, gv):
         model, T, B, N = ctx.model, ctx.T, ctx.B, ctx.N
+        _ = ctx.saved_tensors   # raises if a parameter changed in place since the forward
         L = _lib.lib()
         dev = ctx.state.device
         n = B * N

@@ -68,6 +68,9 @@ constexpr int OFF_SCAL = OFF_VEC + V_COUNT * 64;  // [0] = coord b2, [1] = node_
 // option flags (1.f / 0.f): radial input normalised (EGNO norm=True, basic.py:140-141); coordinate
 // MLP output through tanh (SEGNO tanh=True, gcl.py:57-59)
 constexpr int SC_NORM = 2, SC_TANH = 3;
+// packed half2 lo-part shifts of the fp16x3 matrices (h8_scale): slots SC_H16S + HS_*
+constexpr int SC_H16S = 8;
+enum : int { HS_W2 = 0, HS_WC1 = 1, HS_N = 2, HS_COUNT = HS_N + 6 };   // HS_N + H_*: node-side matrices
 // F.normalize of the one-element radial feature: s / max(|s|, 1e-12) (s >= 0: 1 unless s < 1e-12)
 // (inf, NaN -> NaN as inf / inf and NaN / NaN in the reference)
 __device__ __forceinline__ float radial_norm(float s) {
@@ -215,21 +218,27 @@ __device__ __forceinline__ void load_frags(f4 (&a)[4], const float* wf, int mt, 
 }
 
 // ---- fp16x3 split MFMA (fp32-level accuracy at fp16 matrix-core rate) ------------------------
-// x = hi + lo with hi = fp16(x), lo = fp16(x - hi): |x - hi - lo| <= 2^-22 |x|. W x is accumulated in
-// fp32 as W_lo x_hi + W_hi x_lo + W_hi x_hi (the dropped W_lo x_lo term is ~2^-22 relative).
+// x = hi + lo with hi = fp16(x), lo = fp16(x - hi): |x - hi - lo| <= 2^-22 |x| while lo is an fp16
+// normal, i.e. for |x| >= ~2^-3; below that lo is subnormal and the split error is the absolute
+// 2^-25 of the fp16 subnormal spacing. Weights take a per-matrix power-of-two shift of their lo part
+// for this reason (h8_scale below); activations are O(1) SiLU outputs / states. W x is accumulated
+// in fp32 as W_lo x_hi + W_hi x_lo + W_hi x_hi (the dropped W_lo x_lo term is ~2^-22 relative).
 // The ECL accumulator of one layer is the B operand of v_mfma_f32_16x16x32_f16 for the next:
 // k-step s, half j of lane (g, e) = channel 16*(2s + (j>>2)) + 4g + (j&3) of column e.
 // x - (float)half(hp): one v_fma_mix_f32 (f16 operand taken from the low / high half of hp). For
 // |x| in the fp16 range the difference is exactly representable, so the residual is exact.
+// The asm writes its result over x's own register ("+v"): that register was last written by a
+// compiler-visible VALU instruction (x's producer, or a copy of x the compiler makes when x stays live),
+// which already met every MFMA hazard. A fresh "=v" output could be a register that an MFMA issued
+// just before still reads as SrcC, and the hazard recognizer does not treat an asm block as a VALU
+// write, so it would not pad that WAR hazard.
 __device__ __forceinline__ float resid_lo(unsigned hp, float x) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(x));
-  return r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %0 op_sel_hi:[1,0,0]" : "+v"(x) : "v"(hp));
+  return x;
 }
 __device__ __forceinline__ float resid_hi(unsigned hp, float x) {
-  float r;
-  asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(hp), "v"(x));
-  return r;
+  asm("v_fma_mix_f32 %0, -%1, 1.0, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(x) : "v"(hp));
+  return x;
 }
 __device__ __forceinline__ void h16_split(const f4 (&x)[4], h8 (&hi)[2], h8 (&lo)[2]) {
 #pragma unroll
@@ -258,9 +267,30 @@ __device__ __forceinline__ float amax_ecl(const f4 (&x)[4]) {
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
+// The weight residual W_lo = W - W_hi is ~2^-11 |W|: for |W| < 2^-3 it would be an fp16 subnormal
+// with a 2^-25 absolute floor (3e-5 relative at |W| = 2^-10). So each packed 64x64 matrix stores
+// W_lo' = 2^k W_lo, k the per-matrix shift that puts max |W| 2^k in [2^H16_LO_TARGET, 2^(T+1)), and the
+// kernels pair it with x_hi'' = 2^-k x_hi (one v_pk_mul_f16 per two halves; exact while x_hi'' is an
+// fp16 normal, and a subnormal x_hi'' only touches the ~2^-11 correction term): W_lo x_hi = W_lo' x_hi''.
+// `us` is the packed half2 (2^-k, 2^-k) of the matrix (blob OFF_SCAL + SC_H16S + index).
+// (a compiler-visible multiply, not inline asm: the hazard recognizer does not see an asm VALU
+// write, so an MFMA could read its result, or an asm could overwrite a pending MFMA's operand,
+// without the required wait states)
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h8 h8_scale(h8 x, unsigned us) {
+  const h2 sc = __builtin_bit_cast(h2, us);
+  const u4 w = __builtin_bit_cast(u4, x);
+  u4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned wi = w[i];   // (an rvalue: __builtin_bit_cast of a vector element reads element 0)
+    r[i] = __builtin_bit_cast(unsigned, __builtin_bit_cast(h2, wi) * sc);
+  }
+  return __builtin_bit_cast(h8, r);
+}
 // one edge unit through one 64x64 layer: acc += W x (24 MFMAs, 4 chains)
 __device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&xh)[2], const h8 (&xl)[2],
-                                         int lane) {
+                                         int lane, unsigned us) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     h8 ah[4], al[4];
@@ -269,8 +299,9 @@ __device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&
       ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
       al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
     }
+    const h8 xs = h8_scale(xh[s], us);
 #pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(al[mo], xh[s], acc[mo]);
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(al[mo], xs, acc[mo]);
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(ah[mo], xl[s], acc[mo]);
 #pragma unroll
@@ -280,13 +311,14 @@ __device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&
 
 // acc += W x for one 16-column tile: fp16x3 on the matrix cores, or the exact f32 MFMA path (wf)
 // when any |x| is beyond the fp16 hi range (wave-uniform guard)
-__device__ __forceinline__ void mm64(f4 (&acc)[4], const h8* wh, const float* wf, const f4 (&x)[4], int lane) {
+__device__ __forceinline__ void mm64(f4 (&acc)[4], const h8* wh, const float* wf, const f4 (&x)[4], int lane,
+                                     unsigned us) {
   if (__builtin_expect(__any(amax_ecl(x) > H16_LIMIT), 0)) {
     mfma_dense<4>(acc, wf, x, lane);
   } else {
     h8 xh[2], xl[2];
     h16_split(x, xh, xl);
-    mfma_h16(acc, wh, xh, xl, lane);
+    mfma_h16(acc, wh, xh, xl, lane, us);
   }
 }
 
@@ -316,11 +348,12 @@ __device__ __forceinline__ void pin_agpr(H16Frags& f) {
 }
 // two edge units through register-resident fragments, the two chains interleaved
 __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H16Frags& f, const h8 (&x0h)[2],
-                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2]) {
+                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2], unsigned us) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
+    const h8 x0s = h8_scale(x0h[s], us), x1s = h8_scale(x1h[s], us);
 #pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.lo[s][mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(f.lo[s][mo], x1h[s], acc1[mo]); }
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.lo[s][mo], x0s, acc0[mo]); acc1[mo] = mfma16(f.lo[s][mo], x1s, acc1[mo]); }
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.hi[s][mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(f.hi[s][mo], x1l[s], acc1[mo]); }
 #pragma unroll
@@ -337,7 +370,10 @@ __device__ __forceinline__ f4 add4(f4 a, f4 b) {
 #if NONODE_SCALAR_ADD
   f4 r;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) asm("v_add_f32 %0, %1, %2" : "=v"(r[q]) : "v"(a[q]), "v"(b[q]));
+  for (int q = 0; q < 4; ++q) {   // in place, for the reason given at resid_lo
+    r[q] = a[q];
+    asm("v_add_f32 %0, %0, %1" : "+v"(r[q]) : "v"(b[q]));
+  }
   return r;
 #else
   return a + b;
@@ -401,9 +437,10 @@ __device__ __forceinline__ float group_max(float v) {
 // acc = W x + bias for one 16-column unit whose activations may leave the fp16 range (the guard
 // path): every column (edge) is scaled by 2^-s, s >= 0 the smallest shift that brings its largest
 // |value| below 2^13, before the fp16x3 split, and the product is scaled back by 2^s. Both scalings
-// are exact, so the result keeps the fp16x3 path's ~2^-22 relative accuracy at any magnitude.
+// are exact; the split is then ~2^-22 relative to each column's largest |value| (not to each element:
+// elements more than ~2^16 below their column's maximum fall into the fp16 subnormal range).
 // the same with the fragments in registers (the pair loop's AGPR-resident W2 / Wc1)
-__device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const H16Frags& f, const f4 (&x)[4]) {
+__device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const H16Frags& f, const f4 (&x)[4], unsigned us) {
   const float cmax = group_max(amax_ecl(x));
   const int s = max(__builtin_amdgcn_frexp_expf(cmax) - 13, 0);
   const float dn = __uint_as_float((unsigned)(127 - s) << 23), up = __uint_as_float((unsigned)(127 + min(s, 127)) << 23);
@@ -414,8 +451,9 @@ __device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const H16Frags& f, con
   h16_split(xs, xh, xl);
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
+    const h8 xs2 = h8_scale(xh[k], us);
 #pragma unroll
-    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.lo[k][mo], xh[k], t[mo]);
+    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.lo[k][mo], xs2, t[mo]);
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.hi[k][mo], xl[k], t[mo]);
 #pragma unroll
@@ -424,7 +462,7 @@ __device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const H16Frags& f, con
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt] += t[mt] * up;
 }
-__device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const h8* wh, const f4 (&x)[4], int lane) {
+__device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const h8* wh, const f4 (&x)[4], int lane, unsigned us) {
   const float cmax = group_max(amax_ecl(x));
   const int s = max(__builtin_amdgcn_frexp_expf(cmax) - 13, 0);
   const float dn = __uint_as_float((unsigned)(127 - s) << 23), up = __uint_as_float((unsigned)(127 + min(s, 127)) << 23);
@@ -433,7 +471,7 @@ __device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const h8* wh, const f4
   for (int mt = 0; mt < 4; ++mt) { xs[mt] = x[mt] * dn; t[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
   h8 xh[2], xl[2];
   h16_split(xs, xh, xl);
-  mfma_h16(t, wh, xh, xl, lane);
+  mfma_h16(t, wh, xh, xl, lane, us);
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt] += t[mt] * up;
 }
@@ -463,31 +501,70 @@ __device__ __forceinline__ float vp_src(const float* src, int stride, int d) {
   return src ? src[(16 * mt + 4 * g + q) * stride] : 0.f;
 }
 
+// Shift k of a packed fp16x3 matrix (see h8_scale): the 64x64 block W[0..63][col0 .. col0+63] (row
+// stride ld) times |scale| has max |.| 2^k in [2^H16_LO_TARGET, 2^(H16_LO_TARGET+1)), k in [0, 14]
+// (a zero or non-finite block: k = 0). Called by every thread of a 256-thread workgroup.
+constexpr int H16_LO_TARGET = 1;
+__device__ int h16_lo_shift(const float* W, int ld, int col0, float scale) {
+  __shared__ float red[4];
+  float m = 0.f;
+  if (W)
+    for (int i = threadIdx.x; i < 4096; i += 256) m = fmaxf(m, fabsf(W[(i >> 6) * ld + col0 + (i & 63)]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])) * fabsf(scale);
+  if (!(m > 0.f) || !__builtin_isfinite(m)) return 0;
+  return min(max(H16_LO_TARGET + 1 - __builtin_amdgcn_frexp_expf(m), 0), 14);
+}
+// packed half2 (2^-k, 2^-k) as stored in the blob's SC_H16S slots (read back as the float's bits)
+__device__ __forceinline__ float h16_us_bits(int k) {
+  const unsigned short hb = (unsigned short)((15 - k) << 10);   // fp16 2^-k, k in [0, 14]
+  return __uint_as_float((unsigned)hb | ((unsigned)hb << 16));
+}
+__device__ __forceinline__ unsigned h16_us(const float* scal, int idx) {
+  return __float_as_uint(scal[SC_H16S + idx]);
+}
+
 __device__ __forceinline__ void pack_h16(_Float16* dst, const float* W, int d, int ld = 64, int col0 = 0,
-                                         float scale = 1.f) {
+                                         float scale = 1.f, int k = 0) {
   // d indexes halves of one 64x64 block: [s][mo][hl][lane][j], 2*4*2*64*8 = 8192; the block is
-  // columns col0 .. col0+63 of W (row stride ld), scaled (SiLU-domain factor) before the split
+  // columns col0 .. col0+63 of W (row stride ld), scaled (SiLU-domain factor) before the split; the
+  // lo part is stored x 2^k (exact: the residual w - hi is an f32, the shift a power of two)
   const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s = d >> 12;
   const int row = 16 * mo + (lane & 15);
   const int col = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
   const float w = W ? W[row * ld + col0 + col] * scale : 0.f;
   const _Float16 h = (_Float16)w;
-  dst[d] = hl == 0 ? h : (_Float16)(w - (float)h);
+  // (ldexp, not a multiply: a multiply fuses with the conversion into v_fma_mixlo_f16, which flushes
+  // fp16 subnormals)
+  dst[d] = hl == 0 ? h : (_Float16)__builtin_ldexpf(w - (float)h, k);
+}
+// pack_h16 of one matrix and its shift (slot idx of the scalar table `scal`)
+__device__ __forceinline__ void pack_h16_shifted(_Float16* dst, float* scal, int idx, const float* W, int d,
+                                                 int ld = 64, int col0 = 0, float scale = 1.f) {
+  const int k = h16_lo_shift(W, ld, col0, scale);
+  pack_h16(dst, W, d, ld, col0, scale, k);
+  if (blockIdx.x == 0 && threadIdx.x == 0) scal[SC_H16S + idx] = h16_us_bits(k);
 }
 
 __global__ void pack_kernel(PackArgs a) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
   const int sec = blockIdx.y;
   float* B = a.blob;
+  float* S = B + OFF_SCAL;
+  _Float16* HN = reinterpret_cast<_Float16*>(B + OFF_H16N);
   switch (sec) {
-    case 8: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16), a.w2, d); break;
-    case 9: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16 + 4096), a.cw1, d); break;
-    case 10: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WA * 4096), a.w1, d, a.ld1, a.colA, NEG_LOG2E); break;
-    case 11: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WB * 4096), a.w1, d, a.ld1, a.colB, NEG_LOG2E); break;
-    case 12: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WV1 * 4096), a.vw1, d, 64, 0, NEG_LOG2E); break;
-    case 13: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WN1A * 4096), a.nw1, d, 128, 0, NEG_LOG2E); break;
-    case 14: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WN1B * 4096), a.nw1, d, 128, HID, 1.f); break;
-    case 15: pack_h16(reinterpret_cast<_Float16*>(B + OFF_H16N + H_WN2 * 4096), a.nw2, d, 64, 0, NEG_LN2); break;
+    case 8: pack_h16_shifted(reinterpret_cast<_Float16*>(B + OFF_H16), S, HS_W2, a.w2, d); break;
+    case 9: pack_h16_shifted(reinterpret_cast<_Float16*>(B + OFF_H16 + 4096), S, HS_WC1, a.cw1, d); break;
+    case 10: pack_h16_shifted(HN + H_WA * 8192, S, HS_N + H_WA, a.w1, d, a.ld1, a.colA, NEG_LOG2E); break;
+    case 11: pack_h16_shifted(HN + H_WB * 8192, S, HS_N + H_WB, a.w1, d, a.ld1, a.colB, NEG_LOG2E); break;
+    case 12: pack_h16_shifted(HN + H_WV1 * 8192, S, HS_N + H_WV1, a.vw1, d, 64, 0, NEG_LOG2E); break;
+    case 13: pack_h16_shifted(HN + H_WN1A * 8192, S, HS_N + H_WN1A, a.nw1, d, 128, 0, NEG_LOG2E); break;
+    case 14: pack_h16_shifted(HN + H_WN1B * 8192, S, HS_N + H_WN1B, a.nw1, d, 128, HID, 1.f); break;
+    case 15: pack_h16_shifted(HN + H_WN2 * 8192, S, HS_N + H_WN2, a.nw2, d, 64, 0, NEG_LN2); break;
     // edge W1 (h parts) produce SiLU inputs: x -log2e.  W2 / Wc1 map SiLU outputs (x -log2e) to
     // SiLU inputs (x -log2e): unscaled.  node W1: h columns x -log2e, message-sum columns (sums of
     // SiLU outputs) unscaled.  node W2 maps a SiLU output to h: x -ln2.  node_v W1: x -log2e.
@@ -527,7 +604,7 @@ __global__ void pack_kernel(PackArgs a) {
         else if (i == 1 && a.vb2) val = a.vb2[0];
         else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
         else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
-        B[OFF_SCAL + i] = val;
+        if (i < SC_H16S || i >= SC_H16S + HS_COUNT) B[OFF_SCAL + i] = val;   // shifts: sections 8-15
       }
       break;
   }
@@ -631,6 +708,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_FEAT)[tid];
   const float bc2 = p.blob[OFF_SCAL + 0];
   const float bv2 = p.blob[OFF_SCAL + 1];
+  const unsigned us_w2 = h16_us(p.blob + OFF_SCAL, HS_W2), us_wc1 = h16_us(p.blob + OFF_SCAL, HS_WC1);
   const float* vFEAT_ = sV;
   const float* vB2_ = sV + 512 + V_B2 * 64;
   const float* vBC1_ = sV + 512 + V_BC1 * 64;
@@ -683,8 +761,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       } else {
         h8 xh[2], xl[2];
         h16_split(hin, xh, xl);
-        mfma_h16(ap, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), xh, xl, lane);
-        mfma_h16(aq, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), xh, xl, lane);
+        mfma_h16(ap, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), xh, xl, lane, h16_us(blob + OFF_SCAL, HS_N + H_WA));
+        mfma_h16(aq, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), xh, xl, lane, h16_us(blob + OFF_SCAL, HS_N + H_WB));
       }
       // input-finiteness flag of the node (sX slot 3): the edge guard only recomputes pairs whose
       // inputs are finite (a non-finite state, e.g. a diverged rollout, cannot be helped)
@@ -717,7 +795,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       for (int mt = 0; mt < 4; ++mt) acc[mt] = f4{0.f, 0.f, 0.f, 0.f};
     }
     mm64(acc, reinterpret_cast<const h8*>(blob + OFF_H16N + (isP ? H_WA : H_WB) * 4096),
-         blob + (isP ? OFF_WA : OFF_WB), hin, lane);
+         blob + (isP ? OFF_WA : OFF_WB), hin, lane, h16_us(blob + OFF_SCAL, HS_N + (isP ? H_WA : H_WB)));
     float sa = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -926,11 +1004,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             silu_ecl(a);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) m[mt] = rB2[mt];
-            mm64_scaled(m, rw2, a);
+            mm64_scaled(m, rw2, a, us_w2);
             silu_ecl(m);
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) c[mt] = rBC1[mt];
-            mm64_scaled(c, rwc1, m);
+            mm64_scaled(c, rwc1, m, us_wc1);
             float cc;
             edge_f(c, r0, r1, r2, f0, f1, f2, cc);
           };
@@ -959,7 +1037,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               h8 ah0[2], al0[2], ah1[2], al1[2];
               h16_split(a0, ah0, al0);
               h16_split(a1, ah1, al1);
-              mfma_h16r2(m0, m1, rw2, ah0, al0, ah1, al1);
+              mfma_h16r2(m0, m1, rw2, ah0, al0, ah1, al1, us_w2);
             }
             STAMP(1);
             silu_ecl(m0);
@@ -974,7 +1052,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               h8 mh0[2], ml0[2], mh1[2], ml1[2];
               h16_split(m0, mh0, ml0);
               h16_split(m1, mh1, ml1);
-              mfma_h16r2(a0, a1, rwc1, mh0, ml0, mh1, ml1);
+              mfma_h16r2(a0, a1, rwc1, mh0, ml0, mh1, ml1, us_wc1);
             }
             STAMP(2);
             edge_f(a0, r00, r01, r02, f00, f01, f02, cA);
@@ -1061,24 +1139,24 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             {
               h8 ah[2], al[2];
               h16_split(a, ah, al);
-              mfma_h16(m, w2l, ah, al, lane);   // m = SiLU(W2 a + b2)
+              mfma_h16(m, w2l, ah, al, lane, us_w2);   // m = SiLU(W2 a + b2)
             }
             silu_ecl(m);
             load_vp(a, vBC1_ + loff, g);
             {
               h8 mh[2], ml[2];
               h16_split(m, mh, ml);
-              mfma_h16(a, wc1l, mh, ml, lane);  // SiLU(Wc1 m + bc1)
+              mfma_h16(a, wc1l, mh, ml, lane, us_wc1);  // SiLU(Wc1 m + bc1)
             }
             coord1(a, vWC2_ + loff, r0, r1, r2, f0, f1, f2, c);
             if (__builtin_expect(__any(ok && !__builtin_isfinite(c)), 0)) {
               head1(k, e0, a, r0, r1, r2, ok);
               silu_ecl(a);
               load_vp(m, vB2_, g);
-              mm64_scaled(m, w2h, a, lane);
+              mm64_scaled(m, w2h, a, lane, us_w2);
               silu_ecl(m);
               load_vp(a, vBC1_, g);
-              mm64_scaled(a, wc1h, m, lane);
+              mm64_scaled(a, wc1h, m, lane, us_wc1);
               coord1(a, vWC2_, r0, r1, r2, f0, f1, f2, c);
             }
 #pragma unroll
@@ -1117,11 +1195,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             load_vp(m, vB2l, g);
           }
           if (__builtin_expect(__any(amax_ecl(a) > H16_LIMIT), 0)) {
-            mm64_scaled(m, w2l, a, lane);
+            mm64_scaled(m, w2l, a, lane, us_w2);
           } else {
             h8 ah[2], al[2];
             h16_split(a, ah, al);
-            mfma_h16(m, w2l, ah, al, lane);   // m = SiLU(W2 a + b2)
+            mfma_h16(m, w2l, ah, al, lane, us_w2);   // m = SiLU(W2 a + b2)
           }
           STAMP(1);
           silu_ecl(m);
@@ -1134,11 +1212,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             load_vp(a, vBC1l, g);
           }
           if (__builtin_expect(__any(amax_ecl(m) > H16_LIMIT), 0)) {
-            mm64_scaled(a, wc1l, m, lane);
+            mm64_scaled(a, wc1l, m, lane, us_wc1);
           } else {
             h8 mh[2], ml[2];
             h16_split(m, mh, ml);
-            mfma_h16(a, wc1l, mh, ml, lane);  // SiLU(Wc1 m + bc1)
+            mfma_h16(a, wc1l, mh, ml, lane, us_wc1);  // SiLU(Wc1 m + bc1)
           }
           STAMP(2);
           tail(a, r0, r1, r2);
@@ -1234,7 +1312,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
           // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
           f4 t[4];
           load_vp(t, bj + OFF_VEC + V_BV1 * 64, g);
-          mm64(t, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WV1 * 4096), bj + OFF_WV1, hr, lane);
+          mm64(t, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WV1 * 4096), bj + OFF_WV1, hr, lane,
+               h16_us(bj + OFF_SCAL, HS_N + H_WV1));
           silu_ecl(t);
           const float phi = dot_vp(t, bj + OFF_VEC + V_WV2 * 64, g) + bv2;
           nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
@@ -1257,14 +1336,17 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         } else {
           h8 xh[2], xl[2];
           h16_split(hr, xh, xl);
-          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1A * 4096), xh, xl, lane);
+          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1A * 4096), xh, xl, lane,
+                   h16_us(bj + OFF_SCAL, HS_N + H_WN1A));
           h16_split(Mr, xh, xl);
-          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1B * 4096), xh, xl, lane);
+          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1B * 4096), xh, xl, lane,
+                   h16_us(bj + OFF_SCAL, HS_N + H_WN1B));
         }
         silu_ecl(z);
         f4 hn[4];
         load_vp(hn, bj + OFF_VEC + V_BN2 * 64, g);
-        mm64(hn, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN2 * 4096), bj + OFF_WN2, z, lane);
+        mm64(hn, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN2 * 4096), bj + OFF_WN2, z, lane,
+             h16_us(bj + OFF_SCAL, HS_N + H_WN2));
         if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
   #pragma unroll
           for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
@@ -1274,7 +1356,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   #pragma unroll
           for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[mt] * NEG_LN2;    // sM holds -log2e * sum m
           store_ecl(p.m_out + (size_t)r * HID, mt4, g);
-          if (g == 0) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
+          if (g == 0 && p.f_out) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
         }
         if (rvalid) {
           store_ecl(hO + (size_t)r * HID, hn, g);

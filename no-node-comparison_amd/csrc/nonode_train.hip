@@ -59,14 +59,19 @@ __device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, 
   dst[d] = W[col * ld + row0 + row];
 }
 
-// pack_h16 of W^T: W^T[row][col] = W[col][row] (W row stride ld)
-__device__ __forceinline__ void pack_h16_t(_Float16* dst, const float* W, int d, int ld) {
+// pack_h16 of W^T: W^T[row][col] = W[col][row] (W row stride ld), lo part x 2^k (h8_scale)
+__device__ __forceinline__ void pack_h16_t(_Float16* dst, const float* W, int d, int ld, int k) {
   const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s = d >> 12;
   const int row = 16 * mo + (lane & 15);
   const int col = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
   const float w = W[col * ld + row];
   const _Float16 h = (_Float16)w;
-  dst[d] = hl == 0 ? h : (_Float16)(w - (float)h);
+  dst[d] = hl == 0 ? h : (_Float16)__builtin_ldexpf(w - (float)h, k);   // (see pack_h16)
+}
+__device__ __forceinline__ void pack_h16_t_shifted(_Float16* dst, float* scal, int idx, const float* W, int d) {
+  const int k = h16_lo_shift(W, 64, 0, 1.f);   // the transpose has the same largest |element|
+  pack_h16_t(dst, W, d, 64, k);
+  if (blockIdx.x == 0 && threadIdx.x == 0) scal[SC_H16S + idx] = h16_us_bits(k);
 }
 
 __global__ void pack_bwd_kernel(PackArgs a) {
@@ -74,10 +79,10 @@ __global__ void pack_bwd_kernel(PackArgs a) {
   float* B = a.blob;
   _Float16* H = reinterpret_cast<_Float16*>(B + BOFF_H16);
   switch (blockIdx.y) {
-    case 16: pack_h16(H + BH_W2 * 8192, a.w2, d); break;
-    case 17: pack_h16(H + BH_WC1 * 8192, a.cw1, d); break;
-    case 18: pack_h16_t(H + BH_W2T * 8192, a.w2, d, 64); break;
-    case 19: pack_h16_t(H + BH_WC1T * 8192, a.cw1, d, 64); break;
+    case 16: pack_h16_shifted(H + BH_W2 * 8192, B + BOFF_SCAL, BH_W2, a.w2, d); break;
+    case 17: pack_h16_shifted(H + BH_WC1 * 8192, B + BOFF_SCAL, BH_WC1, a.cw1, d); break;
+    case 18: pack_h16_t_shifted(H + BH_W2T * 8192, B + BOFF_SCAL, BH_W2T, a.w2, d); break;
+    case 19: pack_h16_t_shifted(H + BH_WC1T * 8192, B + BOFF_SCAL, BH_WC1T, a.cw1, d); break;
     case 0: if (d < 4096) pack_frag(B + BOFF_WA, a.w1, a.ld1, a.colA, 4, d, 1.f); break;
     case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
     case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
@@ -123,9 +128,27 @@ __global__ void pack_bwd_kernel(PackArgs a) {
         else if (i == 1 && a.vb2) val = a.vb2[0];
         else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
         else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
-        B[BOFF_SCAL + i] = val;
+        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-19
       }
       break;
+  }
+}
+
+#ifndef NONODE_BWD_PIN
+#define NONODE_BWD_PIN 0
+#endif
+// one unit through register-resident fragments (the NONODE_BWD_PIN diagnostic variant)
+__device__ __forceinline__ void mfma_h16f(f4 (&acc)[4], const H16Frags& f, const h8 (&xh)[2], const h8 (&xl)[2],
+                                          unsigned us) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const h8 xs = h8_scale(xh[s], us);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.lo[s][mo], xs, acc[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xl[s], acc[mo]);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xh[s], acc[mo]);
   }
 }
 
@@ -199,7 +222,7 @@ __device__ __forceinline__ float row_max16(float m) {
 }
 // out += W x for a gradient column set x: each column scaled to [2^11, 2^12) before the split, the
 // product scaled back (per lane: lane (e, g) holds column e)
-__device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane) {
+__device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane, unsigned us) {
   const float sc = p2scale(col_max(amax_ecl(x)));
   const float inv = 1.f / sc;   // exact (power of two)
   f4 xs[4], acc[4];
@@ -207,7 +230,7 @@ __device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x
   for (int mt = 0; mt < 4; ++mt) { xs[mt] = x[mt] * sc; acc[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
   h8 xh[2], xl[2];
   h16_split(xs, xh, xl);
-  mfma_h16(acc, wh, xh, xl, lane);
+  mfma_h16(acc, wh, xh, xl, lane, us);
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) out[mt] += acc[mt] * inv;
 }
@@ -658,6 +681,17 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
     STAMP(PASS ? 9 : 14);
     // ---- B: one unit (16 edges: receivers of a tile x sender offset k) at a time ----
     const int U = ctc * Nm1;
+#if NONODE_BWD_PIN
+    // diagnostic variant (AGPR pin): PASS 0's W2 / Wc1 fp16 fragments read from LDS
+    // once per chunk (after the chunk's barrier) and pinned in AGPRs for the unit loop
+    H16Frags fw2, fwc1;
+    if (PASS == 0) {
+      load_h16frags(fw2, hW2, lane);
+      load_h16frags(fwc1, hWc1, lane);
+      pin_agpr(fw2);
+      pin_agpr(fwc1);
+    }
+#endif
     for (int u = wave; u < U; u += NW) {
       // the weight fragments are loop-invariant: without this barrier the compiler hoists all four
       // 64x64 matrices (256 VGPRs) out of the loop and spills
@@ -721,7 +755,10 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         } else {
           h8 xh[2], xl[2];
           h16_split(a, xh, xl);
-          mfma_h16(z2, hW2, xh, xl, lane);
+#if NONODE_BWD_PIN
+          if (PASS == 0) mfma_h16f(z2, fw2, xh, xl, h16_us(bb + BOFF_SCAL, BH_W2)); else
+#endif
+          mfma_h16(z2, hW2, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_W2));
         }
       }
       // (m = z2 sg2 and c1 = z3 sg3 are recomputed where needed again: register budget)
@@ -737,7 +774,10 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         } else {
           h8 xh[2], xl[2];
           h16_split(m, xh, xl);
-          mfma_h16(z3, hWc1, xh, xl, lane);
+#if NONODE_BWD_PIN
+          if (PASS == 0) mfma_h16f(z3, fwc1, xh, xl, h16_us(bb + BOFF_SCAL, BH_WC1)); else
+#endif
+          mfma_h16(z3, hWc1, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_WC1));
         }
       }
       float c;
@@ -781,7 +821,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       f4 gz2[4];
       load_ecl(gz2, sGM + rl * ROWP, g);
       if (!rvalid) zero4(gz2);
-      mm64_cs(gz2, hWc1T, gz3, lane);
+      mm64_cs(gz2, hWc1T, gz3, lane, h16_us(bb + BOFF_SCAL, BH_WC1T));
       STAMP(4);
       mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
       // dW2 += gz2 (x) a ; db2 += gz2
@@ -794,7 +834,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       STAMP(5);
       f4 gz1[4];
       zero4(gz1);
-      mm64_cs(gz1, hW2T, gz2, lane);
+      mm64_cs(gz1, hW2T, gz2, lane, h16_us(bb + BOFF_SCAL, BH_W2T));
       STAMP(6);
       mul_dsilu_s(gz1, z1, sg1);                 // a = SiLU(z1)
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
@@ -2014,7 +2054,8 @@ __global__ __launch_bounds__(256) void segno_node_bwd_kernel(SegnoNodeBwdArgs p)
 
 struct SegnoState {
   float *hs, *xs, *vs;   // (T + 1) x n x {64, 3, 3}: substep inputs (index T: the result)
-  float *Ms, *Fs;        // T x n x {64, 4}: message sums, clamped-translation sums of each substep
+  float* Ms;             // T x n x 64: message sums of each substep (the reverse pass recomputes the
+                         // per-edge forces and clamp masks itself, so no force sums are kept)
   size_t floats;
 };
 SegnoState segno_state(void* base, int B, int N, int T) {
@@ -2023,8 +2064,8 @@ SegnoState segno_state(void* base, int B, int N, int T) {
   float* p = (float*)base;
   auto take = [&](size_t cnt) { float* q = p; if (p) p += cnt; return q; };
   st.hs = take((T + 1) * n * 64); st.xs = take((T + 1) * n * 3); st.vs = take((T + 1) * n * 3);
-  st.Ms = take(T * n * 64); st.Fs = take(T * n * 4);
-  st.floats = (size_t)(T + 1) * n * 70 + (size_t)T * n * 68;
+  st.Ms = take(T * n * 64);
+  st.floats = (size_t)(T + 1) * n * 70 + (size_t)T * n * 64;
   return st;
 }
 
@@ -2056,7 +2097,7 @@ int nonode_segno_forward_train(int B, int N, int T, int n_edge_feat, const float
     if (int rc = launch_layer<SEGNO>(B, N, n_edge_feat, B, st.hs + t * n * 64, st.xs + t * n * 3, st.vs + t * n * 3,
                                      edge_attr, blob, 1.0f / (float)T, coords_weight, recurrent,
                                      st.hs + (t + 1) * n * 64, st.xs + (t + 1) * n * 3, st.vs + (t + 1) * n * 3, s, 1,
-                                     nullptr, st.Ms + t * n * 64, st.Fs + t * n * 4))
+                                     nullptr, st.Ms + t * n * 64, nullptr))
       return rc;
   }
   hipMemcpyAsync(h_out, st.hs + T * n * 64, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);

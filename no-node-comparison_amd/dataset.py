@@ -184,6 +184,12 @@ class DeviceLoader:
             raise RuntimeError("DeviceLoader: samples of one batch have different numbers of target frames")
         f0 = torch.tensor([list(np.atleast_1d(np.asarray(d[0]))) for d in draws], dtype=torch.int32)
         oi = torch.stack([d[1] for d in draws]).to(torch.int32)
+        # frame indices past the stored trajectory: the reference's loc[frame_0] raises IndexError
+        # (dataset_simple.py:128-163); the gather kernel would read past the sample instead
+        for name, fr in (("frame_0", f0), ("target frame", oi)):
+            if fr.numel() and (int(fr.min()) < 0 or int(fr.max()) >= Tf):
+                raise IndexError(f"DeviceLoader: {name} index out of range [0, {Tf}) "
+                                 f"(got {int(fr.min())}..{int(fr.max())})")
         f0_dev, oi_dev, idx_dev = f0.to(dev), oi.to(dev), idx.to(torch.int32).to(dev)
         loc0 = torch.empty(B, I, N, 3, device=dev)
         vel0 = torch.empty(B, I, N, 3, device=dev)

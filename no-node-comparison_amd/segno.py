@@ -142,7 +142,12 @@ class SEGNO(nn.Module):
 
     def forward(self, his, x, edges, v, edge_attr, T=10, in_steps=None):
         """model.py:53-92 (single input). his [BN, in_node_nf], x, v [BN, 3], edges 2 x [E],
-        edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T."""
+        edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T.
+
+        In train mode with gradients enabled (nn.Module's default state) this records the autograd
+        tape: T single-substep launches that save every substep's state for the reverse pass
+        (autograd.SEGNOStepTrain), slower and heavier in memory than the fused inference launch.
+        Inference should run under model.eval() or torch.no_grad(), as the reference's test loops do."""
         if x.dim() == 3:
             return self._forward_multi(his, x, edges, v, edge_attr, int(T), in_steps)
         if self.bug_compat:
