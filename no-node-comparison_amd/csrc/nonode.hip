@@ -222,7 +222,9 @@ __device__ __forceinline__ void load_frags(f4 (&a)[4], const float* wf, int mt, 
 // normal, i.e. for |x| >= ~2^-3; below that lo is subnormal and the split error is the absolute
 // 2^-25 of the fp16 subnormal spacing. Weights take a per-matrix power-of-two shift of their lo part
 // for this reason (h8_scale below); activations are O(1) SiLU outputs / states. W x is accumulated
-// in fp32 as W_lo x_hi + W_hi x_lo + W_hi x_hi (the dropped W_lo x_lo term is ~2^-22 relative).
+// in fp32 as W_hi x_hi + W_lo x_hi + W_hi x_lo (the dropped W_lo x_lo term is ~2^-22 relative); the
+// chain starts with the product that needs only the hi conversions, so the residual and the x_hi''
+// scaling of the other two terms issue under its MFMAs.
 // The ECL accumulator of one layer is the B operand of v_mfma_f32_16x16x32_f16 for the next:
 // k-step s, half j of lane (g, e) = channel 16*(2s + (j>>2)) + 4g + (j&3) of column e.
 // x - (float)half(hp): one v_fma_mix_f32 (f16 operand taken from the low / high half of hp). For
@@ -301,11 +303,11 @@ __device__ __forceinline__ void mfma_h16(f4 (&acc)[4], const h8* wf, const h8 (&
     }
     const h8 xs = h8_scale(xh[s], us);
 #pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(ah[mo], xh[s], acc[mo]);
+#pragma unroll
     for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(al[mo], xs, acc[mo]);
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(ah[mo], xl[s], acc[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(ah[mo], xh[s], acc[mo]);
   }
 }
 
@@ -353,11 +355,11 @@ __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H
   for (int s = 0; s < 2; ++s) {
     const h8 x0s = h8_scale(x0h[s], us), x1s = h8_scale(x1h[s], us);
 #pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.hi[s][mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(f.hi[s][mo], x1h[s], acc1[mo]); }
+#pragma unroll
     for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.lo[s][mo], x0s, acc0[mo]); acc1[mo] = mfma16(f.lo[s][mo], x1s, acc1[mo]); }
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.hi[s][mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(f.hi[s][mo], x1l[s], acc1[mo]); }
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(f.hi[s][mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(f.hi[s][mo], x1h[s], acc1[mo]); }
   }
 }
 
@@ -453,11 +455,11 @@ __device__ __forceinline__ void mm64_scaled(f4 (&acc)[4], const H16Frags& f, con
   for (int k = 0; k < 2; ++k) {
     const h8 xs2 = h8_scale(xh[k], us);
 #pragma unroll
+    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.hi[k][mo], xh[k], t[mo]);
+#pragma unroll
     for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.lo[k][mo], xs2, t[mo]);
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.hi[k][mo], xl[k], t[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) t[mo] = mfma16(f.hi[k][mo], xh[k], t[mo]);
   }
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) acc[mt] += t[mt] * up;
@@ -1064,9 +1066,14 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             // of 32 v_max3 per pair. Below 65504 the split keeps its 2^-22 relative accuracy.
             const bool redo = (okA && !__builtin_isfinite(cA)) || (okB && !__builtin_isfinite(cB));
             if (__builtin_expect(__any(redo), 0)) {
+              // the recompute's sender offset through an opaque asm: otherwise its head (shared with
+              // the fast path's) lets the speculative-execution pass hoist the column maxima and
+              // scalings of mm64_scaled into the hot block (~60 VALU per pair, every pair)
+              int kg = k;
+              asm volatile("" : "+v"(kg));
               f4 x0[4], x1[4];
-              exact_unit(k, e0, x0, f00, f01, f02);
-              exact_unit(k + 1, e1, x1, f10, f11, f12);
+              exact_unit(kg, e0, x0, f00, f01, f02);
+              exact_unit(kg + 1, e1, x1, f10, f11, f12);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) pm[mt] = x0[mt] + x1[mt];
             }
@@ -1150,7 +1157,9 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             }
             coord1(a, vWC2_ + loff, r0, r1, r2, f0, f1, f2, c);
             if (__builtin_expect(__any(ok && !__builtin_isfinite(c)), 0)) {
-              head1(k, e0, a, r0, r1, r2, ok);
+              int kg = k;
+              asm volatile("" : "+v"(kg));   // keeps the recompute in the branch (see the pair loop)
+              head1(kg, e0, a, r0, r1, r2, ok);
               silu_ecl(a);
               load_vp(m, vB2_, g);
               mm64_scaled(m, w2h, a, lane, us_w2);

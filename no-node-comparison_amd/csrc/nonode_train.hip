@@ -144,11 +144,11 @@ __device__ __forceinline__ void mfma_h16f(f4 (&acc)[4], const H16Frags& f, const
   for (int s = 0; s < 2; ++s) {
     const h8 xs = h8_scale(xh[s], us);
 #pragma unroll
+    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xh[s], acc[mo]);
+#pragma unroll
     for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.lo[s][mo], xs, acc[mo]);
 #pragma unroll
     for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xl[s], acc[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xh[s], acc[mo]);
   }
 }
 

@@ -119,3 +119,61 @@ def test_segno_batch_inputs_equal_reference_run_epoch(dataset, ni, var_dt):
             assert np.array_equal(in_steps.cpu().numpy(), g[f"{tag}::{k}::in_steps"])
         n += 1
     assert n == int(g[f"{tag}::batches"])
+
+
+def _run_epoch_c1(model, loader, N, T, optimizer=None):
+    """run_epoch (main_simulation_simple_no.py:190-307, rollout=False) over the device loader with the
+    drop-in EGNO: the reference's call sequence, criterion and loss bookkeeping."""
+    import no_node_comparison_amd as pkg
+    crit = torch.nn.MSELoss(reduction="none")
+    model.train() if optimizer is not None else model.eval()
+    rec, tot, cnt = [], 0.0, 0
+    for loc, vel, edge_attr, charges, loc_true, in_indices, out_indices in loader:
+        out_indices = out_indices - in_indices.max()
+        in_indices = in_indices - in_indices.max()
+        B = loc.shape[0]
+        edges = pkg.harness.get_edges(B, N, loc.device)
+        if optimizer is not None:
+            optimizer.zero_grad()
+        x, v, ea, nodes, lm = pkg.harness.prepare_inputs(loc, vel, edge_attr.reshape(-1, edge_attr.shape[-1]), edges,
+                                                         N, 1, charges)
+        with torch.set_grad_enabled(optimizer is not None):
+            xo, _, _ = model(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_in=in_indices, timesteps_out=out_indices)
+            pred = xo.reshape(T, -1, 3).transpose(0, 1).reshape(B, N, T, 3)
+            losses = crit(pred, loc_true[:, :, :T]).mean((0, 1, 3))
+            if optimizer is not None:
+                losses.mean().backward()
+                optimizer.step()
+        rec.append(losses.detach().cpu().numpy())
+        tot += float(losses[-1]) * B
+        cnt += B
+    return tot / cnt, np.stack(rec)
+
+
+def test_run_epoch_c1_with_drop_in_egno_matches_reference():
+    """Config C1 end to end through the caller it names: the reference's run_epoch loop (eval pass and
+    one Adam training epoch, lr 1e-4 / wd 1e-8) with the drop-in EGNO and the device loader gives the
+    per-batch per-frame losses and the epoch loss the reference's run_epoch reported on the same split
+    (tests/golden/egno_run_epoch.npz)."""
+    import no_node_comparison_amd as pkg
+    from tests.conftest import load_golden
+    fx = load_golden("egno_run_epoch")
+    N, T, B = int(fx["cfg::N"]), int(fx["cfg::T"]), int(fx["cfg::B"])
+    ds = NBodyDynamicsDataset("train", data_dir=os.path.join(GOLDEN, "nbody_c1"), dataset="charged",
+                              dataset_name="nbody_small", n_balls=N, num_timesteps=T)
+    sd = {k[3:]: torch.tensor(v) for k, v in fx.items() if k.startswith("w::")}
+
+    def model():
+        m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2, num_timesteps=T,
+                     time_emb_dim=32, device="cuda")
+        m.load_state_dict(sd)
+        return m
+
+    avg, losses = _run_epoch_c1(model(), DeviceLoader(ds, batch_size=B), N, T)
+    np.testing.assert_allclose(losses, fx["eval::losses"], rtol=1e-5)
+    assert abs(avg - float(fx["eval::avg_loss"])) <= 1e-5 * abs(float(fx["eval::avg_loss"]))
+    m = model()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4, weight_decay=1e-8)
+    avg, losses = _run_epoch_c1(m, DeviceLoader(ds, batch_size=B), N, T, opt)
+    np.testing.assert_allclose(losses, fx["train::losses"], rtol=1e-5)
+    assert abs(avg - float(fx["train::avg_loss"])) <= 1e-5 * abs(float(fx["train::avg_loss"]))

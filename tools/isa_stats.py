@@ -94,3 +94,23 @@ def loop_hist(path, kname, label, nth=-1):
     ends = [i for i, ln in enumerate(body) if re.match(r"^\ts_(?:cbranch_\w+|branch)\s+" + re.escape(label) + r"\b", ln)]
     seg = [x.split()[0] for x in body[start:ends[nth] + 1] if x.startswith("\t") and not x.startswith("\t.")]
     return collections.Counter(seg)
+
+
+def blocks(path, kname, label, nth=-1):
+    """basic blocks (label, instruction list) of the loop headed by `label`"""
+    body = kernels(path)[kname]["body"]
+    start = next(i for i, ln in enumerate(body) if ln.startswith(label + ":"))
+    ends = [i for i, ln in enumerate(body) if re.match(r"^\ts_(?:cbranch_\w+|branch)\s+" + re.escape(label) + r"\b", ln)]
+    out, cur, name = [], [], label
+    for ln in body[start:ends[nth] + 1]:
+        m = re.match(r"^(\.LBB\S+):|^; %(bb\.\d+):", ln)
+        if m:
+            if cur:
+                out.append((name, cur))
+            name, cur = m.group(1) or m.group(2), []
+            continue
+        if ln.startswith("\t") and not ln.startswith("\t.") and not ln.startswith("\t;"):
+            cur.append(ln.split()[0])
+    if cur:
+        out.append((name, cur))
+    return out
