@@ -260,11 +260,30 @@ def _cpu_params(model):
     return {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
 
 
+def host_cores():
+    """What the CPU baseline ran on: torch's intra-op threads, the CPUs this process may run on, and
+    the host's physical cores (psutil; the GPU box shares a larger host, so only the first two
+    describe the baseline)."""
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:   # noqa: BLE001 - informational
+        phys = None
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:   # noqa: BLE001
+        affinity = None
+    return {"threads": torch.get_num_threads(), "cpus_allowed": affinity, "host_physical_cores": phys,
+            "host_logical_cpus": os.cpu_count()}
+
+
 def _baseline(units, med, calls, sample, unit="trajectories/s"):
-    return {"value": units / med, "unit": unit, "cores": torch.get_num_threads(), "kind": "torch-ref",
-            "median_s_per_call": med, "calls": calls,
+    hc = host_cores()
+    return {"value": units / med, "unit": unit, "cores": hc["threads"], "kind": "torch-ref",
+            "cores_note": "cores = torch intra-op threads used (hardware threads, not verified physical cores)",
+            "host": hc, "median_s_per_call": med, "calls": calls,
             "sample": sample + f"; oracle/torch_ref.py (the reference's torch ops, op by op) on "
-                               f"{torch.get_num_threads()} host threads, median of {calls} calls"}
+                               f"{hc['threads']} host threads, median of {calls} calls"}
 
 
 def _parity(got, ref, key="pos"):
@@ -680,8 +699,7 @@ def c5_substeps(total=50, seed=0):
 # ChargedParticlesSim (synthetic_sim.py:244-260) per ordered pair and step, float64, as the kernel
 # evaluates it: x_i.x_j (5), |x_i|^2 + |x_j|^2 - 2 x_i.x_j (3), s q_i q_j / (l2 sqrt(l2)) (5),
 # F += fs (x_i - x_j) (9)
-FLOP_PER_PAIR_CHARGED = 22
-FP64_PEAK_TFLOPS = 78.6     # MI355X FP64 vector, AMD spec (not in the microarch guide)
+FLOP_PER_PAIR_CHARGED = 22   # f64 operations per pair as listed (the divide and the sqrt count one each)
 
 
 def run_sim_charged(args, world, rank, dev, backend):
@@ -728,7 +746,9 @@ def run_sim_charged(args, world, rank, dev, backend):
         flop = float(FLOP_PER_PAIR_CHARGED) * S * N * (N - 1) * Tn
         ach = flop / (avg * 1e-3) / 1e12
         res["roofline"] = {"kernel": "sim_charged_kernel", "bound": "valu_fp64", "achieved": ach,
-                           "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS,
+                           "peak": None, "unit": "TFLOP/s", "frac": None,
+                           "note": "f64 operation rate (22 per pair, divide and sqrt counted as one each); no "
+                                   "FP64 peak is given in MI355X_MICROARCH.md, so the kernel is not priced",
                            "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
                            "launches_timed": len(sims)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -742,6 +762,7 @@ def run_sim_charged(args, world, rank, dev, backend):
                 break
         cel = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": done / cel, "unit": "trajectories/s", "cores": 1, "kind": "port",
+                               "host": host_cores(),
                                "sample": f"oracle/sim.py charged_trajectory (numpy f64, per simulation like the "
                                f"reference), {done} of the same simulations in {cel:.1f} s"}
         got = out[0][done - 1].cpu().numpy()

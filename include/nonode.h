@@ -279,6 +279,40 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
                           const float* g_v, const float* g_h, const nonode_layer_grads* grads, float* g_h_in,
                           float* g_x_in, float* g_v_in, void* workspace, size_t workspace_bytes, void* stream);
 
+/*
+ * Layer-granular reverse passes (SURVEY §8(b) egno_layer_bwd / spectral_tconv_bwd): autograd of ONE
+ * EGNN_Layer or ONE TimeConv + TimeConv_x given that block's inputs and the gradients of its outputs,
+ * for a caller that differentiates the blocks separately. Each recomputes what it needs of its forward
+ * (message / force sums, LeakyReLU decisions) into the workspace; the whole-model
+ * nonode_egno_backward runs the same reverse kernels from its saved state instead.
+ *
+ * nonode_egnn_layer_bwd: EGNN_Layer.forward (basic.py:167-186; variant NONODE_VARIANT_EGNO) over
+ * n_graphs fully connected graphs of N nodes (N <= 21, edge features of graph g from sample
+ * g % ef_mod) with inputs h [n][64], x, v [n][3] (n = n_graphs N). blob / bblob from
+ * nonode_pack_layer / nonode_pack_layer_bwd. Given dL/dx_out (g_v, g_h: NULL = 0) writes every
+ * parameter gradient of the layer (*grads, written not accumulated) and dL/dh, dL/dx, dL/dv of the
+ * inputs (dL/dv includes the output v, which the layer passes through unchanged).
+ */
+size_t nonode_egnn_layer_bwd_workspace_bytes(int n_graphs, int N);
+int nonode_egnn_layer_bwd(int variant, int n_graphs, int N, int n_edge_feat, int ef_mod, const float* h,
+                          const float* x, const float* v, const float* edge_fea, const float* blob,
+                          const float* bblob, const float* g_x, const float* g_v, const float* g_h,
+                          const nonode_layer_grads* grads, float* g_h_in, float* g_x_in, float* g_v_in,
+                          void* workspace, size_t workspace_bytes, void* stream);
+/*
+ * nonode_egno_tconv_bwd: TimeConv + TimeConv_x of one EGNO layer (layer_no.py:80-178, egno.py:99-108)
+ * on time-major [T][BN] inputs h [..][64], x, v [..][3] with loc_mean [BN][3], as nonode_egno_tconv
+ * runs it (tconv_blob from nonode_pack_tconv; tconv_w / tconvx_w the raw weights1 tensors
+ * [64][64][modes][2] / [2][2][modes][2], modes <= 4). Given the gradients of its outputs (NULL = 0)
+ * writes the input gradients and the weights1 gradients.
+ */
+size_t nonode_egno_tconv_bwd_workspace_bytes(int BN, int T, int modes);
+int nonode_egno_tconv_bwd(int BN, int T, int modes, const float* h, const float* x, const float* v,
+                          const float* loc_mean, const float* tconv_blob, const float* tconv_w,
+                          const float* tconvx_w, const float* g_h, const float* g_x, const float* g_v,
+                          float* g_h_in, float* g_x_in, float* g_v_in, float* g_tconv_w, float* g_tconvx_w,
+                          void* workspace, size_t workspace_bytes, void* stream);
+
 
 /* ---- rollout drivers (rollout_fn / prepare_inputs / energy on the GPU) ---- */
 

@@ -26,6 +26,8 @@ SYMBOLS = (
     "nonode_prepare_inputs", "nonode_energy", "nonode_egno_rollout_workspace_bytes", "nonode_egno_rollout",
     "nonode_segno_rollout_workspace_bytes", "nonode_segno_rollout", "nonode_sim_charged", "nonode_sim_gravity",
     "nonode_gather_batch", "nonode_rollout_metrics",
+    "nonode_egnn_layer_bwd_workspace_bytes", "nonode_egnn_layer_bwd",
+    "nonode_egno_tconv_bwd_workspace_bytes", "nonode_egno_tconv_bwd",
 )
 
 VARIANT_EGNO = 0
@@ -111,6 +113,13 @@ def lib():
     L.nonode_segno_backward_workspace_bytes.restype = _sz
     L.nonode_segno_backward.argtypes = ([_i] * 4 + [_f, _i] + [_vp] * 6 + [ctypes.POINTER(LayerGrads)]
                                         + [_vp] * 4 + [_sz, _vp])
+    L.nonode_egnn_layer_bwd_workspace_bytes.argtypes = [_i, _i]
+    L.nonode_egnn_layer_bwd_workspace_bytes.restype = _sz
+    L.nonode_egnn_layer_bwd.argtypes = ([_i] * 5 + [_vp] * 9 + [ctypes.POINTER(LayerGrads)] + [_vp] * 4
+                                        + [_sz, _vp])
+    L.nonode_egno_tconv_bwd_workspace_bytes.argtypes = [_i] * 3
+    L.nonode_egno_tconv_bwd_workspace_bytes.restype = _sz
+    L.nonode_egno_tconv_bwd.argtypes = [_i] * 3 + [_vp] * 16 + [_sz, _vp]
     L.nonode_prepare_inputs.argtypes = [_i, _i, _i] + [_vp] * 5 + [_i] + [_vp] * 6
     L.nonode_energy.argtypes = [_i] * 4 + [_vp] * 5
     L.nonode_egno_rollout_workspace_bytes.argtypes = [_i] * 6

@@ -1797,6 +1797,118 @@ size_t nonode_egno_backward_workspace_bytes(int B, int N, int T, int modes) {
 }  // extern "C"
 
 namespace {
+// Reverse of ONE EGNN_Layer (basic.py:167-186) over n rows = n_graphs x N given its inputs (he, xe,
+// ve), the forward's message / force sums (Ms, Fs) and the gradients of its outputs (gx, gv, gh):
+// writes every parameter gradient of the layer (*lg) and the gradients of its inputs (g_*in).
+// Shared by nonode_egno_backward (per layer) and nonode_egnn_layer_bwd.
+struct LayerRev {
+  int n, N, n_graphs, ef_mod, ne;
+  const float *he, *xe, *ve, *Ms, *Fs, *edge_fea, *bb;
+  const float *gx, *gv, *gh;
+  const nonode_layer_grads* lg;
+  float *g_xin, *g_vin, *g_hin;
+};
+int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, const Gemm& gemm, hipStream_t s) {
+  const size_t n = (size_t)r.n;
+  const int N = r.N, ne = r.ne, ld1 = 2 * HID + 1 + ne;
+  const nonode_layer_grads& lg = *r.lg;
+  NodeBwdArgs na;
+  na.n = r.n; na.N = N; na.h = r.he; na.v = r.ve; na.M = r.Ms; na.F = r.Fs;
+  na.gxo = r.gx; na.gvo = r.gv; na.gho = r.gh; na.bb = r.bb;
+  na.gv = r.g_vin; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp;
+  na.op_gt = w.op_gt; na.op_t = w.op_t; na.op_gphi = w.op_gphi; na.op_z = w.op_z; na.op_gz = w.op_gz;
+  const int ntile = (int)((n + 15) / 16);
+  na.GB = w.GB; na.GX = w.GX;
+  if (int rc = launch_node_bwd(na, ntile, s)) return rc;
+  ReduceJob rjobs[REDUCE_BATCH_MAX];
+  int nred = 0;
+  {
+    int G = num_cus();
+    G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
+    G = r.n_graphs < G ? r.n_graphs : G;
+    EdgeBwdArgs ea;
+    ea.n_graphs = r.n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = r.ef_mod; ea.ct = 0; ea.s_max = 0;
+    ea.segno = 0;
+    ea.h = r.he; ea.x = r.xe; ea.ef = ne ? r.edge_fea : r.bb; ea.bb = r.bb; ea.gF = w.gF; ea.gM = w.gM;
+    ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
+    if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
+    // edge-level weight gradients: fixed-order sums of the G block partials (launched with the
+    // node-level GEMMs' reductions below)
+    const int nparts = G;   // one partial per block
+    const int nf = 1 + ne;
+    auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int split, int col1) {
+      rjobs[nred++] = ReduceJob{w.wpart + off, nparts, M_, N_, dst, ld, 0, 1, bias, 0, 1.f, split, col1,
+                                (long long)EW_STRIDE};
+    };
+    red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 1 << 30, 0);
+    red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 1 << 30, 0);
+    red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 1 << 30, 0);
+    // edge Linear 1 scalar columns [s | e] (EGNO order [s, h_i, h_j, e], basic.py:152-154, 170)
+    red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1);
+  }
+  hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, r.n, w.ghp, w.GA, w.GB, r.gx,
+                     w.GX, r.bb, r.g_hin, r.g_xin);
+  if (int rc = check_launch("node_post_kernel")) return rc;
+  // ---- node-level weight gradients of this layer: six 64x64 GEMMs in one launch, their and the
+  // edge-level reductions in another ----
+  // edge Linear 1 h_i / h_j blocks; its bias gradient sum_e gz1 = sum_i GA_i comes with the h_i block
+  {
+    const Gemm::Job jobs[6] = {
+        {w.GA, 64, r.he, 64, lg.edge_w1, ld1, 1, lg.edge_b1, 0},
+        {w.GB, 64, r.he, 64, lg.edge_w1, ld1, 1 + HID, nullptr, 0},
+        {w.op_gt, 64, r.he, 64, lg.vel_w1, 64, 0, lg.vel_b1, 0},
+        {w.op_gz, 64, r.he, 64, lg.node_w1, 128, 0, lg.node_b1, 0},
+        {w.op_gz, 64, r.Ms, 64, lg.node_w1, 128, HID, nullptr, 0},
+        {r.gh, 64, w.op_z, 64, lg.node_w2, 64, 0, lg.node_b2, 0}};
+    if (int rc = gemm.batch(jobs, 6, (long long)n, rjobs, &nred)) return rc;
+    if (int rc = launch_reduce_batch(rjobs, nred, s)) return rc;
+  }
+  return gemm(w.op_gphi, 1, 1, w.op_t, 64, 64, (long long)n, lg.vel_w2, 64, 0, lg.vel_b2);
+}
+
+// Reverse of TimeConv + TimeConv_x of one EGNO layer (layer_no.py:80-178, egno.py:99-108): given the
+// layer's TimeConv inputs (h [T][BN][64], x, v) and the gradients of its outputs (gh, gx, gv), writes
+// the input gradients (g_hin, g_xin, g_vin) and the raw weight gradients (g_tw [64][64][modes][2],
+// g_txw [2][2][modes][2]). mask: the forward's LeakyReLU decisions (TconvArgs::mask_out).
+struct TconvRev {
+  int BN, T, M, modes, frames;
+  const float *hs, *xs, *vs, *lm, *tw, *txw;
+  const unsigned long long* mask;
+  const float *gh, *gx, *gv;
+  float *g_hin, *g_xin, *g_vin, *g_tw, *g_txw;
+};
+int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
+  const int BN = r.BN, T = r.T, M = r.M, modes = r.modes;
+  hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes, r.xs, r.vs,
+                     r.lm, r.gx, r.gv, r.txw, r.g_xin, r.g_vin, w.xpart, r.frames);
+  if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
+  {
+    // g_txw [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M zero)
+    float* tmp = w.partial;
+    const int cnt = 2 * 2 * MMAX_T * 2;
+    const long long rows = (long long)BN * 3, slice = 256;
+    const int nb = (int)((rows + slice - 1) / slice);
+    hipLaunchKernelGGL(rows_reduce, dim3(nb), dim3(256), 0, s, w.xpart, rows, cnt, slice, tmp + 64);
+    if (int rc = check_launch("rows_reduce")) return rc;
+    hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, tmp + 64, nb, M, modes, r.g_txw);
+    if (int rc = check_launch("tconvx_grad_finish")) return rc;
+  }
+  hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, r.tw, modes, M, w.twb);
+  if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
+  TconvBwdArgs ta;
+  ta.BN = BN; ta.T = T; ta.M = M; ta.ntiles = (BN + 15) / 16;
+  ta.h = r.hs; ta.gout = r.gh; ta.wp = w.twf; ta.wb = w.twb; ta.gh = r.g_hin; ta.wpart = w.tpart;
+  ta.mask = r.mask;
+  int TG = num_cus();
+  TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;
+  TG = ta.ntiles < TG ? ta.ntiles : TG;
+  if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
+  if (modes > M) hipMemsetAsync(r.g_tw, 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
+  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 + 63) / 64), dim3(256), 0, s, w.tpart, TG, M, modes,
+                     r.g_tw);
+  return check_launch("tconv_wgrad_reduce");
+}
+
 // frames = 1: per-frame loc_mean / edge_fea (num_inputs > 1); emb_cols: time-embedding columns of
 // the embedding Linear (time_emb_dim, or 2 time_emb_dim with the input-time embedding)
 int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
@@ -1823,74 +1935,24 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
   TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, emb_cols);
   BwdWs w = bwd_ws(workspace, B, N, T, M);
   Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
-  ReduceJob rjobs[REDUCE_BATCH_MAX];
-  int nred = 0;
   // grads of the final outputs
   // (read in place: the reverse pass only reads the output gradients of a layer)
   const float *gx = g_x, *gv = g_v, *gh = g_h;
   if (!g_v) { hipMemsetAsync(w.gv[0], 0, n * 3 * sizeof(float), s); gv = w.gv[0]; }
   if (!g_h) { hipMemsetAsync(w.gh[0], 0, n * 64 * sizeof(float), s); gh = w.gh[0]; }
   int cur = 0;
-  const int ld1 = 2 * HID + 1 + ne;
   for (int l = L - 1; l >= 0; --l) {
-    const nonode_layer_grads& lg = layer_grads[l];
     const float* he = (tc ? st.he : st.hs) + l * n * 64;
     const float* xe = (tc ? st.xe : st.xs) + l * n * 3;
     const float* ve = tc ? st.ve + l * n * 3 : st.vs;   // v is unchanged by every layer
-    const float* bb = bblobs[l];
     // ---- EGNN_Layer reverse ----
-    NodeBwdArgs na;
-    na.n = (int)n; na.N = N; na.h = he; na.v = ve; na.M = st.Ms + l * n * 64; na.F = st.Fs + l * n * 4;
-    na.gxo = gx; na.gvo = gv; na.gho = gh; na.bb = bb;
-    na.gv = w.gve; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp;
-    na.op_gt = w.op_gt; na.op_t = w.op_t; na.op_gphi = w.op_gphi; na.op_z = w.op_z; na.op_gz = w.op_gz;
-    const int ntile = (int)((n + 15) / 16);
-    na.GB = w.GB; na.GX = w.GX;
-    if (int rc = launch_node_bwd(na, ntile, s)) return rc;
-    {
-      const int n_graphs = T * B;
-      int G = num_cus();
-      G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
-      G = n_graphs < G ? n_graphs : G;
-      EdgeBwdArgs ea;
-      ea.n_graphs = n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = frames ? T * B : B; ea.ct = 0; ea.s_max = 0;
-      ea.segno = 0;
-      ea.h = he; ea.x = xe; ea.ef = ne ? edge_fea : bb; ea.bb = bb; ea.gF = w.gF; ea.gM = w.gM;
-      ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
-      if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
-      // edge-level weight gradients: fixed-order sums of the G block partials (launched with the
-      // node-level GEMMs' reductions below)
-      const int nparts = G;   // one partial per block
-      const int nf = 1 + ne;
-      auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int split, int col1) {
-        rjobs[nred++] = ReduceJob{w.wpart + off, nparts, M_, N_, dst, ld, 0, 1, bias, 0, 1.f, split, col1,
-                                  (long long)EW_STRIDE};
-      };
-      red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 1 << 30, 0);
-      red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 1 << 30, 0);
-      red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 1 << 30, 0);
-      // edge Linear 1 scalar columns [s | e] (EGNO order [s, h_i, h_j, e], basic.py:152-154, 170)
-      red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1);
-    }
-    hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, (int)n, w.ghp, w.GA, w.GB, gx,
-                       w.GX, bb, w.ghe, w.gxe);
-    if (int rc = check_launch("node_post_kernel")) return rc;
-    // ---- node-level weight gradients of this layer: six 64x64 GEMMs in one launch, their and the
-    // edge-level reductions in another ----
-    // edge Linear 1 h_i / h_j blocks; its bias gradient sum_e gz1 = sum_i GA_i comes with the h_i block
-    {
-      const Gemm::Job jobs[6] = {
-          {w.GA, 64, he, 64, lg.edge_w1, ld1, 1, lg.edge_b1, 0},
-          {w.GB, 64, he, 64, lg.edge_w1, ld1, 1 + HID, nullptr, 0},
-          {w.op_gt, 64, he, 64, lg.vel_w1, 64, 0, lg.vel_b1, 0},
-          {w.op_gz, 64, he, 64, lg.node_w1, 128, 0, lg.node_b1, 0},
-          {w.op_gz, 64, st.Ms + l * n * 64, 64, lg.node_w1, 128, HID, nullptr, 0},
-          {gh, 64, w.op_z, 64, lg.node_w2, 64, 0, lg.node_b2, 0}};
-      if (int rc = gemm.batch(jobs, 6, (long long)n, rjobs, &nred)) return rc;
-      if (int rc = launch_reduce_batch(rjobs, nred, s)) return rc;
-      nred = 0;
-    }
-    if (int rc = gemm(w.op_gphi, 1, 1, w.op_t, 64, 64, (long long)n, lg.vel_w2, 64, 0, lg.vel_b2)) return rc;
+    LayerRev lr;
+    lr.n = (int)n; lr.N = N; lr.n_graphs = T * B; lr.ef_mod = frames ? T * B : B; lr.ne = ne;
+    lr.he = he; lr.xe = xe; lr.ve = ve; lr.Ms = st.Ms + l * n * 64; lr.Fs = st.Fs + l * n * 4;
+    lr.edge_fea = edge_fea; lr.bb = bblobs[l];
+    lr.gx = gx; lr.gv = gv; lr.gh = gh; lr.lg = &layer_grads[l];
+    lr.g_xin = w.gxe; lr.g_vin = w.gve; lr.g_hin = w.ghe;
+    if (int rc = egnn_layer_reverse(lr, w, gemm, s)) return rc;
     const int nxt = cur ^ 1;
     if (!tc) {   // no TimeConv: the layer-input gradients are the next (earlier) layer's output gradients
       hipMemcpyAsync(w.gx[nxt], w.gxe, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -1901,40 +1963,15 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
       gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
       continue;
     }
-    // ---- TimeConv_x reverse: x, v of the layer's TimeConv input ----
-    hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes,
-                       st.xs + l * n * 3, l > 0 ? st.ve + (l - 1) * n * 3 : st.vs, loc_mean, w.gxe, w.gve, tconvx_w[l], w.gx[nxt],
-                       w.gv[nxt], w.xpart, frames);
-    if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
-    {
-      // g_tconvx[l] [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M zero)
-      float* tmp = w.partial;
-      const int cnt = 2 * 2 * MMAX_T * 2;
-      const long long rows = (long long)BN * 3, slice = 256;
-      const int nb = (int)((rows + slice - 1) / slice);
-      hipLaunchKernelGGL(rows_reduce, dim3(nb), dim3(256), 0, s, w.xpart, rows, cnt, slice, tmp + 64);
-      if (int rc = check_launch("rows_reduce")) return rc;
-      hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, tmp + 64, nb, M, modes, g_tconvx[l]);
-      if (int rc = check_launch("tconvx_grad_finish")) return rc;
-    }
-    // ---- TimeConv reverse: h of the layer's TimeConv input ----
-    {
-      hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, tconv_w[l], modes,
-                         M, w.twb);
-      if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
-      TconvBwdArgs ta;
-      ta.BN = BN; ta.T = T; ta.M = M; ta.ntiles = (BN + 15) / 16;
-      ta.h = st.hs + l * n * 64; ta.gout = w.ghe; ta.wp = w.twf; ta.wb = w.twb; ta.gh = w.gh[nxt]; ta.wpart = w.tpart;
-      ta.mask = st.mask + (size_t)l * T * ta.ntiles * 16;
-      int TG = num_cus();
-      TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;
-      TG = ta.ntiles < TG ? ta.ntiles : TG;
-      if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
-      if (modes > M) hipMemsetAsync(g_tconv[l], 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
-      hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 + 63) / 64), dim3(256), 0, s, w.tpart, TG, M, modes,
-                         g_tconv[l]);
-      if (int rc = check_launch("tconv_wgrad_reduce")) return rc;
-    }
+    // ---- TimeConv_x / TimeConv reverse: x, v, h of the layer's TimeConv input ----
+    TconvRev tr;
+    tr.BN = BN; tr.T = T; tr.M = M; tr.modes = modes; tr.frames = frames;
+    tr.hs = st.hs + l * n * 64; tr.xs = st.xs + l * n * 3; tr.vs = l > 0 ? st.ve + (l - 1) * n * 3 : st.vs;
+    tr.lm = loc_mean; tr.tw = tconv_w[l]; tr.txw = tconvx_w[l];
+    tr.mask = st.mask + (size_t)l * T * ((BN + 15) / 16) * 16;
+    tr.gh = w.ghe; tr.gx = w.gxe; tr.gv = w.gve;
+    tr.g_hin = w.gh[nxt]; tr.g_xin = w.gx[nxt]; tr.g_vin = w.gv[nxt]; tr.g_tw = g_tconv[l]; tr.g_txw = g_tconvx[l];
+    if (int rc = tconv_reverse(tr, w, s)) return rc;
     cur = nxt;
     gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
   }
@@ -2198,6 +2235,102 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
   if (g_x_in) hipMemcpyAsync(g_x_in, gx, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   if (g_v_in) hipMemcpyAsync(g_v_in, gv, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   return check_launch("segno_backward");
+}
+
+}  // extern "C"
+
+// ---- layer-granular reverse entry points (egno_layer_bwd, spectral_tconv_bwd) ----
+extern "C" {
+
+size_t nonode_egnn_layer_bwd_workspace_bytes(int n_graphs, int N) {
+  if (n_graphs <= 0 || N < 2) return 0;
+  const size_t n = (size_t)n_graphs * N;
+  return (bwd_ws(nullptr, n_graphs, N, 1, 1).floats + n * (64 + 4 + 64 + 4)) * sizeof(float);
+}
+
+int nonode_egnn_layer_bwd(int variant, int n_graphs, int N, int n_edge_feat, int ef_mod, const float* h,
+                          const float* x, const float* v, const float* edge_fea, const float* blob,
+                          const float* bblob, const float* g_x, const float* g_v, const float* g_h,
+                          const nonode_layer_grads* grads, float* g_h_in, float* g_x_in, float* g_v_in,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if ((variant & 0xff) != NONODE_VARIANT_EGNO)
+    return fail(NONODE_EUNSUPPORTED, "egnn_layer_bwd: EGNO layers only (SEGNO: nonode_segno_backward)");
+  if (n_graphs <= 0 || N < 2 || n_edge_feat < 0 || n_edge_feat > 4 || ef_mod <= 0 || n_graphs % ef_mod)
+    return fail(NONODE_EUNSUPPORTED, "egnn_layer_bwd: n_graphs=%d N=%d ne=%d ef_mod=%d", n_graphs, N, n_edge_feat,
+                ef_mod);
+  if (!h || !x || !v || !blob || !bblob || !g_x || !grads || !g_h_in || !g_x_in || !g_v_in || !workspace ||
+      (n_edge_feat > 0 && !edge_fea))
+    return fail(NONODE_EINVAL, "egnn_layer_bwd: null pointer");
+  if (workspace_bytes < nonode_egnn_layer_bwd_workspace_bytes(n_graphs, N))
+    return fail(NONODE_EINVAL, "egnn_layer_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)n_graphs * N;
+  BwdWs w = bwd_ws(workspace, n_graphs, N, 1, 1);
+  float* Ms = (float*)workspace + w.floats;   // the forward's message / force sums (recomputed here)
+  float* Fs = Ms + n * 64;
+  float* ht = Fs + n * 4;                     // the forward's outputs (not needed, written by the recompute)
+  float* xt = ht + n * 64;
+  if (int rc = launch_layer<EGNO>(n_graphs, N, n_edge_feat, ef_mod, h, x, v, edge_fea, blob, 0.f, 1.f, 0, ht, xt,
+                                  nullptr, s, 1, nullptr, Ms, Fs))
+    return rc;
+  const float *gv = g_v, *gh = g_h;
+  if (!g_v) { hipMemsetAsync(w.gv[0], 0, n * 3 * sizeof(float), s); gv = w.gv[0]; }
+  if (!g_h) { hipMemsetAsync(w.gh[0], 0, n * 64 * sizeof(float), s); gh = w.gh[0]; }
+  Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
+  LayerRev lr;
+  lr.n = (int)n; lr.N = N; lr.n_graphs = n_graphs; lr.ef_mod = ef_mod; lr.ne = n_edge_feat;
+  lr.he = h; lr.xe = x; lr.ve = v; lr.Ms = Ms; lr.Fs = Fs; lr.edge_fea = edge_fea; lr.bb = bblob;
+  lr.gx = g_x; lr.gv = gv; lr.gh = gh; lr.lg = grads;
+  lr.g_xin = g_x_in; lr.g_vin = g_v_in; lr.g_hin = g_h_in;
+  return egnn_layer_reverse(lr, w, gemm, s);
+}
+
+size_t nonode_egno_tconv_bwd_workspace_bytes(int BN, int T, int modes) {
+  if (BN <= 0 || T <= 0 || T > TMAX || modes < 1 || modes > MMAX_T) return 0;
+  const size_t n = (size_t)BN * T;
+  const size_t mask_floats = 2 * (size_t)T * ((BN + 15) / 16) * 16;
+  return (mask_floats + bwd_ws(nullptr, BN, 1, T, effective_modes(T, modes)).floats + n * 70) * sizeof(float);
+}
+
+int nonode_egno_tconv_bwd(int BN, int T, int modes, const float* h, const float* x, const float* v,
+                          const float* loc_mean, const float* tconv_blob, const float* tconv_w,
+                          const float* tconvx_w, const float* g_h, const float* g_x, const float* g_v,
+                          float* g_h_in, float* g_x_in, float* g_v_in, float* g_tconv_w, float* g_tconvx_w,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (BN <= 0 || T <= 0 || T > TMAX || modes < 1 || modes > MMAX_T)
+    return fail(NONODE_EUNSUPPORTED, "egno_tconv_bwd: BN=%d T=%d modes=%d (training: modes <= %d)", BN, T, modes,
+                MMAX_T);
+  if (!h || !x || !v || !loc_mean || !tconv_blob || !tconv_w || !tconvx_w || !g_h_in || !g_x_in || !g_v_in ||
+      !g_tconv_w || !g_tconvx_w || !workspace)
+    return fail(NONODE_EINVAL, "egno_tconv_bwd: null pointer");
+  if (workspace_bytes < nonode_egno_tconv_bwd_workspace_bytes(BN, T, modes))
+    return fail(NONODE_EINVAL, "egno_tconv_bwd: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int M = effective_modes(T, modes);
+  const size_t n = (size_t)BN * T;
+  const size_t mask_floats = 2 * (size_t)T * ((BN + 15) / 16) * 16;
+  auto* mask = reinterpret_cast<unsigned long long*>(workspace);
+  float* base = (float*)workspace + mask_floats;
+  BwdWs w = bwd_ws(base, BN, 1, T, M);
+  float* ht = base + w.floats;   // forward outputs of the mask recompute (unused)
+  float* xt = ht + n * 64;
+  float* vt = xt + n * 3;
+  // the forward's LeakyReLU decisions, recomputed (the same kernel as the training forward)
+  TconvArgs a{};
+  a.BN = BN; a.T = T; a.M = M; a.Mfull = modes;
+  a.h = h; a.x = x; a.v = v; a.lm = loc_mean; a.wp = tconv_blob; a.wx = tconvx_w;
+  a.h_out = ht; a.x_out = xt; a.v_out = vt; a.frames = 0; a.mask_out = mask;
+  if (int rc = launch_tconv(false, a, s)) return rc;
+  const float *gx = g_x, *gv = g_v, *gh = g_h;
+  if (!g_x) { hipMemsetAsync(w.gx[0], 0, n * 3 * sizeof(float), s); gx = w.gx[0]; }
+  if (!g_v) { hipMemsetAsync(w.gv[0], 0, n * 3 * sizeof(float), s); gv = w.gv[0]; }
+  if (!g_h) { hipMemsetAsync(w.gh[0], 0, n * 64 * sizeof(float), s); gh = w.gh[0]; }
+  TconvRev tr;
+  tr.BN = BN; tr.T = T; tr.M = M; tr.modes = modes; tr.frames = 0;
+  tr.hs = h; tr.xs = x; tr.vs = v; tr.lm = loc_mean; tr.tw = tconv_w; tr.txw = tconvx_w; tr.mask = mask;
+  tr.gh = gh; tr.gx = gx; tr.gv = gv;
+  tr.g_hin = g_h_in; tr.g_xin = g_x_in; tr.g_vin = g_v_in; tr.g_tw = g_tconv_w; tr.g_txw = g_tconvx_w;
+  return tconv_reverse(tr, w, s);
 }
 
 }  // extern "C"

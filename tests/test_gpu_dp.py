@@ -1,6 +1,6 @@
 """Data-parallel EGNO training step on the HIP kernels (SURVEY §8 row e, C4's exchange step).
 
-Two ranks share cuda:0 (the gloo backend carries the collective, so no second GPU is needed): each
+The ranks share cuda:0 (the gloo backend carries the collective, so no second GPU is needed): each
 runs the HIP training forward + backward on its half of the batch with the reference's loss
 (main_simulation_simple_no.py:273-280), every p.grad is a view into one FlatGrads buffer, and ONE
 all-reduce of that buffer (then / world) gives the step's gradients. They must equal the
@@ -67,9 +67,11 @@ def _worker(rank, world, port, out, B):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("B", [8, 512])
-def test_dp_step_on_hip_kernels_equals_whole_batch(tmp_path, B):
-    """B=512: two ranks of 256 against the whole C4 shard.
+@pytest.mark.parametrize("world,B", [(2, 8), (2, 512), (8, 4096)])
+def test_dp_step_on_hip_kernels_equals_whole_batch(tmp_path, world, B):
+    """B=512: two ranks of 256 against the whole C4 shard. B=4096: C4's global batch as its eight
+    ranks of 512 (all on the one GPU, gloo carrying the all-reduce) against the whole-4096 step on
+    one GPU (the N=1 point of the strong-scaling curve).
 
     Checks, per parameter tensor:
       - the exchange itself: every rank holds exactly (g_0 + g_1) / 2 of the ranks' local gradients;
@@ -81,19 +83,19 @@ def test_dp_step_on_hip_kernels_equals_whole_batch(tmp_path, B):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     out = str(tmp_path / "dp_grads")
-    mp.start_processes(_worker, args=(2, port, out, B), nprocs=2, join=True, start_method="spawn")
-    r0, r1 = np.load(out + ".0.npz"), np.load(out + ".1.npz")
+    mp.start_processes(_worker, args=(world, port, out, B), nprocs=world, join=True, start_method="spawn")
+    rk = [np.load(out + f".{r}.npz") for r in range(world)]
     whole, _ = _step_grads(B, 0, B, allreduce=False)
     nonzero = 0
     for k, ref in whole.items():
-        dp = r0["dp::" + k]
-        assert np.array_equal(dp, r1["dp::" + k]), k
-        mean = (r0["local::" + k].astype(np.float64) + r1["local::" + k]) / 2
+        dp = rk[0]["dp::" + k]
+        assert all(np.array_equal(dp, r["dp::" + k]) for r in rk[1:]), k
+        mean = sum(r["local::" + k].astype(np.float64) for r in rk) / world
         assert np.abs(dp - mean).max() <= 1e-6 * max(np.abs(mean).max(), 1e-30), k
         if np.abs(ref).max() == 0:   # the last layer's h update does not reach the position loss
             assert np.abs(dp).max() == 0, k
             continue
         nonzero += 1
-        cond = max(np.abs(r0["local::" + k]).max(), np.abs(r1["local::" + k]).max()) / np.abs(ref).max()
-        check_rel(f"dp B={B} grad {k} (split cond {cond:.1f})", dp, ref, DPTOL * max(1.0, cond))
+        cond = max(np.abs(r["local::" + k]).max() for r in rk) / np.abs(ref).max()
+        check_rel(f"dp {world}x{B // world} grad {k} (split cond {cond:.1f})", dp, ref, DPTOL * max(1.0, cond))
     assert nonzero > 50

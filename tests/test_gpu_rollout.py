@@ -131,3 +131,71 @@ def test_rollout_rejects_mismatched_features():
                                  _dev(fx["raw::edge_attr_o"]), _dev(fx["in::edge_attr"]), _dev(fx["in::loc_mean"]), N,
                                  2, B, charges=None, num_steps=T,
                                  timesteps_out=torch.arange(1, 2 * T + 1, device=DEV).repeat(B, 1))
+
+
+def _c5_substeps(total=50, seed=0):
+    """C5's per-segment substep counts: draws in [5, 10) from default_rng(0) until they
+    sum to 50, the last one clipped (bench.py c5_substeps)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while sum(out) < total:
+        out.append(int(min(rng.integers(5, 10), total - sum(out))))
+    return out
+
+
+def _gravity_case(B, N, seed):
+    """SURVEY §8d gravity generator (synthetic_sim.py:370-378): masses 1 + 0.1 N(0,1), positions and
+    velocities N(0,1), centre-of-mass velocity removed; edge_attr [m_i m_j, |x_i - x_j|^2]."""
+    g = torch.Generator().manual_seed(seed)
+    mass = 1.0 + 0.1 * torch.randn(B, N, 1, generator=g)
+    loc = torch.randn(B, N, 3, generator=g)
+    vel = torch.randn(B, N, 3, generator=g)
+    vel = vel - (mass * vel).sum(1, keepdim=True) / mass.sum(1, keepdim=True)
+    return mass.to(DEV), loc.reshape(-1, 3).to(DEV), vel.reshape(-1, 3).to(DEV)
+
+
+def _gravity_rollout(m, mass, x, v, B, N, steps):
+    ei = pkg.harness.get_edges(B, N, DEV)
+    mm = mass.reshape(-1, 1)
+    ea = torch.cat([mm[ei[0]] * mm[ei[1]], ((x[ei[0]] - x[ei[1]]) ** 2).sum(1, keepdim=True)], 1)
+    with torch.no_grad():
+        return pkg.harness.segno_rollout(m, v.norm(dim=1, keepdim=True), x, ei, v, ea, len(steps), num_steps=steps,
+                                         charges=mass, energy_dataset="gravity", batch_size=B)
+
+
+def test_segno_c5_full_size_rollout():
+    """C5 at its real size: SEGNO gravity, B=256, N=100, the 50-frame multi-horizon rollout (the 8-wave
+    layer loop over 256 workgroups). First segment of 16 samples against the float64 torch path
+    (oracle/torch_ref.py, scatter mean: the reference's dense mean needs 259 GB here); E(3)
+    equivariance and batch independence on the whole batch."""
+    from oracle import torch_ref as tr
+    B, N = 256, 100
+    steps = _c5_substeps()
+    assert sum(steps) == 50
+    m = _segno(seed=51)
+    mass, x, v = _gravity_case(B, N, seed=52)
+    preds, en = _gravity_rollout(m, mass, x, v, B, N, steps)
+    assert preds.shape == (len(steps), B * N, 3) and torch.isfinite(preds).all() and torch.isfinite(en).all()
+    # first segment, 16 samples, against float64
+    Bc = 16
+    rows = Bc * N
+    p = {k: q.detach().cpu().double() for k, q in m.state_dict().items()}
+    r, c = tr.full_edges(Bc, N)
+    xd, vd, md = x[:rows].cpu().double(), v[:rows].cpu().double(), mass[:Bc].reshape(-1, 1).cpu().double()
+    ea = torch.cat([md[r] * md[c], ((xd[r] - xd[c]) ** 2).sum(1, keepdim=True)], 1)
+    with torch.no_grad():
+        ref = tr.segno_rollout(p, vd.norm(dim=1, keepdim=True), xd, r, c, vd, ea, steps[:1], md, dense_mean=False)
+    check_rel("C5 first segment (16 samples)", preds[0, :rows].cpu(), ref[0], TOL)
+    # E(3): rotated and translated inputs give rotated and translated positions
+    g = torch.Generator().manual_seed(53)
+    R, _ = torch.linalg.qr(torch.randn(3, 3, generator=g, dtype=torch.float64))
+    R = R.float().to(DEV)
+    sh = torch.tensor([0.7, -0.4, 1.1], device=DEV)
+    preds2, _ = _gravity_rollout(m, mass, x @ R.T + sh, v @ R.T, B, N, steps)
+    check_rel("C5 E(3) first segment", (preds[0] @ R.T + sh).cpu(), preds2[0].cpu(), TOL)
+    # later segments: chaotic growth of fp32 rounding differences over 50 substeps (SURVEY §4.2 item 5)
+    check_rel("C5 E(3) all segments", (preds @ R.T + sh).cpu(), preds2.cpu(), 1e-3)
+    # batch independence: samples 100..102 alone give the same trajectories as inside the batch
+    sl = slice(100 * N, 103 * N)
+    preds3, _ = _gravity_rollout(m, mass[100:103], x[sl], v[sl], 3, N, steps)
+    check_rel("C5 batch independence", preds3.cpu(), preds[:, sl].cpu(), 1e-6)
