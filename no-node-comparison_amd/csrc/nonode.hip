@@ -21,6 +21,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 
 #include "nonode.h"
 
@@ -429,6 +430,17 @@ __device__ __forceinline__ float dot_vp(const f4 (&a)[4], const float* vp, int g
   return group_sum(s);
 }
 
+// sum over the P lane groups of 16 / P columns inside each 16-lane row (P = 2: lanes e, e +- 8;
+// P = 4: e, e +- 4, e +- 8, e +- 12), by DPP row rotations in a fixed order (column packing of the
+// layer kernel's last tile)
+template <int R>
+__device__ __forceinline__ float row_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x120 + R, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float group_fold(float v, int P) {
+  if (P == 4) v += row_ror<4>(v);
+  return v + row_ror<8>(v);
+}
 // max over the 4 lane groups (the column max of an ECL activation)
 __device__ __forceinline__ float group_max(float v) {
   const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -851,7 +863,16 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     // are read from LDS (each read feeds two units' MFMAs); b2 / bc1 / wc2 stay in registers for
     // the edge phase.
     {
-      const int U = ctc * Nm1;
+      // Column packing of the chunk's last tile: a tile with Vl <= 16 / Pk valid receivers (Pk = 2 or 4)
+      // gives each group of 16 / Pk lane columns its own run of sender offsets, so the tile takes
+      // Kp = floor(Nm1 / Pk) packed units plus Nm1 - Pk Kp regular ones instead of Nm1 units (C3: 40
+      // receivers per chunk, 2.5 tiles: 57 -> 48 units; C5: 100 receivers, 693 -> 621). The groups'
+      // partial sums of a receiver are added across lanes (DPP) before the one flush of the segment.
+      const int Vl = (nend - rbase) - 16 * (ctc - 1);
+      const int Pk = (Vl <= 4 && Nm1 >= 8) ? 4 : ((Vl <= 8 && Nm1 >= 4) ? 2 : 1);
+      const int Kp = Nm1 / Pk;
+      const int Ul = Pk == 1 ? Nm1 : Kp + (Nm1 - Pk * Kp);
+      const int U = (ctc - 1) * Nm1 + Ul;
       // waves taking part: a tile must span at most 4 waves (two contributions per sum slot), so
       // every wave's range holds at least a third of a tile
       const int NWB = min(NW, 3 * ctc);
@@ -865,12 +886,23 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       }
       #pragma unroll 1
       while (u < u1) {
-        const int tau = u / Nm1;
-        const int k_lo = u - tau * Nm1 + 1;
-        const int k_hi = min(Nm1, k_lo + (u1 - u) - 1);
+        const int tau = min(u / Nm1, ctc - 1);
+        const int k_lo = u - tau * Nm1 + 1;                                   // unit k: offsets k (+ kof)
+        const int k_hi = min(tau == ctc - 1 ? Ul : Nm1, k_lo + (u1 - u) - 1);
         u += k_hi - k_lo + 1;
         // ---- tile state ----
-        const int rl = 16 * tau + e;
+        // packed tile: lane column e is receiver ee of lane group hp, whose packed unit k takes sender
+        // offset k + hp Kq; units k > Kq are regular (offset k + (P - 1) Kq), groups hp > 0 masked
+        const int P = tau == ctc - 1 ? Pk : 1;        // wave-uniform
+        const int Kq = P == 1 ? Nm1 : Kp;
+        const int hp = P == 1 ? 0 : (P == 2 ? e >> 3 : e >> 2);
+        const int ee = P == 1 ? e : (P == 2 ? e & 7 : e & 3);
+        const int kof = hp * Kq;
+        const int kreg = (P - 1) * Kq;
+        const int rl = 16 * tau + ee;
+        // this lane's sender offset for unit k (always in [1, Nm1]) and whether it contributes
+        auto lane_k = [&](int k) __attribute__((always_inline)) { return k <= Kq ? k + kof : k + kreg; };
+        auto lane_on = [&](int k) __attribute__((always_inline)) { return k <= Kq || hp == 0; };
         const int r = rbase + rl;
         const bool rvalid = r < nend;
         const int rc = rvalid ? r : nend - 1;
@@ -930,7 +962,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             for (int mo = 0; mo < 4; ++mo) a[mo] = mfma(wf[mo], bv, a[mo]);
           }
         };
-        auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2) __attribute__((always_inline)) {
+        auto tail = [&](f4 (&c1)[4], float r0, float r1, float r2, bool on) __attribute__((always_inline)) {
           silu_ecl(c1);
           float c = (PAIR ? dot_r(c1, rWC2) : dot_vp(c1, vWC2_, g)) + bc2;
           if constexpr (ctanh) c = tanhf(c);
@@ -940,7 +972,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             f1 = fminf(fmaxf(f1, -100.f), 100.f);
             f2 = fminf(fmaxf(f2, -100.f), 100.f);
           }
-          fs0 += f0; fs1 += f1; fs2 += f2;
+          fs0 = on ? fs0 + f0 : fs0; fs1 = on ? fs1 + f1 : fs1; fs2 = on ? fs2 + f2 : fs2;
         };
 
         const h8* w2h = reinterpret_cast<const h8*>(sW);
@@ -1014,22 +1046,23 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             float cc;
             edge_f(c, r0, r1, r2, f0, f1, f2, cc);
           };
+          const int kp_hi = min(k_hi, Kq);   // pairs of packed (or ordinary) units
           float e0[KF], e1[KF];
-          fetch_ef(k, e0);
-          fetch_ef(min(k + 1, k_hi), e1);
+          fetch_ef(min(k, kp_hi) + kof, e0);
+          fetch_ef(min(k + 1, kp_hi) + kof, e1);
 #pragma unroll 1
-          for (; k + 1 <= k_hi; k += 2) {
+          for (; k + 1 <= kp_hi; k += 2) {
             float n0[KF], n1[KF];
-            fetch_ef(min(k + 2, k_hi), n0);
-            fetch_ef(min(k + 3, k_hi), n1);
+            fetch_ef(min(k + 2, kp_hi) + kof, n0);
+            fetch_ef(min(k + 3, kp_hi) + kof, n1);
             f4 a0[4], a1[4], m0[4], m1[4];
             float r00, r01, r02, r10, r11, r12;
             float f00, f01, f02, f10, f11, f12;
             f4 pm[4];
             float cA, cB;   // coordinate-MLP outputs: non-finite iff an fp16 hi part overflowed
             bool okA, okB;  // finite inputs (node flags, |r|^2)
-            head2(k, e0, a0, r00, r01, r02, okA);
-            head2(k + 1, e1, a1, r10, r11, r12, okB);
+            head2(k + kof, e0, a0, r00, r01, r02, okA);
+            head2(k + 1 + kof, e1, a1, r10, r11, r12, okB);
             STAMP(0);
             silu_ecl(a0);
             silu_ecl(a1);
@@ -1072,8 +1105,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               int kg = k;
               asm volatile("" : "+v"(kg));
               f4 x0[4], x1[4];
-              exact_unit(kg, e0, x0, f00, f01, f02);
-              exact_unit(kg + 1, e1, x1, f10, f11, f12);
+              exact_unit(kg + kof, e0, x0, f00, f01, f02);
+              exact_unit(kg + 1 + kof, e1, x1, f10, f11, f12);
 #pragma unroll
               for (int mt = 0; mt < 4; ++mt) pm[mt] = x0[mt] + x1[mt];
             }
@@ -1127,12 +1160,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               f2 = fminf(fmaxf(f2, -100.f), 100.f);
             }
           };
-          float e0[KF];
-          fetch_ef(min(k, k_hi), e0);
-#pragma unroll 1
-          for (; k <= k_hi; ++k) {
+          // one unit per iteration: the packed (or ordinary) units, then a tile's few regular units
+          // (k > Kq, lane groups hp > 0 masked) in a second instance of the same body
+          auto unit1 = [&](int k, int k_end, float (&e0)[KF], auto masked) __attribute__((always_inline)) {
             float en[KF];
-            fetch_ef(min(k + 1, k_hi), en);
+            fetch_ef(lane_k(min(k + 1, k_end)), en);
             int loff = 0;
             asm volatile("" : "+v"(loff));   // fragment / bias reads stay in the loop
             const h8* w2l = w2h + loff;
@@ -1140,7 +1172,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             f4 a[4], m[4];
             float r0, r1, r2, f0, f1, f2, c;
             bool ok;
-            head1(k, e0, a, r0, r1, r2, ok);
+            head1(lane_k(k), e0, a, r0, r1, r2, ok);
             silu_ecl(a);
             load_vp(m, vB2_ + loff, g);
             {
@@ -1159,7 +1191,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             if (__builtin_expect(__any(ok && !__builtin_isfinite(c)), 0)) {
               int kg = k;
               asm volatile("" : "+v"(kg));   // keeps the recompute in the branch (see the pair loop)
-              head1(kg, e0, a, r0, r1, r2, ok);
+              head1(lane_k(kg), e0, a, r0, r1, r2, ok);
               silu_ecl(a);
               load_vp(m, vB2_, g);
               mm64_scaled(m, w2h, a, lane, us_w2);
@@ -1168,21 +1200,40 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               mm64_scaled(a, wc1h, m, lane, us_wc1);
               coord1(a, vWC2_, r0, r1, r2, f0, f1, f2, c);
             }
+            if constexpr (decltype(masked)::value) {
+              const bool on = lane_on(k);
 #pragma unroll
-            for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
-            fs0 += f0; fs1 += f1; fs2 += f2;
+              for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) msum[mt][q] = on ? msum[mt][q] + m[mt][q] : msum[mt][q];
+              fs0 = on ? fs0 + f0 : fs0; fs1 = on ? fs1 + f1 : fs1; fs2 = on ? fs2 + f2 : fs2;
+            } else {
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
+              fs0 += f0; fs1 += f1; fs2 += f2;
+            }
 #pragma unroll
             for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
-          }
+          };
+          float e0[KF];
+          fetch_ef(lane_k(min(k, k_hi)), e0);
+          const int ko_hi = min(k_hi, Kq);
+#pragma unroll 1
+          for (; k <= ko_hi; ++k) unit1(k, ko_hi, e0, std::false_type{});
+          if (k <= k_hi) fetch_ef(lane_k(k), e0);
+#pragma unroll 1
+          for (; k <= k_hi; ++k) unit1(k, k_hi, e0, std::true_type{});
         }
         // One unit (16 edges) per iteration; the next unit's edge inputs are in flight meanwhile.
+        // (the pair loop's odd unit and a packed tile's regular units: lane groups hp > 0 masked there)
         float e0[KF];
-        fetch_ef(min(k, k_hi), e0);
+        fetch_ef(lane_k(min(k, k_hi)), e0);
         STAMP(8);
 #pragma unroll 1
         for (; k <= k_hi; ++k) {
           float en[KF];
-          fetch_ef(min(k + 1, k_hi), en);
+          fetch_ef(lane_k(min(k + 1, k_hi)), en);
+          const bool on = lane_on(k);
           // fragment / bias reads stay in the loop (LICM would pin them in VGPRs)
           int loff = 0;
           asm volatile("" : "+v"(loff));
@@ -1192,7 +1243,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
           const float* vBC1l = vBC1_ + loff;
           f4 a[4], m[4];
           float r0, r1, r2;
-          head(k, e0, a, r0, r1, r2);
+          head(lane_k(k), e0, a, r0, r1, r2);
 #pragma unroll
           for (int kf = 0; kf < KF; ++kf) e0[kf] = en[kf];
           STAMP(0);
@@ -1213,7 +1264,9 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
           STAMP(1);
           silu_ecl(m);
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) msum[mt] += m[mt];
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) msum[mt][q] = on ? msum[mt][q] + m[mt][q] : msum[mt][q];
           if (PAIR) {
 #pragma unroll
             for (int mt = 0; mt < 4; ++mt) a[mt] = rBC1[mt];
@@ -1228,11 +1281,18 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             mfma_h16(a, wc1l, mh, ml, lane, us_wc1);  // SiLU(Wc1 m + bc1)
           }
           STAMP(2);
-          tail(a, r0, r1, r2);
+          tail(a, r0, r1, r2, on);
           STAMP(3);
         }
         // ---- flush the segment's partial sums ----
-        if (rvalid) {
+        if (P > 1) {   // wave-uniform: add the lane groups' partial sums of each receiver (DPP, fixed order)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) msum[mt][q] = group_fold(msum[mt][q], P);
+          fs0 = group_fold(fs0, P); fs1 = group_fold(fs1, P); fs2 = group_fold(fs2, P);
+        }
+        if (rvalid && hp == 0) {
           const int slot = wave & 1;
           float* mrow = sM + slot * slotM + rl * ROWP + 4 * g;
 #pragma unroll
