@@ -441,6 +441,65 @@ __device__ __forceinline__ float group_fold(float v, int P) {
   if (P == 4) v += row_ror<4>(v);
   return v + row_ror<8>(v);
 }
+
+// ---- balanced split of a chunk's edge units over the waves (pair mode) ----------------------------
+// A wave's range is walked tile segment by tile segment: per segment a fixed cost (tile state,
+// fragment loads, the flush), then pairs of units up to the tile's packed limit Q and single units
+// after (the pair loop's odd unit, a packed tile's regular units). Modelled costs (stamped, C3:
+// ~3.2K cycles per segment, ~6.4K per pair or single on average):
+constexpr int CS_SEG = 2, CS_PAIR = 4, CS_ONE = 3;
+// cost of units k..kend (1-based offsets) of a tile with packed limit Q
+__device__ __forceinline__ int seg_cost(int k, int kend, int Q) {
+  const int lp = max(min(kend, Q) - k + 1, 0), lr = max(kend - max(k, Q + 1) + 1, 0);
+  return CS_SEG + CS_PAIR * (lp >> 1) + CS_ONE * ((lp & 1) + lr);
+}
+// the most units from offset k on (tile of L units, packed limit Q) within budget b
+__device__ __forceinline__ int seg_take(int k, int L, int Q, int b) {
+  int bb = b - CS_SEG;
+  if (bb < CS_ONE) return 0;
+  const int lp = max(Q - k + 1, 0);
+  const int np = bb / CS_PAIR;
+  if (2 * np < lp) return 2 * np + (bb - CS_PAIR * np >= CS_ONE ? 1 : 0);
+  bb -= CS_PAIR * (lp >> 1) + CS_ONE * (lp & 1);
+  return lp + min(L - max(k, Q + 1) + 1, bb / CS_ONE);
+}
+// Contiguous ranges of the U = (ctc - 1) Nm1 + Ul units (last tile: Ul units, packed limit Ql) over
+// NW waves with the smallest modelled maximum (binary search on it, greedy fill). Wave w takes units
+// [cut[w], cut[w + 1]). Returns whether budget T fits (cut then holds the fill).
+// (cut: this wave's own LDS copy: every lane writes the same values)
+template <int NW>
+__device__ __forceinline__ bool unit_fill(int T, int ctc, int Nm1, int Ul, int Ql, int* cut) {
+  int w = 0, b = T, t = 0, k = 1;
+  const int U = (ctc - 1) * Nm1 + Ul;
+  cut[0] = 0;
+  while (t < ctc) {
+    const int L = t == ctc - 1 ? Ul : Nm1, Q = t == ctc - 1 ? Ql : Nm1;
+    const int n = seg_take(k, L, Q, b);
+    if (k + n - 1 == L) {
+      b -= seg_cost(k, L, Q);
+      ++t;
+      k = 1;
+    } else {
+      k += n;
+      if (++w == NW) return false;
+      b = T;
+      cut[w] = t * Nm1 + k - 1;
+    }
+  }
+  for (int i = w + 1; i <= NW; ++i) cut[i] = U;
+  return true;
+}
+template <int NW>
+__device__ __forceinline__ void unit_split(int ctc, int Nm1, int Ul, int Ql, int* cut) {
+  int lo = 0, hi = 0;
+  for (int t = 0; t < ctc; ++t) hi += seg_cost(1, t == ctc - 1 ? Ul : Nm1, t == ctc - 1 ? Ql : Nm1);
+  while (lo < hi) {   // smallest T that fits
+    const int mid = (lo + hi) >> 1;
+    if (unit_fill<NW>(mid, ctc, Nm1, Ul, Ql, cut)) hi = mid;
+    else lo = mid + 1;
+  }
+  unit_fill<NW>(lo, ctc, Nm1, Ul, Ql, cut);
+}
 // max over the 4 lane groups (the column max of an ECL activation)
 __device__ __forceinline__ float group_max(float v) {
   const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -659,6 +718,10 @@ struct LayerArgs {
   // writes pp_*[s&1], the last step the *_out arrays
   float* pp_h[2]; float* pp_x[2]; float* pp_v[2];
   int steps;
+  // substep fusion (steps > 1, one whole-graph chunk per workgroup): fuse: the node update of step
+  // t also builds step t+1's projection tables and positions in LDS (no phase A, no barrier);
+  // keep: h and v stay in LDS between steps too (only the last step stores to global memory)
+  int fuse, keep;
   // training forward only (else null): per-receiver message sums (true scale) [n][64] and force
   // sums [n][4] (f summed over the N-1 senders, before the mean and clamp)
   float* m_out; float* f_out;
@@ -674,9 +737,9 @@ struct LayerArgs {
 };
 
 // LDS of one chunk: ct receiver tiles (P, two message-sum slots, two force-sum slots) and s_rows senders
-size_t layer_lds_floats(int ct, int s_rows) {
+size_t layer_lds_floats(int ct, int s_rows, int keep = 0) {
   return 8192 + EDGE_STAGE_FLOATS + (size_t)ct * 16 * ROWP * 3 + (size_t)s_rows * (ROWP + 4) +
-         (size_t)ct * 16 * 4 * 2;
+         (size_t)ct * 16 * 4 * 2 + (keep ? (size_t)ct * 16 * (ROWP + 4) : 0);
 }
 
 // One workgroup owns a contiguous range of whole graphs (so every sender of its receivers is its
@@ -684,10 +747,12 @@ size_t layer_lds_floats(int ct, int s_rows) {
 // Per chunk:  A) P = W1[h_i] h + b1 for receivers, Q = W1[h_j] h for every sender of the touched
 //                graphs (LDS tables), sender positions;
 //             B) units (tile, k): receiver r (lane column) meets sender (n + k) mod N of its graph;
-//                edge MLP + coord MLP on MFMA. The chunk's units are split evenly over the waves
-//                (contiguous ranges); wave w flushes its partial message / force sums of a tile
-//                into slot w & 1. A tile spans at most 4 consecutive waves, so each slot of a
-//                receiver gets at most two contributions and the LDS float atomics commute exactly;
+//                edge MLP + coord MLP on MFMA. The chunk's units are split over the waves in
+//                contiguous ranges (four waves: balanced by a cost model of pairs, single units and
+//                tile segments; eight: evenly); wave w flushes its partial message / force sums of a
+//                tile into slot w & 1. A tile spans at most 4 consecutive waves, so each slot of a
+//                receiver gets at most two contributions: a sole contributor stores, two add by LDS
+//                float atomics onto zero, which commute exactly;
 //             C) node update per tile (sums = slot 0 + slot 1): x (and v) update, node MLP, stores.
 // A chunk is a fixed number (cg) of whole graphs, or a fixed slice of one graph's receivers when a
 // graph does not fit, so its tile layout and work split depend only on (cg, ct, N): the layer's
@@ -716,6 +781,10 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   float* sM = sX + p.s_rows * 4;                 // [2][ct*16][ROWP] message sums (slots 0 | 1)
   float* sF = sM + 2 * p.ct * 16 * ROWP;         // [2][ct*16][4]   force sums (slots 0 | 1)
   const int slotM = p.ct * 16 * ROWP, slotF = p.ct * 16 * 4;
+  float* sH = sF + 2 * slotF;                    // keep only: [ct*16][ROWP] h of the chunk's rows
+  float* sVl = sH + p.ct * 16 * ROWP;            // keep only: [ct*16][4]    v of the chunk's rows
+  // (SEGNO only: the EGNO layer runs one step per launch and carries none of it)
+  const bool fused = VARIANT == SEGNO && p.fuse != 0, keep = fused && p.keep != 0;
 
   for (int i = tid; i < 2048; i += NW * 64) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_H16)[i];
   if (tid < EDGE_STAGE_FLOATS / 4)
@@ -756,6 +825,35 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     const int ctc = (nend - rbase + 15) >> 4;
     return p.cpg == 1 ? ctc : ctc + ((S + 15) >> 4);
   };
+  // P = W1[h_i] h + b1 and Q = W1[h_j] h rows of a whole-graph tile from its h (ECL fragments), and the
+  // rows' input-finiteness flags (sX slot 3): the edge guard only recomputes pairs whose inputs are
+  // finite (a non-finite state, e.g. a diverged rollout, cannot be helped)
+  auto proj_tile = [&](const f4 (&hin)[4], const float* blob, int local, bool valid) __attribute__((always_inline)) {
+    f4 ap[4], aq[4];
+    load_vp(ap, blob + OFF_VEC + V_B1 * 64, g);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) aq[mt] = f4{0.f, 0.f, 0.f, 0.f};
+    if (__builtin_expect(__any(amax_ecl(hin) > H16_LIMIT), 0)) {
+      mfma_dense<4>(ap, blob + OFF_WA, hin, lane);
+      mfma_dense<4>(aq, blob + OFF_WB, hin, lane);
+    } else {
+      h8 xh[2], xl[2];
+      h16_split(hin, xh, xl);
+      mfma_h16(ap, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), xh, xl, lane, h16_us(blob + OFF_SCAL, HS_N + H_WA));
+      mfma_h16(aq, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), xh, xl, lane, h16_us(blob + OFF_SCAL, HS_N + H_WB));
+    }
+    float sa = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sa += fabsf(ap[mt][q]) + fabsf(aq[mt][q]);
+    sa = group_sum(sa);
+    if (valid) {
+      store_ecl(sP + local * ROWP, ap, g);
+      store_ecl(sQ + local * ROWP, aq, g);
+      if (g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;
+    }
+  };
   auto proj_job = [&](const float* __restrict__ hI, const float* blob, int rbase, int nend, int s0, int S,
                       int job) __attribute__((always_inline)) {
     int joff = 0;
@@ -764,33 +862,10 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     if (p.cpg == 1) {
       const int local = job * 16 + e;
       const bool valid = rbase + local < nend;
-      f4 hin[4], ap[4], aq[4];
+      f4 hin[4];
       load_ecl(hin, hI + (size_t)(valid ? rbase + local : nend - 1) * HID, g);
-      load_vp(ap, blob + OFF_VEC + V_B1 * 64, g);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) aq[mt] = f4{0.f, 0.f, 0.f, 0.f};
-      if (__builtin_expect(__any(amax_ecl(hin) > H16_LIMIT), 0)) {
-        mfma_dense<4>(ap, blob + OFF_WA, hin, lane);
-        mfma_dense<4>(aq, blob + OFF_WB, hin, lane);
-      } else {
-        h8 xh[2], xl[2];
-        h16_split(hin, xh, xl);
-        mfma_h16(ap, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), xh, xl, lane, h16_us(blob + OFF_SCAL, HS_N + H_WA));
-        mfma_h16(aq, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), xh, xl, lane, h16_us(blob + OFF_SCAL, HS_N + H_WB));
-      }
-      // input-finiteness flag of the node (sX slot 3): the edge guard only recomputes pairs whose
-      // inputs are finite (a non-finite state, e.g. a diverged rollout, cannot be helped)
-      float sa = 0.f;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sa += fabsf(ap[mt][q]) + fabsf(aq[mt][q]);
-      sa = group_sum(sa);
-      if (valid) {
-        store_ecl(sP + local * ROWP, ap, g);
-        store_ecl(sQ + local * ROWP, aq, g);
-        if (g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;
-      }
+      if (keep && valid) store_ecl(sH + local * ROWP, hin, g);
+      proj_tile(hin, blob, local, valid);
       return;
     }
     const int ctc = (nend - rbase + 15) >> 4;
@@ -819,13 +894,18 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
     if (valid && !isP && g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;   // sender flag
   };
-  auto load_sx = [&](const float* __restrict__ xI, int s0, int S) __attribute__((always_inline)) {
+  auto load_sx = [&](const float* __restrict__ xI, const float* __restrict__ vI, int s0, int S) __attribute__((always_inline)) {
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
       sX[s * 4 + d] = xI[(size_t)(s0 + s) * 3 + d];
+      if (keep) sVl[s * 4 + d] = vI[(size_t)(s0 + s) * 3 + d];
     }
   };
   STAMP_DECL
+  // edge-unit ranges of the waves for the last chunk shape (each wave its own copy)
+  __shared__ int s_cut[NW][NW + 1];
+  int* cut = s_cut[wave];
+  int cut_ctc = -1, cut_vl = -1;
   #pragma unroll 1
   for (int step = 0; step < p.steps; ++step) {
   const float* __restrict__ hI = step == 0 ? p.h : p.pp_h[(step - 1) & 1];
@@ -834,17 +914,17 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   float* hO = step == p.steps - 1 ? p.h_out : p.pp_h[step & 1];
   float* xO = step == p.steps - 1 ? p.x_out : p.pp_x[step & 1];
   float* vO = step == p.steps - 1 ? p.v_out : p.pp_v[step & 1];
-  {   // ---------------- phase A of the step's first chunk ----------------
+  if (!fused || step == 0) {   // ---------------- phase A of the step's first chunk ----------------
     int rbase, nend, s0, S;
     chunk_at(ch0, rbase, nend, s0, S);
-    load_sx(xI, s0, S);
+    load_sx(xI, vI, s0, S);
     const int J = proj_jobs(rbase, nend, S);
     #pragma unroll 1
     for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job);
+    STAMP(6);
+    __syncthreads();
+    STAMP(7);
   }
-  STAMP(6);
-  __syncthreads();
-  STAMP(7);
   #pragma unroll 1
   for (int ci = ch0; ci < ch1; ++ci) {
     // keep per-chunk loads of weights/vectors inside the loop (LICM would pin them in VGPRs
@@ -873,11 +953,19 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       const int Kp = Nm1 / Pk;
       const int Ul = Pk == 1 ? Nm1 : Kp + (Nm1 - Pk * Kp);
       const int U = (ctc - 1) * Nm1 + Ul;
-      // waves taking part: a tile must span at most 4 waves (two contributions per sum slot), so
-      // every wave's range holds at least a third of a tile
-      const int NWB = min(NW, 3 * ctc);
-      const int u1 = wave < NWB ? ((wave + 1) * U) / NWB : 0;
-      int u = wave < NWB ? (wave * U) / NWB : 0;
+      // a tile must span at most 4 waves (two contributions per sum slot)
+      if (ctc != cut_ctc || Vl != cut_vl) {   // chunk shapes repeat (every step, every full chunk)
+        cut_ctc = ctc;
+        cut_vl = Vl;
+        if constexpr (PAIR) {   // four waves: any tile spans at most four; ranges balanced by modelled cost
+          unit_split<NW>(ctc, Nm1, Ul, Pk == 1 ? Nm1 : Kp, cut);
+        } else {                // eight waves: every wave's range holds at least a third of a tile
+          const int NWB = min(NW, 3 * ctc);
+          for (int i = 0; i <= NW; ++i) cut[i] = i < NWB ? (i * U) / NWB : U;
+        }
+      }
+      const int u1 = cut[wave + 1];
+      int u = cut[wave];
       f4 rB2[4], rBC1[4], rWC2[4];
       if (PAIR) {
         load_vp(rB2, vB2_, g);
@@ -1292,18 +1380,32 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             for (int q = 0; q < 4; ++q) msum[mt][q] = group_fold(msum[mt][q], P);
           fs0 = group_fold(fs0, P); fs1 = group_fold(fs1, P); fs2 = group_fold(fs2, P);
         }
+        // the only contributor to its sum slot of this tile (no other wave of the same slot parity
+        // has units in it) stores; else the slot's two contributions are LDS float atomics (onto
+        // zero: exact and order-free either way)
+        const int t0 = tau * Nm1, t1 = t0 + (tau == ctc - 1 ? Ul : Nm1);
+        bool solo = true;
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          if (w != wave && ((w ^ wave) & 1) == 0 && cut[w] < cut[w + 1] && cut[w] < t1 && cut[w + 1] > t0)
+            solo = false;
         if (rvalid && hp == 0) {
           const int slot = wave & 1;
-          float* mrow = sM + slot * slotM + rl * ROWP + 4 * g;
+          float* mrow = sM + slot * slotM + rl * ROWP;
+          float* frow = sF + slot * slotF + rl * 4;
+          if (solo) {
+            store_ecl(mrow, msum, g);
+            if (g == 0) *reinterpret_cast<f4*>(frow) = f4{fs0, fs1, fs2, 0.f};
+          } else {
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt)
+            for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) atomicAdd(mrow + 16 * mt + q, msum[mt][q]);
-          if (g == 0) {
-            float* frow = sF + slot * slotF + rl * 4;
-            atomicAdd(frow + 0, fs0);
-            atomicAdd(frow + 1, fs1);
-            atomicAdd(frow + 2, fs2);
+              for (int q = 0; q < 4; ++q) atomicAdd(mrow + 16 * mt + 4 * g + q, msum[mt][q]);
+            if (g == 0) {
+              atomicAdd(frow + 0, fs0);
+              atomicAdd(frow + 1, fs1);
+              atomicAdd(frow + 2, fs2);
+            }
           }
         }
         STAMP(9);
@@ -1323,7 +1425,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       int nrb = 0, nne = 0, ns0 = 0, nS = 0;
       if (has_next) {
         chunk_at(ci + 1, nrb, nne, ns0, nS);
-        load_sx(xI, ns0, nS);
+        load_sx(xI, vI, ns0, nS);
       }
       const int J = ctc + (has_next ? proj_jobs(nrb, nne, nS) : 0);
       constexpr int C_COST = 4;
@@ -1353,9 +1455,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         const int r = rbase + rl;
         const bool rvalid = r < nend;
         const int rc = rvalid ? r : nend - 1;
+        const int lc = rc - rbase;   // the row in the chunk tables (fused: whole-graph chunk)
         f4 in8[8];
         f4 hr[4], Mr[4], Mb[4];
-        load_ecl(hr, hI + (size_t)rc * HID, g);
+        if (keep) load_ecl(hr, sH + lc * ROWP, g);
+        else load_ecl(hr, hI + (size_t)rc * HID, g);
         load_ecl(Mr, sM + rl * ROWP, g);
         load_ecl(Mb, sM + slotM + rl * ROWP, g);
   #pragma unroll
@@ -1372,10 +1476,11 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
             *reinterpret_cast<f4*>(sF + slotF + rl * 4) = z4[0];
           }
         }
-        const float* xp = xI + (size_t)rc * 3;
-        const float* vpn = vI + (size_t)rc * 3;
-        const float x0 = xp[0], x1 = xp[1], x2 = xp[2];
-        const float v0 = vpn[0], v1 = vpn[1], v2 = vpn[2];
+        float x0, x1, x2, v0, v1, v2;
+        if (fused) { x0 = sX[lc * 4 + 0]; x1 = sX[lc * 4 + 1]; x2 = sX[lc * 4 + 2]; }
+        else { x0 = xI[(size_t)rc * 3 + 0]; x1 = xI[(size_t)rc * 3 + 1]; x2 = xI[(size_t)rc * 3 + 2]; }
+        if (keep) { v0 = sVl[lc * 4 + 0]; v1 = sVl[lc * 4 + 1]; v2 = sVl[lc * 4 + 2]; }
+        else { v0 = vI[(size_t)rc * 3 + 0]; v1 = vI[(size_t)rc * 3 + 1]; v2 = vI[(size_t)rc * 3 + 2]; }
         float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
         if (VARIANT == EGNO) {
           // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
@@ -1427,7 +1532,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
           store_ecl(p.m_out + (size_t)r * HID, mt4, g);
           if (g == 0 && p.f_out) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
         }
-        if (rvalid) {
+        const bool next = fused && step + 1 < p.steps;   // fused: this tile's rows of step + 1 in LDS
+        if (rvalid && !(keep && next)) {
           store_ecl(hO + (size_t)r * HID, hn, g);
           if (g == 0) {
             float* xo = xO + (size_t)r * 3;
@@ -1437,6 +1543,16 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
               vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
             }
           }
+        }
+        if (next) {
+          if (rvalid) {
+            if (keep) store_ecl(sH + rl * ROWP, hn, g);
+            if (g == 0) {
+              sX[rl * 4 + 0] = nx0; sX[rl * 4 + 1] = nx1; sX[rl * 4 + 2] = nx2;
+              if (keep) { sVl[rl * 4 + 0] = nv0; sVl[rl * 4 + 1] = nv1; sVl[rl * 4 + 2] = nv2; }
+            }
+          }
+          proj_tile(hn, bj, rl, rvalid);
         }
       }
     }
@@ -1809,6 +1925,14 @@ __global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, cons
 }
 
 // ---- host-side launchers ----------------------------------------------------------------------
+// dynamic LDS of the layer kernel: the 160 KB of a CU less 1 KB for its static tables (the waves'
+// edge-unit cut tables, <= 288 B)
+constexpr int LAYER_DYN_LDS_MAX = 159 * 1024;
+// integer diagnostics switch from the environment (A/B builds of one library): 0 when unset
+int getenv_int(const char* name) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : 0;
+}
 // NONODE_XCD=0 turns off the XCD-aware tile / chunk order of the EGNO forward
 bool xcd_on() {
   static const int on = getenv("NONODE_XCD") ? atoi(getenv("NONODE_XCD")) : 1;
@@ -1818,8 +1942,8 @@ template <int VARIANT, int NW>
 void launch_cfg(int kf, int G, size_t lds, hipStream_t stream, const LayerArgs& a) {
   static std::once_flag once;
   std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 1, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LAYER_DYN_LDS_MAX);
+    hipFuncSetAttribute((const void*)egnn_layer_kernel<VARIANT, 2, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LAYER_DYN_LDS_MAX);
   });
   if (kf == 1) hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 1, NW>), dim3(G), dim3(NW * 64), lds, stream, a);
   else hipLaunchKernelGGL((egnn_layer_kernel<VARIANT, 2, NW>), dim3(G), dim3(NW * 64), lds, stream, a);
@@ -1842,7 +1966,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   // graphs per chunk: at most the graphs per CU, at most 8 tiles, within LDS; among those the one
   // whose rows fill its tiles best (ties: the larger). N = 20: 4 graphs = 80 rows = 5 full tiles.
   // A graph of more than 8 tiles (or beyond the LDS) is cut into cpg receiver slices of ct tiles.
-  constexpr size_t LDS_MAX = 160 * 1024;
+  constexpr size_t LDS_MAX = LAYER_DYN_LDS_MAX;
   const int cap = n_graphs / cus > 1 ? n_graphs / cus : 1;
   int cg = 0, cpg = 1, ct = 0;
   double best = -1.0;
@@ -1861,9 +1985,12 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
     ct = ((N + cpg - 1) / cpg + 15) / 16;   // the same slice count with the least padding
   }
   const int s_rows = cg * N;
-  const size_t lds = layer_lds_floats(ct, s_rows) * 4;
   const int n_units = (n_graphs + cg - 1) / cg;
   const int G = n_units < cus ? n_units : cus;
+  // substep fusion needs one whole-graph chunk per workgroup; keeping h, v in LDS needs the room
+  const int fuse = steps > 1 && cpg == 1 && n_units <= cus;
+  const int keep = fuse && layer_lds_floats(ct, s_rows, 1) * 4 <= LDS_MAX && !getenv_int("NONODE_NO_KEEP");
+  const size_t lds = layer_lds_floats(ct, s_rows, keep) * 4;
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
@@ -1871,6 +1998,8 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   a.cg = cg; a.cpg = cpg; a.n_units = n_units; a.ct = ct; a.s_rows = s_rows;
   if (steps < 1 || (steps > 1 && !pp)) return fail(NONODE_EINVAL, "layer: steps=%d", steps);
   a.steps = steps;
+  a.fuse = fuse && !getenv_int("NONODE_NO_FUSE");
+  a.keep = a.fuse && keep;
   a.m_out = m_out; a.f_out = f_out;
   for (int i = 0; i < 2; ++i) {
     a.pp_h[i] = pp ? pp[i] : nullptr;

@@ -199,3 +199,39 @@ def test_segno_c5_full_size_rollout():
     sl = slice(100 * N, 103 * N)
     preds3, _ = _gravity_rollout(m, mass[100:103], x[sl], v[sl], 3, N, steps)
     check_rel("C5 batch independence", preds3.cpu(), preds[:, sl].cpu(), 1e-6)
+
+
+@pytest.mark.parametrize("B, N, T", [(512, 20, 10), (256, 100, 6), (3, 5, 4)])
+def test_segno_substep_fusion_is_bitwise_unfused(monkeypatch, B, N, T):
+    """Substep fusion of the SEGNO layer (one whole-graph chunk per workgroup: the node update of step
+    t builds step t+1's projection tables and positions in LDS; with room, h and v stay in LDS too) is
+    a change of where values live, not of arithmetic: fused + kept (C3), fused only (C5: the kept
+    rows do not fit the LDS), and the unfused path (NONODE_NO_FUSE, read per launch) agree bitwise."""
+    m = _segno(seed=61)
+    g = torch.Generator().manual_seed(62)
+    x = torch.randn(B * N, 3, generator=g).to(DEV)
+    v = torch.randn(B * N, 3, generator=g).to(DEV)
+    q = torch.randn(B * N, 1, generator=g).sign().to(DEV)
+    ei = pkg.harness.get_edges(B, N, DEV)
+    ea = torch.cat([q[ei[0]] * q[ei[1]], ((x[ei[0]] - x[ei[1]]) ** 2).sum(1, keepdim=True)], 1)
+    his = v.norm(dim=1, keepdim=True)
+
+    def run():
+        with torch.no_grad():
+            out = m(his, x, ei, v, ea, T=T)
+        torch.cuda.synchronize()
+        return [t.clone() for t in out[:2]]
+
+    ref = None
+    for env in ({}, {"NONODE_NO_KEEP": "1"}, {"NONODE_NO_FUSE": "1"}):
+        for k in ("NONODE_NO_KEEP", "NONODE_NO_FUSE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, val in env.items():
+            monkeypatch.setenv(k, val)
+        out = run()
+        assert all(torch.isfinite(t).all() for t in out)
+        if ref is None:
+            ref = out
+        else:
+            for a, b in zip(ref, out):
+                assert torch.equal(a, b), env
