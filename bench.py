@@ -560,7 +560,10 @@ def run_egno_train(args, world, rank, dev, backend):
         res["roofline"] = {"kernel": "edge_bwd_kernel (pass 0 + pass 1, one layer)", "bound": "mfma", "achieved": ach,
                            "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
-                           "traffic": None, "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0)), float(np.mean(e1))],
+                           "traffic": _sum_or_none(pmc_traffic("edge_bwd_kernel<pass 0>"),
+                                                   pmc_traffic("edge_bwd_kernel<pass 1>")),
+                           "traffic_basis": "HBM bytes of pass 0 + pass 1 (profiles/pmc_traffic.json)",
+                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0)), float(np.mean(e1))],
                            "algorithmic_gflop_per_launch": flop / 1e9,
                            "algorithmic_basis": "reverse of W2 and Wc1 per edge (data + weight gradients); "
                                                 "the forward recompute is not counted",
@@ -770,6 +773,10 @@ def run_sim_charged(args, world, rank, dev, backend):
         res["parity"] = {"first_frames_maxabs_vs_oracle": float(np.abs(got[:k] - L_ref[:k]).max()),
                          "frames_checked": k}
     return res
+
+
+def _sum_or_none(*xs):
+    return None if any(x is None for x in xs) else float(sum(xs))
 
 
 def pmc_traffic(kernel):

@@ -22,7 +22,10 @@ def kernel_key(name):
         return f"egnn_layer_kernel<{variant}>"
     if "tconv_kernel" in name:
         return "tconv_kernel<first>" if ("<true>" in name or "<true," in name or "ILb1E" in name) else "tconv_kernel"
-    for k in ("temb_kernel", "embed_kernel"):
+    if "edge_bwd_kernel" in name:   # edge_bwd_kernel<NE, PASS>
+        m = re.search(r"edge_bwd_kernel<\d+,\s*(\d+)>", name) or re.search(r"edge_bwd_kernelILi\d+ELi(\d+)E", name)
+        return f"edge_bwd_kernel<pass {m.group(1)}>" if m else "edge_bwd_kernel"
+    for k in ("temb_kernel", "embed_kernel", "node_bwd_kernel", "node_post_kernel"):
         if k in name:
             return k
     return None
