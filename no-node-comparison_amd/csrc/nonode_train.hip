@@ -45,10 +45,11 @@ enum : int {
 };
 enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
 constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2, [SC_*] option flags
-// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the four 64x64 edge matrices: the edge
-// backward's forward recompute (W2, Wc1) and its transposed products (W2^T, Wc1^T) run fp16x3
+// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the 64x64 edge matrices: the edge backward's
+// forward recompute (W2, Wc1), its transposed products (W2^T, Wc1^T) and its chunk tables
+// P = W_A h + b1, Q = W_B h run fp16x3
 constexpr int BOFF_H16 = BOFF_SCAL + 64;
-enum : int { BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_COUNT };
+enum : int { BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_WA, BH_WB, BH_COUNT };
 constexpr int BBLOB_FLOATS = BOFF_H16 + BH_COUNT * 4096;
 
 // frag of W^T: value W^T[row][col] = W[col][row0 + row] (W row stride ld)
@@ -83,6 +84,8 @@ __global__ void pack_bwd_kernel(PackArgs a) {
     case 17: pack_h16_shifted(H + BH_WC1 * 8192, B + BOFF_SCAL, BH_WC1, a.cw1, d); break;
     case 18: pack_h16_t_shifted(H + BH_W2T * 8192, B + BOFF_SCAL, BH_W2T, a.w2, d); break;
     case 19: pack_h16_t_shifted(H + BH_WC1T * 8192, B + BOFF_SCAL, BH_WC1T, a.cw1, d); break;
+    case 20: pack_h16_shifted(H + BH_WA * 8192, B + BOFF_SCAL, BH_WA, a.w1, d, a.ld1, a.colA); break;
+    case 21: pack_h16_shifted(H + BH_WB * 8192, B + BOFF_SCAL, BH_WB, a.w1, d, a.ld1, a.colB); break;
     case 0: if (d < 4096) pack_frag(B + BOFF_WA, a.w1, a.ld1, a.colA, 4, d, 1.f); break;
     case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
     case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
@@ -128,7 +131,7 @@ __global__ void pack_bwd_kernel(PackArgs a) {
         else if (i == 1 && a.vb2) val = a.vb2[0];
         else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
         else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
-        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-19
+        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-21
       }
       break;
   }
@@ -438,6 +441,11 @@ struct EdgeBwdArgs {
   const float* gF; const float* gM;
   float* GA; float* GB; float* GX;                                    // per node (GB, GX atomically)
   float* wpart;                                                       // [grid * 4][EW_STRIDE]
+  // pass A -> pass B handoff of gz2 = dL/dz2 and the coordinate-MLP output c per edge: the unit
+  // (tile at row rt of block b, sender offset k) owns the 16-row block (k - 1)(n + 16 G) + rt + 16 b
+  // (16 x 64 floats of stash, channel-block-major so each store instruction writes 1 KB contiguous;
+  // 16 floats of stash_c). The 16 b shift keeps a block's partial last tile off the next block's rows.
+  float* stash; float* stash_c;
 };
 
 // PASS 1 sums GA (per receiver), GB (per sender) and GX in WAVE-PRIVATE LDS tables by plain
@@ -445,14 +453,15 @@ struct EdgeBwdArgs {
 // units run in order), and the four tables are added at the end of the chunk: LDS float atomics
 // (ds_add_f32, 38 per unit) had cost more than the whole rest of the pass.
 constexpr int EB_VSTAGE = BOFF_SCAL + 64 - BOFF_FEAT;   // feature k-steps + vectors + scalars
-constexpr int EB_HSTAGE = 2 * 4096;   // + EB_VSTAGE in PASS 0 (PASS 1 at ct = 1 has no room)
+// staged fp16 hi/lo fragments: pass A W2, Wc1, Wc1^T (+ EB_VSTAGE), pass B W2^T
+constexpr int EB_HSTAGE_A = 3 * 4096, EB_HSTAGE_B = 4096;
 size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
   const int s_max = ((16 * ct - 1) / N + 2) * N;
   if (s_max_out) *s_max_out = s_max;
   // sP, sGM [ct*16][ROWP]; sQ [s_max][ROWP]; sX [s_max][4]; sGF [ct*16][4]; 4 x tile;
   // PASS 1: 4 x (sGA [ct*16][ROWP], sGB [s_max][ROWP], sGX [s_max][4])
-  // + two 64x64 fp16 hi/lo fragment sets staged once (EB_HSTAGE floats)
-  return EB_HSTAGE + (pass ? 0 : EB_VSTAGE) + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
+  // + the fp16 hi/lo fragment sets staged once
+  return (pass ? EB_HSTAGE_B : EB_HSTAGE_A + EB_VSTAGE) + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
          4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (size_t)s_max * (ROWP + 4)) : 0);
 }
 
@@ -570,8 +579,9 @@ __device__ __forceinline__ float edge_sum16(float v) {
 }
 
 // Two launches per layer (register budget: one wave cannot hold both 64x64 accumulators next to the
-// per-edge working set): PASS 0 recomputes the edge up to gz3 and accumulates dWc1, dbc1, dwc2,
-// dbc2; PASS 1 does the whole reverse pass with dW2, db2, the W1 scalar columns and GA / GB / GX.
+// per-edge working set). PASS 0 (pass A) recomputes the edge forward, accumulates dWc1, dbc1, dwc2,
+// dbc2 and hands gz2 = dL/dz2 and c to pass B through HBM (stash); PASS 1 (pass B) recomputes only
+// z1 and does the rest of the reverse: dW2, db2, W2^T, the W1 scalar columns and GA / GB / GX.
 // OPT: 1 = EGNO norm=True (radial input normalised, basic.py:140-141), 2 = SEGNO tanh=True (coordinate
 // output through tanh, gcl.py:57-59); each its own copy of the body (no per-edge select by default)
 template <int NE, int PASS, int OPT>
@@ -585,7 +595,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   const int rows = p.ct * 16;
   // LDS-staged fragments: PASS 0 the forward W2, Wc1 (used twice per unit there), PASS 1 W2^T, Wc1^T
   float* sH = smem;
-  float* sP = smem + EB_HSTAGE + (PASS ? 0 : EB_VSTAGE);
+  float* sP = smem + (PASS ? EB_HSTAGE_B : EB_HSTAGE_A + EB_VSTAGE);
   float* sGM = sP + rows * ROWP;
   float* sQ = sGM + rows * ROWP;
   float* sX = sQ + p.s_max * ROWP;
@@ -602,17 +612,21 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   const float* wW2 = bb + BOFF_W2;
   const float* wWc1 = bb + BOFF_WC1;
   {
+    // pass A: W2 | Wc1 (adjacent in the blob) and Wc1^T; pass B: W2^T
     const f4* src = reinterpret_cast<const f4*>(bb + BOFF_H16 + (PASS == 0 ? BH_W2 : BH_W2T) * 4096);
-    for (int i = tid; i < 2 * 1024; i += NW * 64) reinterpret_cast<f4*>(sH)[i] = src[i];
-    const f4* vsrc = reinterpret_cast<const f4*>(bb + BOFF_FEAT);
-    if (PASS == 0)
-      for (int i = tid; i < EB_VSTAGE / 4; i += NW * 64) reinterpret_cast<f4*>(sH + 8192)[i] = vsrc[i];
+    for (int i = tid; i < (PASS == 0 ? 2 : 1) * 1024; i += NW * 64) reinterpret_cast<f4*>(sH)[i] = src[i];
+    if (PASS == 0) {
+      const f4* srcT = reinterpret_cast<const f4*>(bb + BOFF_H16 + BH_WC1T * 4096);
+      for (int i = tid; i < 1024; i += NW * 64) reinterpret_cast<f4*>(sH + 8192)[i] = srcT[i];
+      const f4* vsrc = reinterpret_cast<const f4*>(bb + BOFF_FEAT);
+      for (int i = tid; i < EB_VSTAGE / 4; i += NW * 64) reinterpret_cast<f4*>(sH + EB_HSTAGE_A)[i] = vsrc[i];
+    }
   }
-  const float* sV = PASS == 0 ? sH + 8192 : bb + BOFF_FEAT;   // bb + BOFF_FEAT .. BOFF_SCAL + 64
+  const float* sV = PASS == 0 ? sH + EB_HSTAGE_A : bb + BOFF_FEAT;   // bb + BOFF_FEAT .. BOFF_SCAL + 64
   const h8* hW2 = PASS == 0 ? reinterpret_cast<const h8*>(sH) : reinterpret_cast<const h8*>(bb + BOFF_H16 + BH_W2 * 4096);
   const h8* hWc1 = PASS == 0 ? reinterpret_cast<const h8*>(sH + 4096) : reinterpret_cast<const h8*>(bb + BOFF_H16 + BH_WC1 * 4096);
   const h8* hW2T = reinterpret_cast<const h8*>(sH);
-  const h8* hWc1T = reinterpret_cast<const h8*>(sH + 4096);
+  const h8* hWc1T = reinterpret_cast<const h8*>(sH + 8192);   // pass A only
   float scW = 0x1p112f;   // running scale of the accW / sB sums (wgrad_h16)
   f4 accW[4][4];   // PASS 0: dWc1, PASS 1: dW2
 #pragma unroll
@@ -663,7 +677,15 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       load_ecl(hin, p.h + (size_t)node * HID, g);
       if (isP) load_vp(acc, bb + BOFF_VEC + BV_B1 * 64, g);
       else zero4(acc);
-      mfma_dense<4>(acc, bb + (isP ? BOFF_WA : BOFF_WB), hin, lane);
+      // fp16x3 as in the forward's projections (exact f32 MFMAs beyond the fp16 range)
+      if (__builtin_expect(__any(amax_ecl(hin) > H16_LIMIT), 0)) {
+        mfma_dense<4>(acc, bb + (isP ? BOFF_WA : BOFF_WB), hin, lane);
+      } else {
+        h8 xh[2], xl[2];
+        h16_split(hin, xh, xl);
+        mfma_h16(acc, reinterpret_cast<const h8*>(bb + BOFF_H16 + (isP ? BH_WA : BH_WB) * 4096), xh, xl, lane,
+                 h16_us(bb + BOFF_SCAL, isP ? BH_WA : BH_WB));
+      }
       // rows of receivers past the range are zero: their lanes' a, m feed the weight-gradient
       // MFMAs (multiplied by zero gradients, so they must be finite)
       if (isP && !valid) zero4(acc);
@@ -739,91 +761,122 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           for (int mo = 0; mo < 4; ++mo) z1[mo] = mfma(wf[mo], ev[kf], z1[mo]);
         }
       }
-      // a = SiLU(z1); z2 = W2 a + b2; m = SiLU(z2); z3 = Wc1 m + bc1; c1 = SiLU(z3) (fp16x3 on the
-      // matrix cores, exact f32 MFMAs for a unit whose activations leave the fp16 range)
-      // (a = z1 sg1 is not kept: recomputed for the dW2 gradient, which saves 16 registers)
-      f4 sg1[4], z2[4], sg2[4], z3[4], sg3[4];
+      // this unit's handoff block: 16 edges x 64 channels, contiguous (stash_at)
+      const size_t sunit = (size_t)(k - 1) * ((size_t)p.n_graphs * N + 16 * gridDim.x) + rbase + 16 * tau + 16 * blockIdx.x;
+      f4 sg1[4], gz2[4];
       bool bigA;
-      {
+      float c;
+      if constexpr (PASS == 0) {
+        // a = SiLU(z1); z2 = W2 a + b2; m = SiLU(z2); z3 = Wc1 m + bc1; c1 = SiLU(z3) (fp16x3 on the
+        // matrix cores, exact f32 MFMAs for a unit whose activations leave the fp16 range)
+        f4 z2[4], sg2[4], z3[4], sg3[4];
+        {
+          f4 a[4];
+          STAMP(13);   // pass A sections: 13 head, 2 forward W2 / Wc1 / c, 15 gz3 + dWc1, 3 Wc1^T, 4 handoff
+          silu_keep(z1, sg1, a);
+          bigA = __any(amax_ecl(a) > H16_LIMIT);
+          load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
+          if (__builtin_expect(bigA, 0)) {
+            mfma_dense<4>(z2, wW2, a, lane);
+          } else {
+            h8 xh[2], xl[2];
+            h16_split(a, xh, xl);
+#if NONODE_BWD_PIN
+            mfma_h16f(z2, fw2, xh, xl, h16_us(bb + BOFF_SCAL, BH_W2));
+#else
+            mfma_h16(z2, hW2, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_W2));
+#endif
+          }
+        }
+        // (m = z2 sg2 and c1 = z3 sg3 are recomputed where needed again: register budget)
+        bool bigM;
+        {
+          f4 m[4];
+          silu_keep(z2, sg2, m);
+          bigM = __any(amax_ecl(m) > H16_LIMIT);
+          load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
+          if (__builtin_expect(bigM, 0)) {
+            mfma_dense<4>(z3, wWc1, m, lane);
+          } else {
+            h8 xh[2], xl[2];
+            h16_split(m, xh, xl);
+#if NONODE_BWD_PIN
+            mfma_h16f(z3, fwc1, xh, xl, h16_us(bb + BOFF_SCAL, BH_WC1));
+#else
+            mfma_h16(z3, hWc1, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_WC1));
+#endif
+          }
+        }
+        {
+          f4 c1[4];
+          silu_keep(z3, sg3, c1);
+          c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
+          if constexpr (ctanh) c = tanhf(c);
+        }
+        STAMP(2);
+        // reverse: f = r c (SEGNO: clamp(r c, +-100) per edge)
+        float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
+        if (p.segno) {
+          gF0 = fabsf(r0 * c) <= 100.f ? gF0 : 0.f;
+          gF1 = fabsf(r1 * c) <= 100.f ? gF1 : 0.f;
+          gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
+        }
+        float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
+        if constexpr (ctanh) gc *= 1.f - c * c;   // through the tanh: gc is the gradient of the MLP output
+        // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
+        f4 gz3[4];
+        load_vp(gz3, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) gz3[mt] *= gc;
+        mul_dsilu_s(gz3, z3, sg3);
+        // dWc1 += gz3 (x) m ; dwc2 += gc c1 ; dbc1 += gz3 ; dbc2 += gc
+        {
+          f4 m[4];
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt] * sg2[mt];
+          wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
+        sGC += gc;
+        STAMP(15);
+        // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m); gz2 = gm SiLU'(z2) -> pass B
+        load_ecl(gz2, sGM + rl * ROWP, g);
+        if (!rvalid) zero4(gz2);
+        mm64_cs(gz2, hWc1T, gz3, lane, h16_us(bb + BOFF_SCAL, BH_WC1T));
+        mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
+        STAMP(3);
+        // (rows past the range too: their slots lie inside this unit's block)
+        {
+          float* sb16 = p.stash + sunit * HID;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) *reinterpret_cast<f4*>(sb16 + mt * 256 + e * 16 + 4 * g) = gz2[mt];
+          if (g == 0) p.stash_c[sunit + e] = c;
+        }
+        STAMP(4);
+        continue;
+      } else {
         f4 a[4];
-        STAMP(PASS ? 0 : 13);
+        STAMP(0);
         silu_keep(z1, sg1, a);
         bigA = __any(amax_ecl(a) > H16_LIMIT);
-        load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
-        if (__builtin_expect(bigA, 0)) {
-          mfma_dense<4>(z2, wW2, a, lane);
-        } else {
-          h8 xh[2], xl[2];
-          h16_split(a, xh, xl);
-#if NONODE_BWD_PIN
-          if (PASS == 0) mfma_h16f(z2, fw2, xh, xl, h16_us(bb + BOFF_SCAL, BH_W2)); else
-#endif
-          mfma_h16(z2, hW2, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_W2));
+        // pass A's gz2 and c of this edge (zero gradient for receivers past the range)
+        c = p.stash_c[sunit + e];
+        {
+          const float* sb16 = p.stash + sunit * HID;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) gz2[mt] = *reinterpret_cast<const f4*>(sb16 + mt * 256 + e * 16 + 4 * g);
         }
+        if (!rvalid) zero4(gz2);
       }
-      // (m = z2 sg2 and c1 = z3 sg3 are recomputed where needed again: register budget)
-      bool bigM;
-      {
-        f4 m[4];
-        STAMP(PASS ? 1 : 13);
-        silu_keep(z2, sg2, m);
-        bigM = __any(amax_ecl(m) > H16_LIMIT);
-        load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
-        if (__builtin_expect(bigM, 0)) {
-          mfma_dense<4>(z3, wWc1, m, lane);
-        } else {
-          h8 xh[2], xl[2];
-          h16_split(m, xh, xl);
-#if NONODE_BWD_PIN
-          if (PASS == 0) mfma_h16f(z3, fwc1, xh, xl, h16_us(bb + BOFF_SCAL, BH_WC1)); else
-#endif
-          mfma_h16(z3, hWc1, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_WC1));
-        }
-      }
-      float c;
-      {
-        f4 c1[4];
-        STAMP(PASS ? 2 : 13);
-        silu_keep(z3, sg3, c1);
-        c = dot_vp(c1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g) + bc2;
-        if constexpr (ctanh) c = tanhf(c);
-      }
-      // reverse: f = r c (SEGNO: clamp(r c, +-100) per edge)
+      STAMP(1);
       float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
       if (p.segno) {
         gF0 = fabsf(r0 * c) <= 100.f ? gF0 : 0.f;
         gF1 = fabsf(r1 * c) <= 100.f ? gF1 : 0.f;
         gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
       }
-      float gc = rvalid ? (gF0 * r0 + gF1 * r1 + gF2 * r2) : 0.f;
-      if constexpr (ctanh) gc *= 1.f - c * c;   // through the tanh: gc is the gradient of the MLP output
       float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
-      // c = wc2 . c1 + bc2 ; c1 = SiLU(z3)
-      f4 gz3[4];
-      load_vp(gz3, sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64, g);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) gz3[mt] *= gc;
-      mul_dsilu_s(gz3, z3, sg3);
-      // dWc1 += gz3 (x) m ; dwc2 += gc c1 ; dbc1 += gz3 ; dbc2 += gc
-      if (PASS == 0) {
-        f4 m[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt] * sg2[mt];
-        wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
-        sGC += gc;
-        STAMP(15);
-        continue;
-      }
-      STAMP(3);
-      // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m)
-      f4 gz2[4];
-      load_ecl(gz2, sGM + rl * ROWP, g);
-      if (!rvalid) zero4(gz2);
-      mm64_cs(gz2, hWc1T, gz3, lane, h16_us(bb + BOFF_SCAL, BH_WC1T));
-      STAMP(4);
-      mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
       // dW2 += gz2 (x) a ; db2 += gz2
       {
         f4 a[4];
@@ -1624,6 +1677,7 @@ struct BwdWs {
   float *gF, *gM, *ghp, *GA, *GB, *GX, *gxe, *gve, *ghe;
   float *op_gt, *op_t, *op_gphi, *op_z, *op_gz;
   float *wpart;
+  float *stash, *stash_c;                // edge backward pass A -> pass B ((N - 1) n rows)
   float *twf, *twb, *tpart, *xpart;
   float *partial;
   size_t floats;
@@ -1640,6 +1694,8 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.GX = take(n * 4); w.gxe = take(n * 3); w.gve = take(n * 3); w.ghe = take(n * 64);
   w.op_gt = take(n * 64); w.op_t = take(n * 64); w.op_gphi = take(n); w.op_z = take(n * 64); w.op_gz = take(n * 64);
   w.wpart = take((size_t)EB_MAX_BLOCKS * EW_STRIDE);
+  const size_t npad = n + 16 * EB_MAX_BLOCKS;   // (N - 1) x (n + 16 G) handoff rows, G <= EB_MAX_BLOCKS
+  w.stash = take(npad * (N - 1) * 64); w.stash_c = take(npad * (N - 1));
   w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take(BN * 3 * 2 * 2 * MMAX_T * 2);
@@ -1682,7 +1738,7 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   a.ne = n_edge_feat;
   a.flags = flags;
   a.blob = bblob;
-  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 20), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 22), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_bwd_kernel");
 }
 
@@ -1831,6 +1887,7 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, const Gemm& gemm, hipS
     ea.segno = 0;
     ea.h = r.he; ea.x = r.xe; ea.ef = ne ? r.edge_fea : r.bb; ea.bb = r.bb; ea.gF = w.gF; ea.gM = w.gM;
     ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
+    ea.stash = w.stash; ea.stash_c = w.stash_c;
     if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
     // edge-level weight gradients: fixed-order sums of the G block partials (launched with the
     // node-level GEMMs' reductions below)
@@ -2206,6 +2263,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
       ea.h = hs; ea.x = st.xs + t * n * 3; ea.ef = ne ? edge_attr : bblob; ea.bb = bblob; ea.gF = w.gF;
       ea.gM = w.gM; ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
+      ea.stash = w.stash; ea.stash_c = w.stash_c;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
       auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int col0) {
         const int NO = M_ * (N_ + 1);

@@ -11,10 +11,11 @@ import bench  # noqa: E402
 import no_node_comparison_amd as pkg  # noqa: E402
 from no_node_comparison_amd import _lib  # noqa: E402
 
-NAMES = {0: "P1 head (z1)", 1: "P1 silu + W2", 2: "P1 silu + Wc1", 3: "P1 c, gF, gz3", 4: "P1 Wc1^T",
-         5: "P1 dW2 wgrad", 6: "P1 W2^T", 7: "P1 feat wgrad + GA/GB/GX", 8: "P1 phase A", 9: "P1 barrier A",
-         10: "P1 barrier B", 11: "P1 phase C", 12: "P1 phase D", 13: "P0 head..Wc1", 14: "P0 phase A + barriers",
-         15: "P0 gz3 + dWc1 wgrad"}
+NAMES = {0: "B head (z1)", 1: "B silu + handoff loads", 5: "B dW2 wgrad", 6: "B W2^T",
+         7: "B feat wgrad + GA/GB/GX", 8: "B phase A", 9: "B barrier A", 10: "B barrier B", 11: "B phase C",
+         12: "B phase D", 13: "A head (z1)", 2: "A silu/W2/silu/Wc1/c", 15: "A gz3 + dWc1 wgrad", 3: "A Wc1^T",
+         4: "A handoff stores", 14: "A phase A + barriers"}
+PASS_B, PASS_A = (0, 1, 5, 6, 7, 8, 9, 10, 11, 12), (13, 2, 15, 3, 4, 14)
 dev = torch.device("cuda:0")
 torch.manual_seed(0)
 model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
@@ -37,9 +38,9 @@ for it in range(reps + 1):
     if it:
         acc = [a + b for a, b in zip(acc, buf)]
 waves = 256 * 4 * 4 * reps    # blocks x waves x layers x reps
-for lo, hi, tag in ((0, 13, "PASS 1"), (13, 16, "PASS 0")):
-    tot = sum(acc[lo:hi])
+for idx, tag in ((PASS_B, "pass B (PASS 1)"), (PASS_A, "pass A (PASS 0)")):
+    tot = sum(acc[i] for i in idx)
     print(f"{tag}: {tot / waves:.0f} cycles per wave per launch")
-    for i in range(lo, hi):
+    for i in idx:
         if acc[i]:
             print(f"  {i:2d} {NAMES[i]:28s} {acc[i] / waves:10.0f}  {acc[i] / max(tot, 1):6.1%}")
