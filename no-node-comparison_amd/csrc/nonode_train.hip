@@ -225,8 +225,9 @@ __device__ __forceinline__ float row_max16(float m) {
 }
 // out += W x for a gradient column set x: each column scaled to [2^11, 2^12) before the split, the
 // product scaled back (per lane: lane (e, g) holds column e)
-__device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane, unsigned us) {
-  const float sc = p2scale(col_max(amax_ecl(x)));
+__device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane, unsigned us,
+                                        float cm) {
+  const float sc = p2scale(cm);
   const float inv = 1.f / sc;   // exact (power of two)
   f4 xs[4], acc[4];
 #pragma unroll
@@ -473,9 +474,24 @@ size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
 // units of 1/sc: sc is a wave-uniform running power-of-two scale for G, lowered (and acc, bsum
 // rescaled, exactly) when a unit's G is larger than any before it, so G sc stays below 2^12.
 // exact: A beyond the fp16 range (a diverged rollout) -> the f32 MFMA form for this unit.
+// max |x| over a lane's 16 values as a tree (v_max3), not a 16-long dependent chain
+__device__ __forceinline__ float amax16(const f4 (&x)[4]) {
+  float m[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+    m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
+  return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
+}
+// cm: col_max(amax16(G)), shared with the transposed product of the same G (mm64_cs)
 __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], float& sc, const f4 (&G)[4],
-                                          const f4 (&A)[4], float* tile, int g, int e, bool exact) {
-  const float m = row_max16(col_max(amax_ecl(G)));
+                                          const f4 (&A)[4], float* tile, int g, int e, bool exact, float cm) {
+  // G goes to the transpose tile unscaled, so the wave-wide max / scale below runs beside the LDS
+  // round trip instead of before it; the scale is applied to the transposed values
+  float* tG = tile;
+  float* tA = tile + 16 * ROWT;
+  store_ecl(tG + e * ROWT, G, g);
+  store_ecl(tA + e * ROWT, A, g);
+  const float m = row_max16(cm);
   const float mu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m)));
   if (mu > 0.f) {
     const float su = p2scale(mu);
@@ -490,13 +506,6 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
       sc = su;
     }
   }
-  float* tG = tile;
-  float* tA = tile + 16 * ROWT;
-  f4 Gs[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) Gs[mt] = G[mt] * sc;
-  store_ecl(tG + e * ROWT, Gs, g);
-  store_ecl(tA + e * ROWT, A, g);
   __builtin_amdgcn_wave_barrier();
   if (__builtin_expect(exact, 0)) {
 #pragma unroll
@@ -504,7 +513,7 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
       const int row = (4 * g + ks) * ROWT + e;
       float gv[4], av[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { gv[t] = tG[row + 16 * t]; av[t] = tA[row + 16 * t]; bsum[t] += gv[t]; }
+      for (int t = 0; t < 4; ++t) { gv[t] = tG[row + 16 * t] * sc; av[t] = tA[row + 16 * t]; bsum[t] += gv[t]; }
 #pragma unroll
       for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
@@ -526,7 +535,7 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
   for (int ot = 0; ot < 4; ++ot) {
     f4 v;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) v[ks] = tG[(4 * g + ks) * ROWT + e + 16 * ot];
+    for (int ks = 0; ks < 4; ++ks) v[ks] = tG[(4 * g + ks) * ROWT + e + 16 * ot] * sc;
     bsum[ot] += (v[0] + v[1]) + (v[2] + v[3]);
     h4 gh, gl;
     h4_split(v, gh, gl);
@@ -587,6 +596,8 @@ __device__ __forceinline__ float edge_sum16(float v) {
 template <int NE, int PASS, int OPT>
 __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   constexpr bool rnorm = OPT == 1, ctanh = OPT == 2;
+  // OPT 0: EGNO, OPT 3: SEGNO (compile-time: no per-edge branch); the option variants read p.segno
+  const bool segno = OPT == 0 ? false : (OPT == 3 ? true : p.segno != 0);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NW = 4;
   constexpr int NF = 1 + NE;   // scalar inputs of edge W1: |r|^2, e_0 .. e_{NE-1}
@@ -714,10 +725,70 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       pin_agpr(fwc1);
     }
 #endif
+    f4 gaR[4];   // pass B: GA of the current tile's receivers (lane e), and the receiver-side GX
+    zero4(gaR);
+    float gxR0 = 0.f, gxR1 = 0.f, gxR2 = 0.f;
+    int cur_tau = -1;
+    auto flush_ga = [&](int t) {   // into the wave-private tables (distinct receivers: no race)
+      const int rl_ = 16 * t + e;
+      f4 v[4];
+      load_ecl(v, myGA + rl_ * ROWP, g);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) v[mt] += gaR[mt];
+      store_ecl(myGA + rl_ * ROWP, v, g);
+      const int rr = rbase + rl_;
+      if (g == 0 && rr < nend) {
+        f4* xr = reinterpret_cast<f4*>(myGX + (rr - s0) * 4);
+        *xr += f4{gxR0, gxR1, gxR2, 0.f};
+      }
+      zero4(gaR);
+      gxR0 = gxR1 = gxR2 = 0.f;
+    };
+    // the wave's next unit's edge features and (pass B) handoff block are requested one unit ahead,
+    // so their global-memory latency overlaps this unit's work
+    auto unit_src = [&](int uu, const float*& efp_o, size_t& sunit_o) {
+      const int tau_ = uu / Nm1, k_ = uu - tau_ * Nm1 + 1;
+      const int r_ = rbase + 16 * tau_ + e;
+      const int rc_ = r_ < nend ? r_ : nend - 1;
+      const int gr_ = rc_ / N, n_ = rc_ - gr_ * N;
+      int j_ = n_ + k_;
+      j_ = (j_ >= N) ? j_ - N : j_;
+      const int jj_ = (j_ < n_) ? j_ : j_ - 1;
+      efp_o = p.ef + (((size_t)(gr_ % p.ef_mod) * N + n_) * Nm1 + jj_) * NE;
+      sunit_o = (size_t)(k_ - 1) * ((size_t)p.n_graphs * N + 16 * gridDim.x) + rbase + 16 * tau_ + 16 * blockIdx.x;
+    };
+    float efn[NE > 0 ? NE : 1];
+    f4 gzn[4];
+    float cn = 0.f;
+    auto prefetch = [&](int uu) {
+      const float* ep;
+      size_t su;
+      unit_src(uu, ep, su);
+#pragma unroll
+      for (int kk = 0; kk < NE; ++kk) efn[kk] = ep[kk];
+      if constexpr (PASS == 1) {
+        const float* sb16 = p.stash + su * HID;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) gzn[mt] = *reinterpret_cast<const f4*>(sb16 + mt * 256 + e * 16 + 4 * g);
+        cn = p.stash_c[su + e];
+      }
+    };
+    if (U > 0) prefetch(wave < U ? wave : U - 1);
     for (int u = wave; u < U; u += NW) {
       // the weight fragments are loop-invariant: without this barrier the compiler hoists all four
       // 64x64 matrices (256 VGPRs) out of the loop and spills
       asm volatile("" ::: "memory");
+      float fe_in[NE > 0 ? NE : 1];
+#pragma unroll
+      for (int kk = 0; kk < NE; ++kk) fe_in[kk] = efn[kk];
+      f4 gz_in[4];
+      float c_in = 0.f;
+      if constexpr (PASS == 1) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) gz_in[mt] = gzn[mt];
+        c_in = cn;
+      }
+      prefetch(u + NW < U ? u + NW : u);
       const int tau = u / Nm1, k = u - tau * Nm1 + 1;
       const int rl = 16 * tau + e;
       const int r = rbase + rl;
@@ -733,12 +804,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       const float r1 = sX[rls * 4 + 1] - sX[sl * 4 + 1];
       const float r2 = sX[rls * 4 + 2] - sX[sl * 4 + 2];
       const float s2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
-      const float* efp = p.ef + (((size_t)(gr % p.ef_mod) * N + n) * Nm1 + jj) * NE;
       float fe[NF];
       fe[0] = s2;
       if constexpr (rnorm) fe[0] = radial_norm(s2);
 #pragma unroll
-      for (int kk = 0; kk < NE; ++kk) fe[1 + kk] = efp[kk];
+      for (int kk = 0; kk < NE; ++kk) fe[1 + kk] = fe_in[kk];
       float ev[2];
 #pragma unroll
       for (int kf = 0; kf < 2; ++kf) {
@@ -816,7 +886,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         STAMP(2);
         // reverse: f = r c (SEGNO: clamp(r c, +-100) per edge)
         float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
-        if (p.segno) {
+        if (segno) {
           gF0 = fabsf(r0 * c) <= 100.f ? gF0 : 0.f;
           gF1 = fabsf(r1 * c) <= 100.f ? gF1 : 0.f;
           gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
@@ -830,11 +900,12 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         for (int mt = 0; mt < 4; ++mt) gz3[mt] *= gc;
         mul_dsilu_s(gz3, z3, sg3);
         // dWc1 += gz3 (x) m ; dwc2 += gc c1 ; dbc1 += gz3 ; dbc2 += gc
+        const float cm3 = col_max(amax16(gz3));
         {
           f4 m[4];
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt] * sg2[mt];
-          wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM);
+          wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM, cm3);
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
@@ -843,7 +914,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m); gz2 = gm SiLU'(z2) -> pass B
         load_ecl(gz2, sGM + rl * ROWP, g);
         if (!rvalid) zero4(gz2);
-        mm64_cs(gz2, hWc1T, gz3, lane, h16_us(bb + BOFF_SCAL, BH_WC1T));
+        mm64_cs(gz2, hWc1T, gz3, lane, h16_us(bb + BOFF_SCAL, BH_WC1T), cm3);
         mul_dsilu_s(gz2, z2, sg2);                 // m = SiLU(z2)
         STAMP(3);
         // (rows past the range too: their slots lie inside this unit's block)
@@ -861,33 +932,31 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         silu_keep(z1, sg1, a);
         bigA = __any(amax_ecl(a) > H16_LIMIT);
         // pass A's gz2 and c of this edge (zero gradient for receivers past the range)
-        c = p.stash_c[sunit + e];
-        {
-          const float* sb16 = p.stash + sunit * HID;
+        c = c_in;
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) gz2[mt] = *reinterpret_cast<const f4*>(sb16 + mt * 256 + e * 16 + 4 * g);
-        }
+        for (int mt = 0; mt < 4; ++mt) gz2[mt] = gz_in[mt];
         if (!rvalid) zero4(gz2);
       }
       STAMP(1);
       float gF0 = sGF[rl * 4 + 0], gF1 = sGF[rl * 4 + 1], gF2 = sGF[rl * 4 + 2];
-      if (p.segno) {
+      if (segno) {
         gF0 = fabsf(r0 * c) <= 100.f ? gF0 : 0.f;
         gF1 = fabsf(r1 * c) <= 100.f ? gF1 : 0.f;
         gF2 = fabsf(r2 * c) <= 100.f ? gF2 : 0.f;
       }
       float gr0 = c * gF0, gr1 = c * gF1, gr2 = c * gF2;
       // dW2 += gz2 (x) a ; db2 += gz2
+      const float cm2 = col_max(amax16(gz2));
       {
         f4 a[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
-        wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA);
+        wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA, cm2);
       }
       STAMP(5);
       f4 gz1[4];
       zero4(gz1);
-      mm64_cs(gz1, hW2T, gz2, lane, h16_us(bb + BOFF_SCAL, BH_W2T));
+      mm64_cs(gz1, hW2T, gz2, lane, h16_us(bb + BOFF_SCAL, BH_W2T), cm2);
       STAMP(6);
       mul_dsilu_s(gz1, z1, sg1);                 // a = SiLU(z1)
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
@@ -898,30 +967,32 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       gr0 = fmaf(2.f * gs, r0, gr0);
       gr1 = fmaf(2.f * gs, r1, gr1);
       gr2 = fmaf(2.f * gs, r2, gr2);
+      // GA and the receiver side of GX stay in registers while the wave's units keep the same tile
+      // (a lane's receiver is fixed within a tile; lanes of rows past the range add zeros: their gz2
+      // and gF are zero); the sender sums go to the wave-private tables per unit
+      if (tau != cur_tau) {   // wave-uniform
+        if (cur_tau >= 0) flush_ga(cur_tau);
+        cur_tau = tau;
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) gaR[mt] += gz1[mt];
+      gxR0 += gr0;
+      gxR1 += gr1;
+      gxR2 += gr2;
       if (rvalid) {
-        // per-receiver / per-sender sums of gz1 (the W_A h_i and W_B h_j inputs) and x terms
-        {
-          f4 t[4];
-          load_ecl(t, myGA + rl * ROWP, g);
+        f4 t[4];
+        load_ecl(t, myGB + sl * ROWP, g);
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
-          store_ecl(myGA + rl * ROWP, t, g);
-          load_ecl(t, myGB + sl * ROWP, g);
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
-          store_ecl(myGB + sl * ROWP, t, g);
-        }
+        for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
+        store_ecl(myGB + sl * ROWP, t, g);
         if (g == 0) {
-          // receiver rows first, then sender rows (a receiver of one lane can be the sender of another)
-          f4* xr = reinterpret_cast<f4*>(myGX + rls * 4);
-          *xr += f4{gr0, gr1, gr2, 0.f};
-          __builtin_amdgcn_wave_barrier();
           f4* xs = reinterpret_cast<f4*>(myGX + sl * 4);
           *xs -= f4{gr0, gr1, gr2, 0.f};
         }
       }
       STAMP(7);
     }
+    if (PASS == 1 && cur_tau >= 0) flush_ga(cur_tau);
     STAMP(PASS ? 7 : 15);
     __syncthreads();
     STAMP(PASS ? 10 : 14);
@@ -998,6 +1069,7 @@ template <int NE, int PASS>
 __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
   if (p.bb[BOFF_SCAL + SC_NORM] != 0.f) edge_bwd_body<NE, PASS, 1>(p);        // wave-uniform
   else if (p.bb[BOFF_SCAL + SC_TANH] != 0.f) edge_bwd_body<NE, PASS, 2>(p);
+  else if (p.segno) edge_bwd_body<NE, PASS, 3>(p);
   else edge_bwd_body<NE, PASS, 0>(p);
 }
 // per-pass chunk size (tiles per LDS chunk) and dynamic LDS bytes

@@ -155,6 +155,27 @@ __global__ __launch_bounds__(512) void kf16(float* out, int iters, unsigned long
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
   if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
 }
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+// fp16 MFMA 16x16x16 (the K = 16 form the edge backward's weight gradients use), 4 accumulators
+__global__ __launch_bounds__(512) void kf16k16(float* out, int iters, unsigned long long* clk) {
+  const int lane = threadIdx.x & 63;
+  h4 a, b;
+  for (int j = 0; j < 4; ++j) { a[j] = (_Float16)(lane * 1e-3f + j); b[j] = (_Float16)(1.0f - j * 0.01f); }
+  f4 acc[4];
+  for (int m = 0; m < 4; ++m) acc[m] = f4{0, 0, 0, 0};
+  unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+#pragma unroll
+      for (int mo = 0; mo < 4; ++mo) acc[mo] = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, acc[mo], 0, 0, 0);
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  float s = 0;
+  for (int m = 0; m < 4; ++m) s += acc[m][0] + acc[m][1] + acc[m][2] + acc[m][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }
+}
 // SiLU VALU work alone (same count as the MODE 1/2 variants) to price it
 __global__ __launch_bounds__(512) void ksilu(float* out, int iters, unsigned long long* clk) {
   const int lane = threadIdx.x & 63;
@@ -217,6 +238,7 @@ int main() {
     run("f16 16x16x32 x64", kf16<0>, wpb, blocks, iters, 64.0 * 16384);
     run("f16 16x16x32 x64 + 16 silu", kf16<1>, wpb, blocks, iters, 64.0 * 16384);
     run("16 silu alone (flop=f16 eq)", ksilu, wpb, blocks, iters, 64.0 * 16384);
+    run("f16 16x16x16 x64", kf16k16, wpb, blocks, iters, 64.0 * 8192);
   }
   return 0;
 }
