@@ -551,8 +551,8 @@ def run_egno_train(args, world, rank, dev, backend):
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0, loss=float(loss.detach()))
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
-    if e0 and e1:
-        avg = float(np.mean(e0) + np.mean(e1))
+    if e0:   # e1 is empty when the merged single-launch edge backward runs (NONODE_EBWD_MERGED=1)
+        avg = float(np.mean(e0) + (np.mean(e1) if e1 else 0.0))
         E = T * B * N * (N - 1)
         flop = 2.0 * E * MAC_PER_EDGE_BWD
         ach = flop / (avg * 1e-3) / 1e12
@@ -563,7 +563,7 @@ def run_egno_train(args, world, rank, dev, backend):
                            "traffic": _sum_or_none(pmc_traffic("edge_bwd_kernel<pass 0>"),
                                                    pmc_traffic("edge_bwd_kernel<pass 1>")),
                            "traffic_basis": "HBM bytes of pass 0 + pass 1 (profiles/pmc_traffic.json)",
-                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0)), float(np.mean(e1))],
+                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0))] + ([float(np.mean(e1))] if e1 else []),
                            "algorithmic_gflop_per_launch": flop / 1e9,
                            "algorithmic_basis": "reverse of W2 and Wc1 per edge (data + weight gradients); "
                                                 "the forward recompute is not counted",

@@ -447,6 +447,9 @@ struct EdgeBwdArgs {
   // (16 x 64 floats of stash, channel-block-major so each store instruction writes 1 KB contiguous;
   // 16 floats of stash_c). The 16 b shift keeps a block's partial last tile off the next block's rows.
   float* stash; float* stash_c;
+  // per node: P = W_A h + b1 and Q = W_B h, written by pass A for its chunks' receiver rows (each node
+  // is a receiver of exactly one chunk) and copied into pass B's tables (no second projection)
+  float* Pn; float* Qn;
 };
 
 // PASS 1 sums GA (per receiver), GB (per sender) and GX in WAVE-PRIVATE LDS tables by plain
@@ -462,7 +465,7 @@ size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
   // sP, sGM [ct*16][ROWP]; sQ [s_max][ROWP]; sX [s_max][4]; sGF [ct*16][4]; 4 x tile;
   // PASS 1: 4 x (sGA [ct*16][ROWP], sGB [s_max][ROWP], sGX [s_max][4])
   // + the fp16 hi/lo fragment sets staged once
-  return (pass ? EB_HSTAGE_B : EB_HSTAGE_A + EB_VSTAGE) + (size_t)ct * 16 * ROWP * 2 + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
+  return (pass ? EB_HSTAGE_B : EB_HSTAGE_A + EB_VSTAGE) + (size_t)ct * 16 * ROWP * (pass ? 1 : 2) + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
          4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (size_t)s_max * (ROWP + 4)) : 0);
 }
 
@@ -607,8 +610,8 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   // LDS-staged fragments: PASS 0 the forward W2, Wc1 (used twice per unit there), PASS 1 W2^T, Wc1^T
   float* sH = smem;
   float* sP = smem + (PASS ? EB_HSTAGE_B : EB_HSTAGE_A + EB_VSTAGE);
-  float* sGM = sP + rows * ROWP;
-  float* sQ = sGM + rows * ROWP;
+  float* sGM = sP + rows * ROWP;   // pass A only
+  float* sQ = PASS ? sGM : sGM + rows * ROWP;
   float* sX = sQ + p.s_max * ROWP;
   float* sGF = sX + p.s_max * 4;
   float* tile = sGF + rows * 4 + wave * EB_TSTRIDE;
@@ -678,7 +681,20 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       const int rr = rbase + i / 4;
       sGF[i] = rr < nend ? p.gF[(size_t)rr * 4 + (i & 3)] : 0.f;
     }
-    for (int job = wave; job < ctc + nsT; job += NW) {
+    if (PASS == 1) {
+      // pass A's node projections: P of the receiver rows (zero past the range), Q of the senders
+      for (int i = tid; i < ctc * 16 * 16; i += NW * 64) {
+        const int rl = i >> 4, c4 = i & 15;
+        const int rr = rbase + rl;
+        const f4 v = rr < nend ? reinterpret_cast<const f4*>(p.Pn + (size_t)rr * HID)[c4] : f4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f4*>(sP + rl * ROWP + 4 * c4) = v;
+      }
+      for (int i = tid; i < S * 16; i += NW * 64) {
+        const int sl = i >> 4, c4 = i & 15;
+        *reinterpret_cast<f4*>(sQ + sl * ROWP + 4 * c4) = reinterpret_cast<const f4*>(p.Qn + (size_t)(s0 + sl) * HID)[c4];
+      }
+    }
+    for (int job = wave; job < (PASS == 0 ? ctc + nsT : 0); job += NW) {
       const bool isP = job < ctc;
       const int local = (isP ? job : job - ctc) * 16 + e;
       int node = isP ? rbase + local : s0 + local;
@@ -702,6 +718,9 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       if (isP && !valid) zero4(acc);
       if (valid || isP) {
         store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
+        // each node is a receiver of exactly one chunk: it writes that node's P and Q for pass B
+        const bool mine = isP ? valid : (node >= rbase && node < rbase + ctc * 16 && node < nend);
+        if (mine) store_ecl((isP ? p.Pn : p.Qn) + (size_t)node * HID, acc, g);
         if (isP) {
           f4 gm[4];
           load_ecl(gm, p.gM + (size_t)node * HID, g);
@@ -1750,6 +1769,7 @@ struct BwdWs {
   float *op_gt, *op_t, *op_gphi, *op_z, *op_gz;
   float *wpart;
   float *stash, *stash_c;                // edge backward pass A -> pass B ((N - 1) n rows)
+  float *Pn, *Qn;                        // edge backward pass A -> pass B: node projections (n rows)
   float *twf, *twb, *tpart, *xpart;
   float *partial;
   size_t floats;
@@ -1768,6 +1788,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.wpart = take((size_t)EB_MAX_BLOCKS * EW_STRIDE);
   const size_t npad = n + 16 * EB_MAX_BLOCKS;   // (N - 1) x (n + 16 G) handoff rows, G <= EB_MAX_BLOCKS
   w.stash = take(npad * (N - 1) * 64); w.stash_c = take(npad * (N - 1));
+  w.Pn = take(n * 64); w.Qn = take(n * 64);
   w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take(BN * 3 * 2 * 2 * MMAX_T * 2);
@@ -1959,7 +1980,7 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, const Gemm& gemm, hipS
     ea.segno = 0;
     ea.h = r.he; ea.x = r.xe; ea.ef = ne ? r.edge_fea : r.bb; ea.bb = r.bb; ea.gF = w.gF; ea.gM = w.gM;
     ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
-    ea.stash = w.stash; ea.stash_c = w.stash_c;
+    ea.stash = w.stash; ea.stash_c = w.stash_c; ea.Pn = w.Pn; ea.Qn = w.Qn;
     if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
     // edge-level weight gradients: fixed-order sums of the G block partials (launched with the
     // node-level GEMMs' reductions below)
@@ -2335,7 +2356,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
       ea.h = hs; ea.x = st.xs + t * n * 3; ea.ef = ne ? edge_attr : bblob; ea.bb = bblob; ea.gF = w.gF;
       ea.gM = w.gM; ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
-      ea.stash = w.stash; ea.stash_c = w.stash_c;
+      ea.stash = w.stash; ea.stash_c = w.stash_c; ea.Pn = w.Pn; ea.Qn = w.Qn;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
       auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int col0) {
         const int NO = M_ * (N_ + 1);
