@@ -1348,9 +1348,7 @@ __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
       }
 }
 
-// dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
-// strided partial lanes, combined in a fixed order (deterministic).
-// the TimeConv_x weight gradient from rows_reduce's per-slice sums [nb][io][MMAX_T][2]: one block adds
+// the TimeConv_x weight gradient from tconvx_bwd_kernel's per-block sums [nb][io][MMAX_T][2]: one block adds
 // the slices in order and writes g_tconvx [2][2][Mfull][2] whole (modes >= M zero), replacing a
 // memset and four copies
 __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int nb, int M, int Mfull, float* dst) {
@@ -1372,20 +1370,31 @@ __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int
   }
 }
 
+// dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
+// strided partial lanes, combined in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst) {
   __shared__ float red[4][64];
   const int per = M * 2 * 4096;
   const int ol = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + ol;
-  float s = 0.f;
-  if (d < per)
-    for (int b = pl; b < nblk; b += 4) s += part[(size_t)b * per + d];
+  // four independent sums per thread keep several partial rows in flight (one dependent chain of
+  // nblk / 4 loads had left this HBM pass latency-bound: 16.7 us for 16.8 MB at C4)
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (d < per) {
+#pragma unroll 4
+    for (int b = pl; b < nblk; b += 16) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (b + 4 * j < nblk) s4[j] += part[(size_t)(b + 4 * j) * per + d];
+    }
+  }
+  const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   red[pl][ol] = s;
   __syncthreads();
   if (pl != 0 || d >= per) return;
-  s = ((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol];
+  const float tot = ((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol];
   const int mc = d >> 12, r = d & 4095, m = mc >> 1, c = mc & 1, i = r >> 6, o = r & 63;
-  dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = s;
+  dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = tot;
 }
 
 int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
@@ -1401,52 +1410,80 @@ int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
 
 // TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. One thread per (c, d).
 // Writes gx, gv and per-thread weight-gradient terms part[(c*3+d)][i][o][m][2].
-__global__ void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x, const float* v, const float* lm,
-                                  const float* gxo, const float* gvo, const float* w, float* gx, float* gv,
-                                  float* part, int frames) {
+// One thread per (column c, coordinate d); the block sums its threads' weight-gradient terms in a
+// fixed order and writes one row of 2*2*MMAX_T*2 partials (tconvx_grad_finish adds the blocks' rows).
+constexpr int TX_THREADS = 128;
+__global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x,
+                                                                const float* v, const float* lm, const float* gxo,
+                                                                const float* gvo, const float* w, float* gx,
+                                                                float* gv, float* part, int frames) {
+  constexpr int CNT = 2 * 2 * MMAX_T * 2;
+  // twiddles cos / sin(pi 2 m t / T) once per block in LDS (the same float values a per-thread double
+  // cospi / sinpi gave; that software double trig per thread had made this kernel ~38 us at C4)
+  __shared__ float sCs[MMAX_T * TMAX], sSn[MMAX_T * TMAX];
+  __shared__ float red[TX_THREADS][CNT + 1];
+  for (int i = threadIdx.x; i < M * T; i += blockDim.x) {
+    const int m = i / T, t = i - m * T;
+    const double ang = 2.0 * (double)m * (double)t / (double)T;
+    sCs[m * TMAX + t] = (float)cospi(ang);
+    sSn[m * TMAX + t] = (float)sinpi(ang);
+  }
+  __syncthreads();
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= BN * 3) return;
-  const int c = idx / 3, d = idx - 3 * c;
-  float X[2][TMAX], G[2][TMAX], GO[2][TMAX];
-  for (int t = 0; t < T; ++t) {
-    const size_t row = (size_t)t * BN + c;
-    X[0][t] = x[row * 3 + d] - lm[(frames ? row : (size_t)c) * 3 + d];
-    X[1][t] = v[row * 3 + d];
-    GO[0][t] = G[0][t] = gxo[row * 3 + d];
-    GO[1][t] = G[1][t] = gvo[row * 3 + d];
-  }
-  float* pp = part + (size_t)idx * (2 * 2 * MMAX_T * 2);
-  for (int k = 0; k < 2 * 2 * MMAX_T * 2; ++k) pp[k] = 0.f;
-  for (int m = 0; m < M; ++m) {
-    const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
-    float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f}, gYr[2] = {0.f, 0.f}, gYi[2] = {0.f, 0.f};
+  const bool valid = idx < BN * 3;
+  const int c = valid ? idx / 3 : 0, d = valid ? idx - 3 * (idx / 3) : 0;
+  float pp[CNT];
+#pragma unroll
+  for (int k = 0; k < CNT; ++k) pp[k] = 0.f;
+  if (valid) {
+    float X[2][TMAX], G[2][TMAX], GO[2][TMAX];
     for (int t = 0; t < T; ++t) {
-      const double ang = 2.0 * (double)m * (double)t / (double)T;
-      const float cs = (float)cospi(ang), sn = (float)sinpi(ang);
+      const size_t row = (size_t)t * BN + c;
+      X[0][t] = x[row * 3 + d] - lm[(frames ? row : (size_t)c) * 3 + d];
+      X[1][t] = v[row * 3 + d];
+      GO[0][t] = G[0][t] = gxo[row * 3 + d];
+      GO[1][t] = G[1][t] = gvo[row * 3 + d];
+    }
+#pragma unroll
+    for (int m = 0; m < MMAX_T; ++m) {
+      if (m >= M) break;
+      const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
+      float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f}, gYr[2] = {0.f, 0.f}, gYi[2] = {0.f, 0.f};
+      for (int t = 0; t < T; ++t) {
+        const float cs = sCs[m * TMAX + t], sn = sSn[m * TMAX + t];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          Xr[i] = fmaf(X[i][t], cs, Xr[i]); Xi[i] = fmaf(-X[i][t], sn, Xi[i]);
+          gYr[i] = fmaf(cm * cs, GO[i][t], gYr[i]); gYi[i] = fmaf(-cm * sn, GO[i][t], gYi[i]);
+        }
+      }
+#pragma unroll
       for (int i = 0; i < 2; ++i) {
-        Xr[i] = fmaf(X[i][t], cs, Xr[i]); Xi[i] = fmaf(-X[i][t], sn, Xi[i]);
-        gYr[i] = fmaf(cm * cs, GO[i][t], gYr[i]); gYi[i] = fmaf(-cm * sn, GO[i][t], gYi[i]);
+        float gxr = 0.f, gxi = 0.f;
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const float wr = w[((i * 2 + o) * Mfull + m) * 2 + 0], wi = w[((i * 2 + o) * Mfull + m) * 2 + 1];
+          gxr += gYr[o] * wr + gYi[o] * wi;
+          gxi += -gYr[o] * wi + gYi[o] * wr;
+          pp[((i * 2 + o) * MMAX_T + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
+          pp[((i * 2 + o) * MMAX_T + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
+        }
+        for (int t = 0; t < T; ++t) G[i][t] += gxr * sCs[m * TMAX + t] - gxi * sSn[m * TMAX + t];
       }
     }
-    for (int i = 0; i < 2; ++i) {
-      float gxr = 0.f, gxi = 0.f;
-      for (int o = 0; o < 2; ++o) {
-        const float wr = w[((i * 2 + o) * Mfull + m) * 2 + 0], wi = w[((i * 2 + o) * Mfull + m) * 2 + 1];
-        gxr += gYr[o] * wr + gYi[o] * wi;
-        gxi += -gYr[o] * wi + gYi[o] * wr;
-        pp[((i * 2 + o) * MMAX_T + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
-        pp[((i * 2 + o) * MMAX_T + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
-      }
-      for (int t = 0; t < T; ++t) {
-        const double ang = 2.0 * (double)m * (double)t / (double)T;
-        G[i][t] += gxr * (float)cospi(ang) - gxi * (float)sinpi(ang);
-      }
+    for (int t = 0; t < T; ++t) {
+      const size_t row = (size_t)t * BN + c;
+      gx[row * 3 + d] = G[0][t];
+      gv[row * 3 + d] = G[1][t];
     }
   }
-  for (int t = 0; t < T; ++t) {
-    const size_t row = (size_t)t * BN + c;
-    gx[row * 3 + d] = G[0][t];
-    gv[row * 3 + d] = G[1][t];
+#pragma unroll
+  for (int k = 0; k < CNT; ++k) red[threadIdx.x][k] = pp[k];
+  __syncthreads();
+  if (threadIdx.x < CNT) {
+    float acc = 0.f;
+    for (int r = 0; r < TX_THREADS; ++r) acc += red[r][threadIdx.x];
+    part[(size_t)blockIdx.x * CNT + threadIdx.x] = acc;
   }
 }
 
@@ -1652,26 +1689,6 @@ int launch_reduce_batch(const ReduceJob* jobs, int count, hipStream_t s) {
   }
   hipLaunchKernelGGL(gemm_reduce_batch, dim3(gx, count), dim3(256), 0, s, a);
   return check_launch("gemm_reduce_batch");
-}
-
-// out[blk][o] = sum over this block's row slice of part[rows][cnt] (cnt <= 32): 256 threads =
-// 32 values x 8 strided row lanes, combined in a fixed order; a second launch with one block
-// sums the block partials (deterministic)
-__global__ __launch_bounds__(256) void rows_reduce(const float* part, long long rows, int cnt, long long slice,
-                                                   float* out) {
-  __shared__ float red[8][33];
-  const int o = threadIdx.x & 31, lanei = threadIdx.x >> 5;
-  const long long r0 = (long long)blockIdx.x * slice, r1 = min(rows, r0 + slice);
-  float s = 0.f;
-  if (o < cnt)
-    for (long long r = r0 + lanei; r < r1; r += 8) s += part[r * cnt + o];
-  red[lanei][o] = s;
-  __syncthreads();
-  if (lanei == 0 && o < cnt) {
-    s = 0.f;
-    for (int q = 0; q < 8; ++q) s += red[q][o];
-    out[(size_t)blockIdx.x * cnt + o] = s;
-  }
 }
 
 struct Gemm {
@@ -2029,20 +2046,13 @@ struct TconvRev {
 };
 int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   const int BN = r.BN, T = r.T, M = r.M, modes = r.modes;
-  hipLaunchKernelGGL(tconvx_bwd_kernel, dim3((BN * 3 + 127) / 128), dim3(128), 0, s, BN, T, M, modes, r.xs, r.vs,
+  // g_txw [2][2][Mfull][2]: one partial row per tconvx block, added in block order (modes >= M zero)
+  const int nbx = (BN * 3 + TX_THREADS - 1) / TX_THREADS;
+  hipLaunchKernelGGL(tconvx_bwd_kernel, dim3(nbx), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
                      r.lm, r.gx, r.gv, r.txw, r.g_xin, r.g_vin, w.xpart, r.frames);
   if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
-  {
-    // g_txw [2][2][Mfull][2]: reduce the per-(c, d) terms (modes >= M zero)
-    float* tmp = w.partial;
-    const int cnt = 2 * 2 * MMAX_T * 2;
-    const long long rows = (long long)BN * 3, slice = 256;
-    const int nb = (int)((rows + slice - 1) / slice);
-    hipLaunchKernelGGL(rows_reduce, dim3(nb), dim3(256), 0, s, w.xpart, rows, cnt, slice, tmp + 64);
-    if (int rc = check_launch("rows_reduce")) return rc;
-    hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, tmp + 64, nb, M, modes, r.g_txw);
-    if (int rc = check_launch("tconvx_grad_finish")) return rc;
-  }
+  hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, w.xpart, nbx, M, modes, r.g_txw);
+  if (int rc = check_launch("tconvx_grad_finish")) return rc;
   hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, r.tw, modes, M, w.twb);
   if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
   TconvBwdArgs ta;
