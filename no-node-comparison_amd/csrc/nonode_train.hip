@@ -1355,9 +1355,12 @@ __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int
   __shared__ float red[8][33];
   constexpr int cnt = 2 * 2 * MMAX_T * 2;
   const int o = threadIdx.x & 31, lanei = threadIdx.x >> 5;
-  float s = 0.f;
-  for (int r = lanei; r < nb; r += 8) s += part[(size_t)r * cnt + o];
-  red[lanei][o] = s;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};   // independent sums: several partial rows in flight
+  for (int r = lanei; r < nb; r += 32)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (r + 8 * j < nb) s4[j] += part[(size_t)(r + 8 * j) * cnt + o];
+  red[lanei][o] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   __syncthreads();
   for (int d = threadIdx.x; d < 4 * Mfull * 2; d += 256) {
     const int io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
@@ -1373,26 +1376,23 @@ __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int
 // dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
 // strided partial lanes, combined in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst) {
-  __shared__ float red[4][64];
+  // 16 outputs x 16 partial lanes per block, one float4 of 4 consecutive outputs per load (1 KB per
+  // wave and partial row instead of 256 B; the scalar form ran at ~0.9 TB/s)
+  __shared__ f4 red[16][17];
   const int per = M * 2 * 4096;
-  const int ol = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  const int d = blockIdx.x * 64 + ol;
-  // four independent sums per thread keep several partial rows in flight (one dependent chain of
-  // nblk / 4 loads had left this HBM pass latency-bound: 16.7 us for 16.8 MB at C4)
-  float s4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (d < per) {
-#pragma unroll 4
-    for (int b = pl; b < nblk; b += 16) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (b + 4 * j < nblk) s4[j] += part[(size_t)(b + 4 * j) * per + d];
-    }
-  }
-  const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  const int ol = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int d4 = blockIdx.x * 16 + ol;   // float4 index
+  f4 s = f4{0.f, 0.f, 0.f, 0.f};
+  if (4 * d4 < per)
+    for (int b = pl; b < nblk; b += 16) s += reinterpret_cast<const f4*>(part + (size_t)b * per)[d4];
   red[pl][ol] = s;
   __syncthreads();
-  if (pl != 0 || d >= per) return;
-  const float tot = ((red[0][ol] + red[1][ol]) + red[2][ol]) + red[3][ol];
+  if (threadIdx.x >= 64) return;
+  const int oq = threadIdx.x >> 2, c4 = threadIdx.x & 3;   // output float4 oq, component c4
+  const int d = 4 * (blockIdx.x * 16 + oq) + c4;
+  if (d >= per) return;
+  float tot = 0.f;
+  for (int q = 0; q < 16; ++q) tot += red[q][oq][c4];
   const int mc = d >> 12, r = d & 4095, m = mc >> 1, c = mc & 1, i = r >> 6, o = r & 63;
   dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = tot;
 }
@@ -2064,7 +2064,7 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   TG = ta.ntiles < TG ? ta.ntiles : TG;
   if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
   if (modes > M) hipMemsetAsync(r.g_tw, 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
-  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 + 63) / 64), dim3(256), 0, s, w.tpart, TG, M, modes,
+  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 / 4 + 15) / 16), dim3(256), 0, s, w.tpart, TG, M, modes,
                      r.g_tw);
   return check_launch("tconv_wgrad_reduce");
 }
