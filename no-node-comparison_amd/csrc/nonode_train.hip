@@ -417,12 +417,12 @@ int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s) {
 // gemm_reduce adds the partials in a fixed order (deterministic). No per-edge operand ever goes to
 // HBM (the unfused version wrote 6 x 64 floats per edge, 3 GB per layer at C2).
 //
-// Weight-gradient MFMA: v_mfma_f32_16x16x4_f32 with K = edges. The ECL holds edges along
-// lane & 15, so a unit's [16 edges][64] operands go through a per-wave LDS tile ([edge][ROWT]) and
-// come back with channels along lane & 15: k-step ks, lane (e', g) reads edge 4g + ks, channel
-// 16t + e' (row stride 84 floats puts the four lane groups on disjoint banks). Columns 64..79 of
-// the first operand's rows carry the edge's scalar inputs [|r|^2, e_0, ..] (zero past NF), the B
-// operand of the W1 scalar-column gradient.
+// Weight-gradient MFMA (wgrad_h16): fp16x3 v_mfma_f32_16x16x16_f16 with K = the unit's 16 edges. The
+// ECL holds edges along lane & 15, so a unit's [16 edges][64] operands go through a per-wave LDS tile
+// ([edge][ROWT]) and come back with channels along lane & 15: lane (e', g) reads edges 4g .. 4g + 3,
+// channel 16t + e' (row stride 68 floats: the two 32-lane halves of a ds_read_b32 and the 8-lane
+// groups of a ds_write_b128 hit distinct banks). The W1 scalar-input columns' gradient is summed per
+// lane on the VALU (accFe) and across the lane group's edges once at the end.
 //
 // Per-wave partial (floats), blocks in gemm_reduce's [M][N+1] layout (column N = bias):
 constexpr int EW_W2 = 0;                  // dW2  [64][65], column 64 = db2
@@ -431,7 +431,7 @@ constexpr int EW_WC2 = 2 * 64 * 65;       // dwc2 [1][65],  column 64 = dbc2
 constexpr int EW_FEAT = EW_WC2 + 68;      // dW1 scalar-input columns [64][NF + 1] (NF = 1 + ne <= 5)
 constexpr int EW_STRIDE = EW_FEAT + 64 * 6;
 constexpr int EB_MAX_BLOCKS = 256;        // edge_bwd grid cap: EB_MAX_BLOCKS * 4 wave partials
-constexpr int ROWT = 84;                  // transpose-tile row stride (floats)
+constexpr int ROWT = 68;                  // transpose-tile row stride (floats)
 constexpr int EB_TSTRIDE = 2 * 16 * ROWT; // per-wave transpose tile (two [16][ROWT] operands)
 
 struct EdgeBwdArgs {
@@ -552,30 +552,6 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
   __builtin_amdgcn_wave_barrier();
 }
 
-// acc[ot] += sum over the unit's edges of G[e][16 ot + .] (x) fe[e][.]: lane (e, g) of acc[ot][q]
-// holds dW1[16 ot + 4 g + q][scalar column e] (e < NF)
-template <int NF>
-__device__ __forceinline__ void wgrad_feat(f4 (&acc)[4], const f4 (&G)[4], const float (&fe)[NF], float* tile, int g,
-                                           int e) {
-  store_ecl(tile + e * ROWT, G, g);
-  if (g == 0) {
-#pragma unroll
-    for (int k = 0; k < NF; ++k) tile[e * ROWT + 64 + k] = fe[k];
-  }
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int row = (4 * g + ks) * ROWT + e;
-    float gv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) gv[t] = tile[row + 16 * t];
-    const float fv = tile[row + 64];
-#pragma unroll
-    for (int ot = 0; ot < 4; ++ot) acc[ot] = mfma(gv[ot], fv, acc[ot]);
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
 // dst[o] = sum of the block's four wave partials (LDS, EW_STRIDE apart) for o in [o0, o1)
 __device__ __forceinline__ void block_partial(const float* red, float* dst, int o0, int o1) {
   __syncthreads();
@@ -647,12 +623,15 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) accW[a][b] = f4{0.f, 0.f, 0.f, 0.f};
-  f4 accFe[4], sWC2[4];
-  zero4(accFe); zero4(sWC2);
+  // pass B: dW1 scalar-input columns per lane, sum over the lane's edges of fe[f] gz1 (the 16 edges
+  // of a lane group are added once at the end): NF x 16 FMAs per unit on the VALU instead of a
+  // transpose through LDS and 16 f32 MFMAs
+  f4 accFe[NF][4], sWC2[4];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) zero4(accFe[f]);
+  zero4(sWC2);
   float sB[4] = {0.f, 0.f, 0.f, 0.f};   // PASS 0: dbc1, PASS 1: db2
   float sGC = 0.f;
-  // scalar-input columns 64..79 of the tile rows: zero once (columns past NF stay zero)
-  for (int i = lane; i < 16 * 16; i += 64) tile[(i >> 4) * ROWT + 64 + (i & 15)] = 0.f;
   const int G = gridDim.x;
   const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;
   const int nend = (int)(((long long)(blockIdx.x + 1) * p.n_graphs) / G) * N;
@@ -979,7 +958,10 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       STAMP(6);
       mul_dsilu_s(gz1, z1, sg1);                 // a = SiLU(z1)
       // scalar-input columns of W1: dW1[:, f] += gz1 (x) fe[f]
-      wgrad_feat<NF>(accFe, gz1, fe, tile, g, e);
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) accFe[f][mt] += fe[f] * gz1[mt];
       // s = |r|^2 input column
       float gs = dot_vp(gz1, sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64, g);
       if constexpr (rnorm) gs = s2 < 1e-12f ? gs * 1e12f : 0.f;   // d normalize(s) / ds: 1 / eps below eps, else 0
@@ -1058,13 +1040,19 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   put(accW, sB, scW, PASS == 0 ? EW_WC1 : EW_W2);
   if (PASS == 1) {
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
+    for (int f = 0; f < NF; ++f)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ch = 16 * ot + 4 * g + q;
-        if (e < NF) wp[EW_FEAT + ch * (NF + 1) + e] = accFe[ot][q];
-        if (e == NF) wp[EW_FEAT + ch * (NF + 1) + NF] = 0.f;
-      }
+      for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = edge_sum16(accFe[f][ot][q]);
+          if (e == 0) wp[EW_FEAT + (16 * ot + 4 * g + q) * (NF + 1) + f] = v;
+        }
+    if (e == 0)
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wp[EW_FEAT + (16 * ot + 4 * g + q) * (NF + 1) + NF] = 0.f;
   }
   if (PASS == 0) {
 #pragma unroll
