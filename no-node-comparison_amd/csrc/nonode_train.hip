@@ -838,15 +838,18 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         // a = SiLU(z1); z2 = W2 a + b2; m = SiLU(z2); z3 = Wc1 m + bc1; c1 = SiLU(z3) (fp16x3 on the
         // matrix cores, exact f32 MFMAs for a unit whose activations leave the fp16 range)
         f4 z2[4], sg2[4], z3[4], sg3[4];
+        bool bigM;
         {
-          f4 a[4];
+          // fp16x3 unconditionally, so silu -> W2 -> silu -> Wc1 is one basic block for the scheduler;
+          // a unit whose activations leave the fp16 range is recomputed afterwards with exact f32
+          // MFMAs (both products; its dWc1 term then takes the exact form too)
           STAMP(13);   // pass A sections: 13 head, 2 forward W2 / Wc1 / c, 15 gz3 + dWc1, 3 Wc1^T, 4 handoff
-          silu_keep(z1, sg1, a);
-          bigA = __any(amax_ecl(a) > H16_LIMIT);
-          load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
-          if (__builtin_expect(bigA, 0)) {
-            mfma_dense<4>(z2, wW2, a, lane);
-          } else {
+          float ma, mm;
+          {
+            f4 a[4];
+            silu_keep(z1, sg1, a);
+            ma = amax16(a);
+            load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
             h8 xh[2], xl[2];
             h16_split(a, xh, xl);
 #if NONODE_BWD_PIN
@@ -855,17 +858,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
             mfma_h16(z2, hW2, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_W2));
 #endif
           }
-        }
-        // (m = z2 sg2 and c1 = z3 sg3 are recomputed where needed again: register budget)
-        bool bigM;
-        {
-          f4 m[4];
-          silu_keep(z2, sg2, m);
-          bigM = __any(amax_ecl(m) > H16_LIMIT);
-          load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
-          if (__builtin_expect(bigM, 0)) {
-            mfma_dense<4>(z3, wWc1, m, lane);
-          } else {
+          {
+            f4 m[4];
+            silu_keep(z2, sg2, m);
+            mm = amax16(m);
+            load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
             h8 xh[2], xl[2];
             h16_split(m, xh, xl);
 #if NONODE_BWD_PIN
@@ -873,6 +870,19 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
 #else
             mfma_h16(z3, hWc1, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_WC1));
 #endif
+          }
+          bigA = __any(ma > H16_LIMIT);
+          bigM = __any(mm > H16_LIMIT);
+          if (__builtin_expect(bigA || bigM, 0)) {
+            f4 a[4], m[4];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
+            load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
+            mfma_dense<4>(z2, wW2, a, lane);
+            silu_keep(z2, sg2, m);
+            load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
+            mfma_dense<4>(z3, wWc1, m, lane);
+            bigM = true;
           }
         }
         {
