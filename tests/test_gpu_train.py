@@ -77,7 +77,8 @@ def test_egno_train_forward_equals_inference_forward():
         check_rel("a.detach()", a.detach().cpu(), b.cpu(), 1e-6)
 
 
-@pytest.mark.parametrize("B,N,T", [(2, 5, 10), (3, 9, 4), (1, 20, 10)])
+# (2, 31, 4): the largest N whose per-chunk sender tables fit pass B's LDS
+@pytest.mark.parametrize("B,N,T", [(2, 5, 10), (3, 9, 4), (1, 20, 10), (1, 26, 4), (2, 31, 4)])
 def test_egno_gradients_match_oracle(B, N, T):
     c = _egno_case(B, N, T, seed=B * 100 + N)
     m = _egno(T=T, seed=N)
@@ -95,6 +96,17 @@ def test_egno_gradients_match_oracle(B, N, T):
             assert np.abs(g[k]).max() == 0, k
         else:
             check_rel(f"grad {k}", g[k], ref, GTOL_F64)
+
+
+def test_egno_training_rejects_n_beyond_the_edge_backward_tables():
+    """N = 40 needs more LDS for the edge backward's sender tables than a CU has: the backward
+    raises the library's error instead of running a kernel that does not fit."""
+    B, N, T = 1, 40, 2
+    c = _egno_case(B, N, T, seed=3)
+    m = _egno(T=T, seed=3)
+    inp = {k: _dev(v) for k, v in c.items()}
+    with pytest.raises(pkg.NonodeError, match="too large"):
+        _train_step_grads(m, inp, _dev(np.zeros((B, N, T, 3), np.float32)), T, B, N)
 
 
 def test_egno_adam_step_runs_and_repacks():
