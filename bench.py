@@ -617,6 +617,126 @@ def run_egno_train(args, world, rank, dev, backend):
     return res
 
 
+def run_segno_train(args, world, rank, dev, backend):
+    """Row †g: SEGNO training step at the C3 configuration (charged N=20, B=512 per GPU, 10 substeps
+    of forward_step): forward with saved state, nn.MSELoss of the positions after T substeps
+    (train_nbody.py:150-178), backward through the HIP integrator's reverse pass, ONE all-reduce of
+    the flat gradient buffer, Adam. Synthetic target: x + 0.3 v (tests/test_gpu_train_segno.py)."""
+    import no_node_comparison_amd as pkg
+    from no_node_comparison_amd import _lib
+    from no_node_comparison_amd.sharding import FlatGrads, max_over_ranks
+    N, T = 20, 10
+    plan = batch_plan(args, world, rank, 512)
+    B = plan["B"]
+    torch.manual_seed(0)
+    model = pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=64, n_layers=4, recurrent=True, device=dev).train()
+    p0 = _cpu_params(model)
+    loc, vel, q = synthetic_charged(plan["B_global"], N, 4321)
+    loc, vel, q = (t[plan["lo"]:plan["hi"]].to(dev) for t in (loc, vel, q))
+    edges = pkg.harness.get_edges(B, N, dev)
+    x = loc.reshape(-1, 3)
+    v = vel.reshape(-1, 3)
+    qq = q.reshape(-1, 1)
+    ea = torch.cat([qq[edges[0]] * qq[edges[1]], ((x[edges[0]] - x[edges[1]]) ** 2).sum(-1, keepdim=True)], 1)
+    his = v.norm(dim=-1, keepdim=True)
+    target = x + 0.3 * v
+    fg = FlatGrads(model.parameters())
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    w = B * world / plan["B_global"]   # shard-size weight: the all-reduce averages shard means
+
+    def step():
+        opt.zero_grad()
+        xo = model(his, x, edges, v, ea, T=T)[0]
+        loss = torch.nn.functional.mse_loss(xo, target) * w
+        loss.backward()
+        fg.allreduce_()
+        opt.step()
+        return loss
+
+    grads0 = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        opt.zero_grad()
+        (torch.nn.functional.mse_loss(model(his, x, edges, v, ea, T=T)[0], target) * w).backward()
+        fg.gather_()
+        grads0 = {k: _cpu(t.grad) for k, t in model.named_parameters() if t.grad is not None}
+    _prewarm(step, args, dev)
+    for _ in range(args.warmup):
+        step()
+    barrier_sync(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier_sync(world, dev)
+    el = max_over_ranks(time.perf_counter() - t0, dev)
+    records = []
+    if args.kernel_events:
+        _lib.profile_begin(64 * args.steps * T + 64)
+        for _ in range(args.steps):
+            step()
+        records = _lib.profile_end()
+    value = plan["B_global"] * args.steps / el
+    res = _result(args, world, plan, el / args.steps * 1e3, value,
+                  f"SEGNO training step (forward_step of {T} substeps + MSE + HIP reverse pass + 1 all-reduce + "
+                  f"Adam), charged N={N}, B={B} per GPU",
+                  {"n_balls": N, "substeps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                   "parallelism": f"data-parallel x{world}, one {backend or 'no'} all-reduce per step"},
+                  backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0)
+    e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
+    e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
+    if e0:
+        avg = float(np.mean(e0) + (np.mean(e1) if e1 else 0.0))
+        E = B * N * (N - 1)   # edges per substep
+        flop = 2.0 * E * MAC_PER_EDGE_BWD
+        ach = flop / (avg * 1e-3) / 1e12
+        res["roofline"] = {"kernel": "edge_bwd_kernel (pass 0 + pass 1, one substep, SEGNO per-edge clamp)",
+                           "bound": "mfma", "achieved": ach, "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": ach / FP16X3_PEAK_TFLOPS,
+                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)", "traffic": None,
+                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0))] + ([float(np.mean(e1))] if e1 else []),
+                           "algorithmic_gflop_per_launch": flop / 1e9,
+                           "algorithmic_basis": "reverse of W2 and Wc1 per edge (data + weight gradients); "
+                                                "the forward recompute is not counted",
+                           "launches_timed": len(e0) + len(e1),
+                           "share_of_step": float(np.sum(e0) + np.sum(e1)) / (el * 1e3)}
+    if grads0 is not None:
+        from oracle import torch_ref as tr
+        def sample(Bc):
+            r, c = tr.full_edges(Bc, N)
+            rows, erows = Bc * N, Bc * N * (N - 1)
+            return (_cpu(his, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(ea, erows)), _cpu(target, rows)
+
+        Bc = min(B, args.cpu_samples or 64)   # the autograd tape of the dense one-hot mean grows with B^2
+        inp, tgt = sample(Bc)
+        p = {k: t.clone().requires_grad_(True) for k, t in p0.items()}
+        copt = torch.optim.Adam(list(p.values()), lr=1e-4)
+
+        def cstep():
+            copt.zero_grad()
+            xr, _, _ = tr.segno_forward_step(p, *inp, T=T, dense_mean=True)
+            torch.nn.functional.mse_loss(xr, tgt).backward()
+            copt.step()
+
+        med, calls, _ = cpu_time(cstep, args.cpu_budget)
+        res["cpu_baseline"] = _baseline(Bc, med, calls, f"SEGNO training step (forward_step {T} substeps with the "
+                                        f"reference's dense one-hot mean, MSE, autograd backward, Adam) on the first "
+                                        f"{Bc} samples of the batch")
+        # gradient parity over the whole measured batch: float64 autograd with the scatter mean
+        inp, tgt = sample(B)
+        p64 = {k: t.double().requires_grad_(True) for k, t in p0.items()}
+        xr, _, _ = tr.segno_forward_step(p64, *[t.double() if t.is_floating_point() else t for t in inp], T=T,
+                                         dense_mean=False)
+        torch.nn.functional.mse_loss(xr, tgt.double()).backward()
+        errs = {k: float((grads0[k].double() - t.grad).abs().max() / t.grad.abs().max())
+                for k, t in p64.items() if t.grad is not None and float(t.grad.abs().max()) > 0 and k in grads0}
+        worst = max(errs, key=errs.get)
+        res["parity"] = {"samples_checked": B, "tensors_checked": len(errs),
+                         "grad_maxnorm_rel_vs_f64_max": errs[worst], "worst_tensor_vs_f64": worst,
+                         "grad_maxnorm_rel_vs_f64_median": float(np.median(list(errs.values()))),
+                         "note": "first step's gradients at the initial weights, HIP reverse pass vs float64 "
+                                 "torch autograd of the op-by-op restatement; max-norm relative per tensor"}
+    return res
+
+
 def run_egno_rollout(args, world, rank, dev, backend):
     """rollout_fn (main_simulation_simple_no.py:342-384) at the C2 shape, traj_len =
     10 segments (the script's --traj_len default, :79) with per-frame charged energies, as ONE
@@ -797,7 +917,7 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=0, help="samples per GPU (weak scaling; 0 = the workload's default)")
     ap.add_argument("--global-batch", type=int, default=0, help="total samples over all GPUs (strong scaling)")
     ap.add_argument("--workload", default="egno",
-                    choices=["egno", "segno", "segno_gravity", "egno_train", "egno_rollout", "sim_charged"],
+                    choices=["egno", "segno", "segno_gravity", "egno_train", "segno_train", "egno_rollout", "sim_charged"],
                     help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4; "
                          "egno_rollout = SURVEY row f1; sim_charged = row f3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -822,7 +942,8 @@ def main():
     if args.check_launch:
         res = check_launch(args, world, rank, dev, backend)
     else:
-        runners = {"egno": run_egno, "egno_train": run_egno_train, "egno_rollout": run_egno_rollout,
+        runners = {"egno": run_egno, "egno_train": run_egno_train, "segno_train": run_segno_train,
+                   "egno_rollout": run_egno_rollout,
                    "sim_charged": run_sim_charged, "segno": run_segno,
                    "segno_gravity": lambda *a: run_segno(*a, gravity=True)}
         res = runners[args.workload](args, world, rank, dev, backend)

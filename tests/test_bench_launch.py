@@ -55,3 +55,11 @@ def test_strong_scaling_plan():
     a = bench.parse_args(["--gpus", "4"])
     p = bench.batch_plan(a, 4, 2, 512)
     assert p["B"] == 512 and p["B_global"] == 2048 and p["scaling"] == "weak"
+
+
+def test_every_workload_is_registered():
+    """Each --workload choice parses (row †g's segno_train included)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for wl in ("egno", "segno", "segno_gravity", "egno_train", "segno_train", "egno_rollout", "sim_charged"):
+        assert bench.parse_args(["--workload", wl]).workload == wl
