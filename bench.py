@@ -251,6 +251,13 @@ def cpu_time(fn, budget_s, min_calls=1, max_calls=20):
     return float(np.median(times)), len(times), out
 
 
+def cpu_baseline_time(fn, budget_s, min_calls=1, max_calls=20):
+    """cpu_time of the CPU baseline on baseline_threads() torch threads. The threads actually used are
+    recorded by _baseline (called inside the same context)."""
+    with _BaselineThreads():
+        return cpu_time(fn, budget_s, min_calls, max_calls)
+
+
 def _cpu(t, rows=None):
     t = t.detach()
     return (t[:rows] if rows is not None else t).cpu()
@@ -260,10 +267,25 @@ def _cpu_params(model):
     return {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs quota), or None."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) / int(per)))
+    except Exception:   # noqa: BLE001 - informational
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else max(1, q // per)
+    except Exception:   # noqa: BLE001
+        return None
+
+
 def host_cores():
-    """What the CPU baseline ran on: torch's intra-op threads, the CPUs this process may run on, and
-    the host's physical cores (psutil; the GPU box shares a larger host, so only the first two
-    describe the baseline)."""
+    """What the CPU baseline may run on: the host's physical cores (psutil), the CPUs this process may
+    run on (affinity), the cgroup CPU quota and the pool's per-GPU thread share (OMP_NUM_THREADS, set
+    by the GPU pool; the box runs one GPU's share of a larger host)."""
     try:
         import psutil
         phys = psutil.cpu_count(logical=False)
@@ -273,14 +295,41 @@ def host_cores():
         affinity = len(os.sched_getaffinity(0))
     except Exception:   # noqa: BLE001
         affinity = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
     return {"threads": torch.get_num_threads(), "cpus_allowed": affinity, "host_physical_cores": phys,
-            "host_logical_cpus": os.cpu_count()}
+            "host_logical_cpus": os.cpu_count(), "cgroup_cpus": _cgroup_cpus(), "pool_thread_share": share}
+
+
+def baseline_threads():
+    """Threads for the CPU baseline. BASELINE.md §3 asks for every physical host core; on the GPU pool
+    one box is one GPU's share of a larger host, so the count is capped by what this process is granted:
+    min(physical cores, affinity, cgroup quota, the pool's OMP_NUM_THREADS share)."""
+    hc = host_cores()
+    caps = [c for c in (hc["host_physical_cores"], hc["cpus_allowed"], hc["cgroup_cpus"], hc["pool_thread_share"])
+            if c]
+    return max(1, min(caps)) if caps else torch.get_num_threads()
+
+
+class _BaselineThreads:
+    """torch intra-op threads = baseline_threads() for the CPU baseline leg, restored afterwards."""
+
+    def __enter__(self):
+        self.prev = torch.get_num_threads()
+        torch.set_num_threads(baseline_threads())
+        return self
+
+    def __exit__(self, *exc):
+        torch.set_num_threads(self.prev)
 
 
 def _baseline(units, med, calls, sample, unit="trajectories/s"):
     hc = host_cores()
+    hc["threads"] = baseline_threads()   # what cpu_baseline_time ran on
     return {"value": units / med, "unit": unit, "cores": hc["threads"], "kind": "torch-ref",
-            "cores_note": "cores = torch intra-op threads used (hardware threads, not verified physical cores)",
+            "cores_note": "cores = torch intra-op threads used = min(host physical cores, affinity, cgroup quota, "
+                          "the pool's per-GPU OMP_NUM_THREADS share); BASELINE.md §3 asks for every physical core, "
+                          "but the GPU box is one GPU's share of a larger host (host fields below)",
             "host": hc, "median_s_per_call": med, "calls": calls,
             "sample": sample + f"; oracle/torch_ref.py (the reference's torch ops, op by op) on "
                                f"{hc['threads']} host threads, median of {calls} calls"}
@@ -357,7 +406,7 @@ def run_egno(args, world, rank, dev, backend):
                            "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
                            "frac_of_fp32_mfma_peak": achieved / FP32_PEAK_TFLOPS,
-                           "traffic": pmc_traffic("egnn_layer_kernel<EGNO>"), "avg_launch_ms": avg_ms,
+                           "traffic": pmc_traffic("C2", "egnn_layer_kernel<EGNO>"), "avg_launch_ms": avg_ms,
                            "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(layer_events),
                            "tconv_avg_launch_ms": float(np.mean(tconv_ms)) if tconv_ms else None,
                            "north_star_hbm": {
@@ -374,7 +423,7 @@ def run_egno(args, world, rank, dev, backend):
         inp = [_cpu(case[k]) for k in ("x", "h")] + [r, c] + [_cpu(case[k]) for k in ("edge_fea", "v", "loc_mean")]
         t_out = _cpu(case["t_out"])
         with torch.no_grad():
-            med, calls, ref = cpu_time(lambda: tr.egno_forward(p, *inp, t_out, T=T), args.cpu_budget, 3)
+            med, calls, ref = cpu_baseline_time(lambda: tr.egno_forward(p, *inp, t_out, T=T), args.cpu_budget, 3)
         res["cpu_baseline"] = _baseline(B, med, calls, f"EGNO forward at the measured batch B={B}, N={N}, T={T}")
         res["parity"] = dict(_parity(_cpu(out[0]), ref[0]), samples_checked=B,
                              bar="1e-5 max-norm relative (north_star)")
@@ -445,7 +494,7 @@ def run_segno(args, world, rank, dev, backend, gravity=False):
                            "achieved": ach, "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
                            "frac_of_fp32_mfma_peak": ach / FP32_PEAK_TFLOPS,
-                           "traffic": pmc_traffic("egnn_layer_kernel<SEGNO>"), "avg_launch_ms": avg,
+                           "traffic": pmc_traffic("C5" if gravity else "C3", "egnn_layer_kernel<SEGNO>"), "avg_launch_ms": avg,
                            "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(layer),
                            "launch_ms_min_max": [float(np.min(layer)), float(np.max(layer))]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -460,7 +509,7 @@ def run_segno(args, world, rank, dev, backend, gravity=False):
             args_c = (_cpu(his, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(ea, erows), steps,
                       _cpu(q.reshape(-1), rows))
             with torch.no_grad():
-                med, calls, ref = cpu_time(lambda: tr.segno_rollout(p, *args_c, dense_mean=False), args.cpu_budget)
+                med, calls, ref = cpu_baseline_time(lambda: tr.segno_rollout(p, *args_c, dense_mean=False), args.cpu_budget)
             res["cpu_baseline"] = _baseline(Bc, med, calls, f"SEGNO gravity rollout, first {Bc} samples of the "
                                             f"batch, substeps {steps}, scatter mean (the reference's dense mean "
                                             f"is infeasible at this size)")
@@ -471,7 +520,7 @@ def run_segno(args, world, rank, dev, backend, gravity=False):
             r, c = tr.full_edges(B, N)
             args_c = (_cpu(his), _cpu(x), r, c, _cpu(v), _cpu(ea))
             with torch.no_grad():
-                med, calls, ref = cpu_time(lambda: tr.segno_forward_step(p, *args_c, T=steps[0], dense_mean=True),
+                med, calls, ref = cpu_baseline_time(lambda: tr.segno_forward_step(p, *args_c, T=steps[0], dense_mean=True),
                                            args.cpu_budget)
             res["cpu_baseline"] = _baseline(B, med, calls, f"SEGNO embedding + forward_step at the measured batch "
                                             f"B={B}, {steps[0]} substeps, the reference's dense one-hot mean")
@@ -551,8 +600,10 @@ def run_egno_train(args, world, rank, dev, backend):
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0, loss=float(loss.detach()))
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
-    if e0:   # e1 is empty when the merged single-launch edge backward runs (NONODE_EBWD_MERGED=1)
-        avg = float(np.mean(e0) + (np.mean(e1) if e1 else 0.0))
+    wl_key = "C4" if B == 512 else f"C4@B={B}"   # PMC traffic is per measured shard size
+    if e0 or e1:
+        _check_pass_records(e0, e1)
+        avg = float(np.mean(e0) + np.mean(e1))
         E = T * B * N * (N - 1)
         flop = 2.0 * E * MAC_PER_EDGE_BWD
         ach = flop / (avg * 1e-3) / 1e12
@@ -560,10 +611,10 @@ def run_egno_train(args, world, rank, dev, backend):
         res["roofline"] = {"kernel": "edge_bwd_kernel (pass 0 + pass 1, one layer)", "bound": "mfma", "achieved": ach,
                            "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
-                           "traffic": _sum_or_none(pmc_traffic("edge_bwd_kernel<pass 0>"),
-                                                   pmc_traffic("edge_bwd_kernel<pass 1>")),
-                           "traffic_basis": "HBM bytes of pass 0 + pass 1 (profiles/pmc_traffic.json)",
-                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0))] + ([float(np.mean(e1))] if e1 else []),
+                           "traffic": _sum_or_none(pmc_traffic(wl_key, "edge_bwd_kernel<pass 0>"),
+                                                   pmc_traffic(wl_key, "edge_bwd_kernel<pass 1>")),
+                           "traffic_basis": f"HBM bytes of pass 0 + pass 1 measured at {wl_key} (profiles/pmc_traffic.json)",
+                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0)), float(np.mean(e1))],
                            "algorithmic_gflop_per_launch": flop / 1e9,
                            "algorithmic_basis": "reverse of W2 and Wc1 per edge (data + weight gradients); "
                                                 "the forward recompute is not counted",
@@ -592,7 +643,7 @@ def run_egno_train(args, world, rank, dev, backend):
                 first.update({k: t.grad.clone() for k, t in p.items() if t.grad is not None})
             copt.step()
 
-        med, calls, _ = cpu_time(cstep, args.cpu_budget)
+        med, calls, _ = cpu_baseline_time(cstep, args.cpu_budget)
         res["cpu_baseline"] = _baseline(Bc, med, calls, f"EGNO training step (forward, loss, autograd backward, "
                                         f"Adam) at B={Bc}")
         if Bc == B:
@@ -603,16 +654,27 @@ def run_egno_train(args, world, rank, dev, backend):
             pred = xx.reshape(T, Bc, N, 3).permute(1, 2, 0, 3)
             torch.nn.functional.mse_loss(pred, tgt.double(), reduction="none").mean((0, 1, 3)).mean().backward()
             par = {"samples_checked": B, "tensors_checked": 0,
-                   "note": "first step's gradients at the initial weights, HIP backward vs torch autograd of "
-                           "the op-by-op restatement; max-norm relative per tensor"}
-            for tag, ref in (("f64", {k: t.grad for k, t in p64.items() if t.grad is not None}), ("ref_fp32", first)):
-                errs = {k: float((grads0[k].double() - ref[k].double()).abs().max() / ref[k].abs().max())
+                   "note": "first step's gradients at the initial weights, max-norm relative per tensor. The parity "
+                           "figure is grad_maxnorm_rel_vs_f64 (HIP backward vs float64 torch autograd of the op-by-op "
+                           "restatement). The *_vs_ref_fp32 figures compare HIP with the same autograd run in fp32 and "
+                           "are dominated by the fp32 torch path's own rounding: ref_fp32_own_error_vs_f64_max is that "
+                           "path's distance from float64 on the same tensors"}
+            g64 = {k: t.grad for k, t in p64.items() if t.grad is not None}
+
+            def rel(a, ref):
+                return {k: float((a[k].double() - ref[k].double()).abs().max() / ref[k].abs().max())
                         for k in ref if float(ref[k].abs().max()) > 0}
+
+            for tag, ref in (("f64", g64), ("ref_fp32", first)):
+                errs = rel(grads0, ref)
                 worst = max(errs, key=errs.get)
                 par[f"grad_maxnorm_rel_vs_{tag}_max"] = errs[worst]
                 par[f"grad_maxnorm_rel_vs_{tag}_median"] = float(np.median(list(errs.values())))
                 par[f"worst_tensor_vs_{tag}"] = worst
                 par["tensors_checked"] = len(errs)
+            own = rel(first, g64)
+            par["ref_fp32_own_error_vs_f64_max"] = max(own.values())
+            par["ref_fp32_own_error_worst_tensor"] = max(own, key=own.get)
             res["parity"] = par
     return res
 
@@ -683,16 +745,20 @@ def run_segno_train(args, world, rank, dev, backend):
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0)
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
-    if e0:
-        avg = float(np.mean(e0) + (np.mean(e1) if e1 else 0.0))
+    if e0 or e1:
+        _check_pass_records(e0, e1)
+        avg = float(np.mean(e0) + np.mean(e1))
         E = B * N * (N - 1)   # edges per substep
         flop = 2.0 * E * MAC_PER_EDGE_BWD
         ach = flop / (avg * 1e-3) / 1e12
         res["roofline"] = {"kernel": "edge_bwd_kernel (pass 0 + pass 1, one substep, SEGNO per-edge clamp)",
                            "bound": "mfma", "achieved": ach, "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": ach / FP16X3_PEAK_TFLOPS,
-                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)", "traffic": None,
-                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0))] + ([float(np.mean(e1))] if e1 else []),
+                           "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
+                           "traffic": _sum_or_none(pmc_traffic("segno_train", "edge_bwd_kernel<pass 0>"),
+                                                   pmc_traffic("segno_train", "edge_bwd_kernel<pass 1>")),
+                           "traffic_basis": "HBM bytes of pass 0 + pass 1 per substep (profiles/pmc_traffic.json)",
+                           "avg_launch_ms": avg, "pass_ms": [float(np.mean(e0)), float(np.mean(e1))],
                            "algorithmic_gflop_per_launch": flop / 1e9,
                            "algorithmic_basis": "reverse of W2 and Wc1 per edge (data + weight gradients); "
                                                 "the forward recompute is not counted",
@@ -716,7 +782,7 @@ def run_segno_train(args, world, rank, dev, backend):
             torch.nn.functional.mse_loss(xr, tgt).backward()
             copt.step()
 
-        med, calls, _ = cpu_time(cstep, args.cpu_budget)
+        med, calls, _ = cpu_baseline_time(cstep, args.cpu_budget)
         res["cpu_baseline"] = _baseline(Bc, med, calls, f"SEGNO training step (forward_step {T} substeps with the "
                                         f"reference's dense one-hot mean, MSE, autograd backward, Adam) on the first "
                                         f"{Bc} samples of the batch")
@@ -787,8 +853,8 @@ def run_egno_rollout(args, world, rank, dev, backend):
                            "peak": FP16X3_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach / FP16X3_PEAK_TFLOPS,
                            "peak_basis": "dense fp16 MFMA peak / 3 (fp16x3 split products)",
                            "frac_of_fp32_mfma_peak": ach / FP32_PEAK_TFLOPS,
-                           "traffic": None, "avg_launch_ms": avg, "algorithmic_gflop_per_launch": flop / 1e9,
-                           "launches_timed": len(layer),
+                           "traffic": pmc_traffic("f1", "egnn_layer_kernel<EGNO>"), "avg_launch_ms": avg,
+                           "algorithmic_gflop_per_launch": flop / 1e9, "launches_timed": len(layer),
                            "layer_kernel_share": float(np.sum(layer)) / (el / args.steps * 1e3)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import torch_ref as tr
@@ -799,7 +865,7 @@ def run_egno_rollout(args, world, rank, dev, backend):
         args_c = (_cpu(nodes, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(eao, erows), _cpu(ea, erows),
                   _cpu(lm, rows), N, L, Bc, _cpu(q.reshape(-1), rows))
         with torch.no_grad():
-            med, calls, ref = cpu_time(lambda: tr.egno_rollout(p, *args_c, T=T, t_out=_cpu(t_all, Bc)),
+            med, calls, ref = cpu_baseline_time(lambda: tr.egno_rollout(p, *args_c, T=T, t_out=_cpu(t_all, Bc)),
                                        args.cpu_budget)
         res["cpu_baseline"] = _baseline(Bc, med, calls, f"EGNO rollout_fn positions, first {Bc} samples of the "
                                         f"batch, traj_len={L} (energies not included)")
@@ -895,17 +961,27 @@ def run_sim_charged(args, world, rank, dev, backend):
     return res
 
 
+def _check_pass_records(e0, e1):
+    """The edge backward is two launches (pass A, pass B) per layer / substep: both must have been
+    recorded the same number of times, else the roofline would price a partial edge backward."""
+    if not e0 or len(e0) != len(e1):
+        raise RuntimeError(f"edge backward profile records: {len(e0)} pass-A vs {len(e1)} pass-B launches "
+                           f"(profile buffer too small?)")
+
+
 def _sum_or_none(*xs):
     return None if any(x is None for x in xs) else float(sum(xs))
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` measured on `workload` (C2, C3, C4, C4@4096, C5, segno_train, ...)
+    from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json, tools/pmc_traffic.py), or None
+    when that workload's kernel was not measured (never another workload's figure)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:
+        return d.get(workload, {}).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:   # noqa: BLE001 - absent file: no traffic figure
         return None
 
 

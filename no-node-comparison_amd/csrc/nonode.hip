@@ -33,10 +33,6 @@ typedef float f8 __attribute__((ext_vector_type(8)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
 
-// tconv_kernel h stream cache policy: bit 0 = nontemporal loads, bit 1 = nontemporal stores
-#ifndef NONODE_TC_NT
-#define NONODE_TC_NT 0
-#endif
 constexpr int HID = 64;    // hidden width (hidden_nf in model_confs.yaml:5,25)
 constexpr int ROWP = 68;   // LDS row stride of node tables (floats): 64 + 4 breaks bank aliasing
 constexpr int TMAX = 16;   // max trajectory length handled by tconv_kernel
@@ -366,11 +362,7 @@ __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H
 
 // f4 sum as four plain v_add_f32: the backend would emit two v_pk_add_f32, which cost more than the
 // plain ops they replace when issued beside MFMAs (MI355X_MICROARCH.md constants table)
-#ifndef NONODE_SCALAR_ADD
-#define NONODE_SCALAR_ADD 1
-#endif
 __device__ __forceinline__ f4 add4(f4 a, f4 b) {
-#if NONODE_SCALAR_ADD
   f4 r;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {   // in place, for the reason given at resid_lo
@@ -378,9 +370,6 @@ __device__ __forceinline__ f4 add4(f4 a, f4 b) {
     asm("v_add_f32 %0, %0, %1" : "+v"(r[q]) : "v"(b[q]));
   }
   return r;
-#else
-  return a + b;
-#endif
 }
 __device__ __forceinline__ void load_ecl(f4 (&d)[4], const float* row, int g) {
 #pragma unroll
@@ -1668,11 +1657,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   auto hval = [&](int t) -> f4 {
     if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + (p.frames ? hin_part((size_t)t * BN + sc) : base);
-#if NONODE_TC_NT & 1
-    return __builtin_nontemporal_load(reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs));
-#else
     return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs);
-#endif
   };
   __syncthreads();
   // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
@@ -1841,11 +1826,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
         }
       }
       if (svalid) {
-#if NONODE_TC_NT & 2
-        __builtin_nontemporal_store(o, reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs));
-#else
         *reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs) = o;
-#endif
       }
     }
   }

@@ -137,24 +137,6 @@ __global__ void pack_bwd_kernel(PackArgs a) {
   }
 }
 
-#ifndef NONODE_BWD_PIN
-#define NONODE_BWD_PIN 0
-#endif
-// one unit through register-resident fragments (the NONODE_BWD_PIN diagnostic variant)
-__device__ __forceinline__ void mfma_h16f(f4 (&acc)[4], const H16Frags& f, const h8 (&xh)[2], const h8 (&xl)[2],
-                                          unsigned us) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const h8 xs = h8_scale(xh[s], us);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xh[s], acc[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.lo[s][mo], xs, acc[mo]);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) acc[mo] = mfma16(f.hi[s][mo], xl[s], acc[mo]);
-  }
-}
-
 // ---- true-scale SiLU and its derivative ---------------------------------------------------------
 __device__ __forceinline__ float sigm(float z) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z * NEG_LOG2E)); }
 __device__ __forceinline__ void silu_true(f4 (&a)[4]) {
@@ -712,17 +694,6 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
     STAMP(PASS ? 9 : 14);
     // ---- B: one unit (16 edges: receivers of a tile x sender offset k) at a time ----
     const int U = ctc * Nm1;
-#if NONODE_BWD_PIN
-    // diagnostic variant (AGPR pin): PASS 0's W2 / Wc1 fp16 fragments read from LDS
-    // once per chunk (after the chunk's barrier) and pinned in AGPRs for the unit loop
-    H16Frags fw2, fwc1;
-    if (PASS == 0) {
-      load_h16frags(fw2, hW2, lane);
-      load_h16frags(fwc1, hWc1, lane);
-      pin_agpr(fw2);
-      pin_agpr(fwc1);
-    }
-#endif
     f4 gaR[4];   // pass B: GA of the current tile's receivers (lane e), and the receiver-side GX
     zero4(gaR);
     float gxR0 = 0.f, gxR1 = 0.f, gxR2 = 0.f;
@@ -852,11 +823,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
             load_vp(z2, sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64, g);
             h8 xh[2], xl[2];
             h16_split(a, xh, xl);
-#if NONODE_BWD_PIN
-            mfma_h16f(z2, fw2, xh, xl, h16_us(bb + BOFF_SCAL, BH_W2));
-#else
             mfma_h16(z2, hW2, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_W2));
-#endif
           }
           {
             f4 m[4];
@@ -865,11 +832,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
             load_vp(z3, sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64, g);
             h8 xh[2], xl[2];
             h16_split(m, xh, xl);
-#if NONODE_BWD_PIN
-            mfma_h16f(z3, fwc1, xh, xl, h16_us(bb + BOFF_SCAL, BH_WC1));
-#else
             mfma_h16(z3, hWc1, xh, xl, lane, h16_us(bb + BOFF_SCAL, BH_WC1));
-#endif
           }
           bigA = __any(ma > H16_LIMIT);
           bigM = __any(mm > H16_LIMIT);
@@ -1096,10 +1059,28 @@ int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_ma
   int s_max = 0;
   while (ct > 1 && edge_bwd_lds_floats(pass, ct, N, &s_max) * 4 > 160 * 1024) --ct;
   size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max) * 4;
-  if (lds > 160 * 1024) return fail(NONODE_EUNSUPPORTED, "egno_backward: N=%d too large", N);
+  if (lds > 160 * 1024)
+    return fail(NONODE_EUNSUPPORTED, "edge backward: N=%d too large (pass %d LDS tables %zu bytes > 160 KB)", N, pass, lds);
   const size_t red = (size_t)4 * EW_STRIDE * 4;   // the end-of-kernel partial combine
   lds = lds > red ? lds : red;
   *ct_out = ct; *s_max_out = s_max; *lds_out = lds;
+  return NONODE_OK;
+}
+
+// grid of the edge backward over n_graphs graphs (one workgroup per CU, at most EB_MAX_BLOCKS)
+int edge_bwd_grid(int n_graphs) {
+  int G = num_cus();
+  G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
+  return n_graphs < G ? n_graphs : G;
+}
+// the entry points check that both passes' LDS tables fit before any launch, naming themselves
+int edge_bwd_fits(const char* who, int n_graphs, int N) {
+  int ct, s_max;
+  size_t lds;
+  for (int pass = 0; pass < 2; ++pass)
+    if (edge_bwd_config(pass, n_graphs, N, edge_bwd_grid(n_graphs), &ct, &s_max, &lds))
+      return fail(NONODE_EUNSUPPORTED, "%s: N=%d too large for the edge backward (pass %d LDS tables > 160 KB; "
+                  "training supports N <= 31)", who, N, pass);
   return NONODE_OK;
 }
 
@@ -1406,8 +1387,7 @@ int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
   return check_launch("tconv_bwd_kernel");
 }
 
-// TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. One thread per (c, d).
-// Writes gx, gv and per-thread weight-gradient terms part[(c*3+d)][i][o][m][2].
+// TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. Writes gx, gv.
 // One thread per (column c, coordinate d); the block sums its threads' weight-gradient terms in a
 // fixed order and writes one row of 2*2*MMAX_T*2 partials (tconvx_grad_finish adds the blocks' rows).
 constexpr int TX_THREADS = 128;
@@ -1806,7 +1786,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.Pn = take(n * 64); w.Qn = take(n * 64);
   w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
-  w.xpart = take(BN * 3 * 2 * 2 * MMAX_T * 2);
+  w.xpart = take((BN * 3 + TX_THREADS - 1) / TX_THREADS * (2 * 2 * MMAX_T * 2));   // one row per tconvx block
   w.partial = take((size_t)GEMM_BATCH_MAX * (GEMM_MAX_WAVES / 4 + 1) * 64 * 65);   // gemm_tn_batch partials
   w.floats = tot;
   return w;
@@ -1987,9 +1967,7 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, const Gemm& gemm, hipS
   ReduceJob rjobs[REDUCE_BATCH_MAX];
   int nred = 0;
   {
-    int G = num_cus();
-    G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
-    G = r.n_graphs < G ? r.n_graphs : G;
+    const int G = edge_bwd_grid(r.n_graphs);
     EdgeBwdArgs ea;
     ea.n_graphs = r.n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = r.ef_mod; ea.ct = 0; ea.s_max = 0;
     ea.segno = 0;
@@ -2083,6 +2061,7 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
       (!tc && (tconvx_w || g_tconv || g_tconvx)) || !bblobs || !state || !g_x || !layer_grads ||
       !g_emb_w || !g_emb_b || !workspace || (n_edge_feat > 0 && !edge_fea))
     return fail(NONODE_EINVAL, "egno_backward: null pointer");
+  if (int rc = edge_bwd_fits("egno_backward", B * T, N)) return rc;
   const int M = effective_modes(T, modes);
   if (workspace_bytes < nonode_egno_backward_workspace_bytes(B, N, T, modes))
     return fail(NONODE_EINVAL, "egno_backward: workspace too small");
@@ -2319,6 +2298,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
     return fail(NONODE_EINVAL, "segno_backward: missing gradient pointer");
   if (workspace_bytes < nonode_segno_backward_workspace_bytes(B, N))
     return fail(NONODE_EINVAL, "segno_backward: workspace too small");
+  if (int rc = edge_bwd_fits("segno_backward", B, N)) return rc;
   hipStream_t s = (hipStream_t)stream;
   const int ne = n_edge_feat, ld1 = 2 * HID + 1 + ne;
   const size_t n = (size_t)B * N;
@@ -2356,9 +2336,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
     hipMemsetAsync(w.GB, 0, n * 64 * sizeof(float), s);
     hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
     {
-      int G = num_cus();
-      G = G < EB_MAX_BLOCKS ? G : EB_MAX_BLOCKS;
-      G = B < G ? B : G;
+      const int G = edge_bwd_grid(B);
       EdgeBwdArgs ea;
       ea.segno = 1;
       ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
@@ -2422,6 +2400,7 @@ int nonode_egnn_layer_bwd(int variant, int n_graphs, int N, int n_edge_feat, int
     return fail(NONODE_EINVAL, "egnn_layer_bwd: null pointer");
   if (workspace_bytes < nonode_egnn_layer_bwd_workspace_bytes(n_graphs, N))
     return fail(NONODE_EINVAL, "egnn_layer_bwd: workspace too small");
+  if (int rc = edge_bwd_fits("egnn_layer_bwd", n_graphs, N)) return rc;
   hipStream_t s = (hipStream_t)stream;
   const size_t n = (size_t)n_graphs * N;
   BwdWs w = bwd_ws(workspace, n_graphs, N, 1, 1);

@@ -33,22 +33,26 @@ def _reduce_device(dev):
     return dev if dist.get_backend() == "nccl" else torch.device("cpu")
 
 
+def allreduce_scalar(value, op, dev=torch.device("cpu")):
+    """One scalar all-reduce of a host number over the process group (a device tensor under RCCL,
+    a host tensor under gloo). Runs the collective at any world size, 1 included."""
+    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(dev))
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
 def max_over_ranks(value, dev=torch.device("cpu")):
     """Max of a host float over all ranks (the bench's step time): one scalar all-reduce."""
     if not _initialized() or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(dev))
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return allreduce_scalar(value, dist.ReduceOp.MAX, dev)
 
 
 def sum_over_ranks(value, dev=torch.device("cpu")):
     """Sum of a host number over all ranks (e.g. samples processed)."""
     if not _initialized() or dist.get_world_size() == 1:
         return float(value)
-    t = torch.tensor([float(value)], dtype=torch.float64, device=_reduce_device(dev))
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return allreduce_scalar(value, dist.ReduceOp.SUM, dev)
 
 
 def gather_samples(local, total):
@@ -122,10 +126,15 @@ class FlatGrads:
         self._bind()
         return self.flat
 
+    def exchange_(self):
+        """The step's one collective: sum of the flat buffer over the ranks, then / world size
+        (runs at any world size; allreduce_ skips it when there is nothing to exchange)."""
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
+        self.flat.div_(dist.get_world_size())
+        return self.flat
+
     def allreduce_(self):
         self.gather_()
         if not _initialized() or dist.get_world_size() == 1:
             return self.flat
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
-        self.flat.div_(dist.get_world_size())
-        return self.flat
+        return self.exchange_()

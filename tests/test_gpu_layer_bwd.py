@@ -13,8 +13,9 @@ import torch
 
 import no_node_comparison_amd as pkg
 from no_node_comparison_amd import _lib
+from oracle import egno_grad as og
 from tests.conftest import check_rel, load_golden, params_of
-from tests.test_gpu_parity import DEV, _dev, _egno
+from tests.test_gpu_parity import DEV, _dev, _egno, _egno_case, _sd_np
 
 pytestmark = pytest.mark.gpu
 GTOL = 1e-5
@@ -92,6 +93,63 @@ def test_egno_tconv_bwd_matches_reference_block_autograd(i):
     gXi = lg[f"tcx{i}::gin0"]
     check_rel(f"tconv_x {i} dL/dx_in", gxi, gXi[..., 0].reshape(T * BN, 3), GTOL)
     check_rel(f"tconv_x {i} dL/dv_in", gvi, gXi[..., 1].reshape(T * BN, 3), GTOL)
+
+
+def _layer_bwd(m, i, n_graphs, N, h, x, v, ef, gxo, gvo, gho):
+    L = pkg.lib()
+    blobs, _ = m._packed()
+    bblobs = m._packed_bwd()
+    names = m.layer_param_names(i)
+    grads = {nm: torch.empty_like(dict(m.named_parameters())[nm]) for nm in names}
+    lgs = _lib.LayerGrads(*[grads[nm].data_ptr() for nm in names])
+    ghi, gxi, gvi = torch.empty_like(h), torch.empty_like(x), torch.empty_like(v)
+    ws_bytes = L.nonode_egnn_layer_bwd_workspace_bytes(n_graphs, N)
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=DEV)
+    P = _lib.ptr
+    _lib.check(L.nonode_egnn_layer_bwd(_lib.VARIANT_EGNO, n_graphs, N, 2, n_graphs, P(h), P(x), P(v), P(ef),
+                                       P(blobs[i]), P(bblobs[i]), P(gxo), P(gvo), P(gho), ctypes.byref(lgs), P(ghi),
+                                       P(gxi), P(gvi), P(ws), ws_bytes, _lib.stream_of(x)))
+    torch.cuda.synchronize()
+    return grads, ghi, gxi, gvi
+
+
+@pytest.mark.parametrize("N", [26, 31])
+def test_egnn_layer_bwd_large_n_matches_float64_oracle(N):
+    """The layer entry point at the top of the training range (N <= 31, set by the edge backward's
+    LDS tables), against the float64 reverse pass of oracle/egno_grad.py (basic.py:167-186)."""
+    B, i = 3, 2
+    c = _egno_case(B, N, 10, seed=N)
+    m = _egno(T=10, seed=N)
+    rng = np.random.default_rng(N)
+    h = rng.standard_normal((B * N, 64)) * 0.7
+    gxo, gvo, gho = (rng.standard_normal(s) * 1e-3 for s in ((B * N, 3), (B * N, 3), (B * N, 64)))
+    grads, ghi, gxi, gvi = _layer_bwd(m, i, B, N, _dev(h.astype(np.float32)), _dev(c["x"]), _dev(c["v"]),
+                                      _dev(c["edge_fea"]), *(_dev(a.astype(np.float32)) for a in (gxo, gvo, gho)))
+    p = _sd_np(m)
+    f64 = lambda a: np.asarray(a, np.float64)  # noqa: E731
+    h32 = f64(h.astype(np.float32))
+    _, _, _, cache = og.egnn_layer_fwd(p, f"layers.{i}", f64(c["x"]), h32, c["row"], c["col"], f64(c["edge_fea"]),
+                                       f64(c["v"]))
+    rg = {}
+    gx, gh, gv, _ = og.egnn_layer_bwd(p, f"layers.{i}", cache, *(f64(a.astype(np.float32)) for a in (gxo, gvo, gho)),
+                                      rg)
+    for nm in m.layer_param_names(i):
+        check_rel(f"N={N} grad {nm}", grads[nm], rg[nm], GTOL)
+    check_rel(f"N={N} dL/dx_in", gxi, gx, GTOL)
+    check_rel(f"N={N} dL/dh_in", ghi, gh, GTOL)
+    check_rel(f"N={N} dL/dv_in", gvi, gv, GTOL)
+
+
+def test_layer_bwd_rejects_n_beyond_the_tables_before_any_launch():
+    L = pkg.lib()
+    lg = _lib.LayerGrads()
+    t = torch.zeros(16, device=DEV)
+    P = _lib.ptr
+    N = 40
+    ws = L.nonode_egnn_layer_bwd_workspace_bytes(2, N)
+    rc = L.nonode_egnn_layer_bwd(_lib.VARIANT_EGNO, 2, N, 2, 2, *([P(t)] * 9), ctypes.byref(lg), P(t), P(t), P(t),
+                                 P(t), ws, _lib.stream_of(t))
+    assert rc != 0 and b"egnn_layer_bwd: N=40 too large" in L.nonode_last_error()
 
 
 def test_layer_bwd_rejects_segno_and_small_workspace():

@@ -220,7 +220,7 @@ def test_segno_substep_fusion_is_bitwise_unfused(monkeypatch, B, N, T):
         with torch.no_grad():
             out = m(his, x, ei, v, ea, T=T)
         torch.cuda.synchronize()
-        return [t.clone() for t in out[:2]]
+        return [t.clone() for t in out]   # x, h and v (v leaves LDS only at the last substep in keep mode)
 
     ref = None
     for env in ({}, {"NONODE_NO_KEEP": "1"}, {"NONODE_NO_FUSE": "1"}):

@@ -72,6 +72,25 @@ def test_reductions_gloo_ws2():
     _run(2, _reductions)
 
 
+def _exchange_world1(rank, world):
+    # the collectives FlatGrads / the bench timing run at world size 1 (the world-1 early returns
+    # bypassed), here over gloo; tests/test_gpu_rccl.py runs the same calls over RCCL on the GPU
+    from no_node_comparison_amd.sharding import FlatGrads, allreduce_scalar
+    p = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7))]
+    fg = FlatGrads(p)
+    for q in p:
+        q.grad = torch.randn_like(q)
+    before = fg.gather_().clone()
+    assert torch.equal(fg.exchange_(), before)
+    assert all(q.grad.data_ptr() == v.data_ptr() for q, v in zip(fg.params, fg.views))
+    assert allreduce_scalar(2.5, dist.ReduceOp.MAX) == 2.5
+    assert allreduce_scalar(2.5, dist.ReduceOp.SUM) == 2.5
+
+
+def test_exchange_runs_at_world1_gloo():
+    _run(1, _exchange_world1)
+
+
 def _bench_shards(rank, world, B_per, N):
     import bench
     loc, vel, q = bench.rank_batch(B_per, world, rank, N, seed=99)

@@ -1,6 +1,7 @@
-"""Per-kernel HBM traffic per launch from a tools/gpu_profile.sh output directory.
+"""Per-kernel HBM traffic per launch of one workload from a `tools/gpu.sh profile` output directory.
 
-Usage: python3 tools/pmc_traffic.py gpurun_out/prof_TAG > profiles/pmc_traffic.json
+Usage: python3 tools/pmc_traffic.py WORKLOAD gpurun_out/prof_TAG_<workload> [--merge profiles/pmc_traffic.json]
+(WORKLOAD = the key bench.py's pmc_traffic() looks up: C2, C3, C4, C4@B=4096, C5, segno_train, f1)
 
 FETCH_SIZE / WRITE_SIZE are in KB per dispatch. On gfx950 FETCH_SIZE reports half the bytes of
 wide coalesced reads (MI355X_MICROARCH.md, HBM / rocprofv3 section), so
@@ -31,7 +32,7 @@ def kernel_key(name):
     return None
 
 
-def main(d):
+def main(workload, d, merge=None):
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(f"{d}/pmc_*/**/*counter_collection.csv", recursive=True):
         per = collections.defaultdict(float)
@@ -48,9 +49,24 @@ def main(d):
             row["hbm_bytes_per_launch"] = (2 * row["FETCH_SIZE"] + row["WRITE_SIZE"]) * 1024
             row["correction"] = "(2*FETCH_SIZE + WRITE_SIZE) KB -> bytes; FETCH doubled per MI355X_MICROARCH.md HBM section"
         out[k] = row
-    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    if merge:
+        try:
+            allw = json.load(open(merge))
+        except FileNotFoundError:
+            allw = {}
+        allw[workload] = out
+        with open(merge, "w") as f:
+            json.dump(allw, f, indent=1, sort_keys=True)
+            f.write("\n")
+    json.dump({workload: out}, sys.stdout, indent=1, sort_keys=True)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    a = sys.argv[1:]
+    m = None
+    if "--merge" in a:
+        i = a.index("--merge")
+        m = a[i + 1]
+        a = a[:i] + a[i + 2:]
+    main(a[0], a[1], m)
