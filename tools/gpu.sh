@@ -66,7 +66,7 @@ step_ab() {
 
 step_profile() {
   local wl OUT ctr
-  for wl in ${WORKLOADS:-egno}; do
+  for wl in ${WORKLOADS-egno}; do
     OUT=gpurun_out/prof_${TAG:-r04}_$wl
     mkdir -p $OUT
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py \
