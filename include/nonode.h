@@ -304,7 +304,7 @@ int nonode_egnn_layer_bwd(int variant, int n_graphs, int N, int n_edge_feat, int
  * nonode_egno_tconv_bwd: TimeConv + TimeConv_x of one EGNO layer (layer_no.py:80-178, egno.py:99-108)
  * on time-major [T][BN] inputs h [..][64], x, v [..][3] with loc_mean [BN][3], as nonode_egno_tconv
  * runs it (tconv_blob from nonode_pack_tconv; tconv_w / tconvx_w the raw weights1 tensors
- * [64][64][modes][2] / [2][2][modes][2], modes <= 4). Given the gradients of its outputs (NULL = 0)
+ * [64][64][modes][2] / [2][2][modes][2], modes <= 9). Given the gradients of its outputs (NULL = 0)
  * writes the input gradients and the weights1 gradients.
  */
 size_t nonode_egno_tconv_bwd_workspace_bytes(int BN, int T, int modes);

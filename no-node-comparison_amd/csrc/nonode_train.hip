@@ -21,7 +21,21 @@
 
 namespace {
 
-constexpr int MMAX_T = 4;   // training path: at most 4 Fourier modes (tconv_bwd_kernel<MM> registers)
+#ifndef NONODE_PAIR_A
+#define NONODE_PAIR_A 1
+#endif
+#ifndef NONODE_PAIR_B
+#define NONODE_PAIR_B 1
+#endif
+#ifndef NONODE_PAIR_FENCE
+#define NONODE_PAIR_FENCE 1
+#endif
+#if NONODE_PAIR_FENCE
+#define PAIR_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define PAIR_FENCE() do {} while (0)
+#endif
+constexpr int MMAX_T = 9;   // training path: every rfft bin of T <= 16 (as the forward, MMAX): tconv_bwd_kernel<1..9>
 
 // ---- backward weight blob (unscaled f32 fragments, forward and transposed) --------------------
 enum : int {
@@ -169,6 +183,17 @@ __device__ __forceinline__ void silu_keep(const f4 (&z)[4], f4 (&s)[4], f4 (&a)[
       a[mt][q] = z[mt][q] * s[mt][q];
     }
 }
+// a = SiLU(z) and d = SiLU'(z) = s (1 + z (1 - s)) (one exp + one rcp per value)
+__device__ __forceinline__ void silu_dsilu(const f4 (&z)[4], f4 (&a)[4], f4 (&d)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float s = sigm(z[mt][q]);
+      a[mt][q] = z[mt][q] * s;
+      d[mt][q] = s * fmaf(z[mt][q], 1.f - s, 1.f);
+    }
+}
 // g *= silu'(z) from the kept sigmoid
 __device__ __forceinline__ void mul_dsilu_s(f4 (&gz)[4], const f4 (&z)[4], const f4 (&s)[4]) {
 #pragma unroll
@@ -230,6 +255,70 @@ __device__ __forceinline__ void h4_split(f4 v, h4& hi, h4& lo) {
 }
 __device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
+}
+// The pair path's weight-gradient MFMAs (wgrad_pair) are inline asm with the accumulators bound to
+// AGPRs ("+a"): the library forces VGPR-form MFMAs, which would keep dWc1's 64 accumulator values in
+// VGPRs through pass A's pair loop (its register demand then exceeds 512 and LLVM's AGPR-copy rewrite
+// crashes). The hazard recognizer does not see inside asm, so each statement carries its own wait
+// states: "s_nop 1" first (an accumulator the compiler just wrote or copied, read as C) and "s_nop 11"
+// last (12 states: an MFMA result read or copied by compiler code after the statement, the 8-pass XDL
+// requirement, more than a 16x16x32 MFMA needs); inside, consecutive MFMAs only chain accumulators.
+// One statement = the 12 MFMAs of one output row block (3 fp16x3 terms x 4 column blocks).
+__device__ __forceinline__ void amfma32_block(f4 (&acc)[4], h8 al, h8 ah, const h8 (&bh)[4], const h8 (&bl)[4]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %4, %6, %0\n\t"
+      "v_mfma_f32_16x16x32_f16 %1, %4, %7, %1\n\t"
+      "v_mfma_f32_16x16x32_f16 %2, %4, %8, %2\n\t"
+      "v_mfma_f32_16x16x32_f16 %3, %4, %9, %3\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %5, %10, %0\n\t"
+      "v_mfma_f32_16x16x32_f16 %1, %5, %11, %1\n\t"
+      "v_mfma_f32_16x16x32_f16 %2, %5, %12, %2\n\t"
+      "v_mfma_f32_16x16x32_f16 %3, %5, %13, %3\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %5, %6, %0\n\t"
+      "v_mfma_f32_16x16x32_f16 %1, %5, %7, %1\n\t"
+      "v_mfma_f32_16x16x32_f16 %2, %5, %8, %2\n\t"
+      "v_mfma_f32_16x16x32_f16 %3, %5, %9, %3\n\t"
+      "s_nop 11"
+      : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3])
+      : "v"(al), "v"(ah), "v"(bh[0]), "v"(bh[1]), "v"(bh[2]), "v"(bh[3]), "v"(bl[0]), "v"(bl[1]), "v"(bl[2]),
+        "v"(bl[3]));
+}
+// the same for the single-unit form in pass A (K = 16: fp16x3 on v_mfma_f32_16x16x16_f16, operands
+// split on the VALU just before: the leading s_nop 1 covers that write)
+__device__ __forceinline__ void amfma16_block(f4 (&acc)[4], h4 gl, h4 gh, const h4 (&ah)[4], const h4 (&al)[4]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x16_f16 %0, %4, %6, %0\n\t"
+      "v_mfma_f32_16x16x16_f16 %1, %4, %7, %1\n\t"
+      "v_mfma_f32_16x16x16_f16 %2, %4, %8, %2\n\t"
+      "v_mfma_f32_16x16x16_f16 %3, %4, %9, %3\n\t"
+      "v_mfma_f32_16x16x16_f16 %0, %5, %10, %0\n\t"
+      "v_mfma_f32_16x16x16_f16 %1, %5, %11, %1\n\t"
+      "v_mfma_f32_16x16x16_f16 %2, %5, %12, %2\n\t"
+      "v_mfma_f32_16x16x16_f16 %3, %5, %13, %3\n\t"
+      "v_mfma_f32_16x16x16_f16 %0, %5, %6, %0\n\t"
+      "v_mfma_f32_16x16x16_f16 %1, %5, %7, %1\n\t"
+      "v_mfma_f32_16x16x16_f16 %2, %5, %8, %2\n\t"
+      "v_mfma_f32_16x16x16_f16 %3, %5, %9, %3\n\t"
+      "s_nop 11"
+      : "+a"(acc[0]), "+a"(acc[1]), "+a"(acc[2]), "+a"(acc[3])
+      : "v"(gl), "v"(gh), "v"(ah[0]), "v"(ah[1]), "v"(ah[2]), "v"(ah[3]), "v"(al[0]), "v"(al[1]), "v"(al[2]),
+        "v"(al[3]));
+}
+// exact f32 form (16x16x4 f32), one k-step: acc[ot][it] += gv[ot] av[it]
+__device__ __forceinline__ void amfma4_block(f4 (&acc)[4][4], const float (&gv)[4], const float (&av)[4]) {
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot)
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_16x16x4_f32 %0, %4, %5, %0\n\t"
+        "v_mfma_f32_16x16x4_f32 %1, %4, %6, %1\n\t"
+        "v_mfma_f32_16x16x4_f32 %2, %4, %7, %2\n\t"
+        "v_mfma_f32_16x16x4_f32 %3, %4, %8, %3\n\t"
+        "s_nop 11"
+        : "+a"(acc[ot][0]), "+a"(acc[ot][1]), "+a"(acc[ot][2]), "+a"(acc[ot][3])
+        : "v"(gv[ot]), "v"(av[0]), "v"(av[1]), "v"(av[2]), "v"(av[3]));
 }
 
 // ---- training-forward helpers (h0_kernel: nonode.hip) ----------------------------------------
@@ -451,13 +540,14 @@ size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
          4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (size_t)s_max * (ROWP + 4)) : 0);
 }
 
-// acc[ot][it] += sum over the unit's 16 edges of G[e][16 ot + .] (x) A[e][16 it + .]; lane (e, g)
-// of acc[ot][it][q] holds dW[16 ot + 4 g + q][16 it + e]. bsum[t] += G summed over the lane's four
-// edges 4g..4g+3 at channel 16 t + e (the bias gradient, finished by group_sum).
+// acc[ot][it] += sum over the unit's 16 edges of G[e] (x) A[e], accumulated in image-column order
+// (chan_img, below: the order of the pair path's K = 32 form, so both forms share one accumulator):
+// lane (e, g) of acc[ot][it][q] holds dW[chan_img(ot, 4g + q)][chan_img(it, e)].
 // fp16x3 on v_mfma_f32_16x16x16_f16 (K = the unit's 16 edges: lane (e', g) supplies edges
-// 4g .. 4g+3 of channel 16 t + e' after the LDS transpose). acc and bsum are kept in
-// units of 1/sc: sc is a wave-uniform running power-of-two scale for G, lowered (and acc, bsum
-// rescaled, exactly) when a unit's G is larger than any before it, so G sc stays below 2^12.
+// 4g .. 4g+3 of channel chan_img(t, e') after the LDS transpose). acc is kept in units of 1/sc: sc is
+// a wave-uniform running power-of-two scale for G, lowered (and acc rescaled, exactly) when a unit's G
+// is larger than any before it, so G sc stays below 2^12. The bias gradient (sum of G) is summed
+// unscaled in ECL registers by the caller.
 // exact: A beyond the fp16 range (a diverged rollout) -> the f32 MFMA form for this unit.
 // max |x| over a lane's 16 values as a tree (v_max3), not a 16-long dependent chain
 __device__ __forceinline__ float amax16(const f4 (&x)[4]) {
@@ -467,15 +557,13 @@ __device__ __forceinline__ float amax16(const f4 (&x)[4]) {
     m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
   return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
 }
-// cm: col_max(amax16(G)), shared with the transposed product of the same G (mm64_cs)
-__device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], float& sc, const f4 (&G)[4],
-                                          const f4 (&A)[4], float* tile, int g, int e, bool exact, float cm) {
-  // G goes to the transpose tile unscaled, so the wave-wide max / scale below runs beside the LDS
-  // round trip instead of before it; the scale is applied to the transposed values
-  float* tG = tile;
-  float* tA = tile + 16 * ROWT;
-  store_ecl(tG + e * ROWT, G, g);
-  store_ecl(tA + e * ROWT, A, g);
+// channel held by image column 16 t + i (see the pair path below)
+__device__ __forceinline__ int chan_img(int t, int i) {
+  const int s = t >> 1, g = 2 * (t & 1) + (i >> 3), j = i & 7;
+  return 16 * (2 * s + (j >> 2)) + 4 * g + (j & 3);
+}
+// running-scale update shared by both weight-gradient forms: cm = col_max of this step's G
+__device__ __forceinline__ void wgrad_rescale(f4 (&acc)[4][4], float& sc, float cm) {
   const float m = row_max16(cm);
   const float mu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m)));
   if (mu > 0.f) {
@@ -483,26 +571,44 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
     if (su < sc) {
       const float r = su / sc;
 #pragma unroll
-      for (int ot = 0; ot < 4; ++ot) {
-        bsum[ot] *= r;
+      for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
         for (int it = 0; it < 4; ++it) acc[ot][it] *= r;
-      }
       sc = su;
     }
   }
+}
+// cm: col_max(amax16(G)), shared with the transposed product of the same G (mm64_cs)
+// AG: the accumulators live in AGPRs (pass A: the asm blocks above, as the pair path); else builtins
+template <bool AG>
+__device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float& sc, const f4 (&G)[4], const f4 (&A)[4],
+                                          float* tile, int g, int e, bool exact, float cm) {
+  // G goes to the transpose tile unscaled, so the wave-wide max / scale below runs beside the LDS
+  // round trip instead of before it; the scale is applied to the transposed values
+  float* tG = tile;
+  float* tA = tile + 16 * ROWT;
+  store_ecl(tG + e * ROWT, G, g);
+  store_ecl(tA + e * ROWT, A, g);
+  wgrad_rescale(acc, sc, cm);
   __builtin_amdgcn_wave_barrier();
+  int ce[4];   // this lane's channel of image column 16 t + e
+#pragma unroll
+  for (int t = 0; t < 4; ++t) ce[t] = chan_img(t, e);
   if (__builtin_expect(exact, 0)) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const int row = (4 * g + ks) * ROWT + e;
+      const int row = (4 * g + ks) * ROWT;
       float gv[4], av[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { gv[t] = tG[row + 16 * t] * sc; av[t] = tA[row + 16 * t]; bsum[t] += gv[t]; }
+      for (int t = 0; t < 4; ++t) { gv[t] = tG[row + ce[t]] * sc; av[t] = tA[row + ce[t]]; }
+      if constexpr (AG) {
+        amfma4_block(acc, gv, av);
+      } else {
 #pragma unroll
-      for (int ot = 0; ot < 4; ++ot)
+        for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
-        for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ot], av[it], acc[ot][it]);
+          for (int it = 0; it < 4; ++it) acc[ot][it] = mfma(gv[ot], av[it], acc[ot][it]);
+      }
     }
     __builtin_amdgcn_wave_barrier();
     return;
@@ -513,25 +619,145 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float (&bsum)[4], flo
   for (int it = 0; it < 4; ++it) {
     f4 v;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) v[ks] = tA[(4 * g + ks) * ROWT + e + 16 * it];
+    for (int ks = 0; ks < 4; ++ks) v[ks] = tA[(4 * g + ks) * ROWT + ce[it]];
     h4_split(v, ah[it], al[it]);
   }
 #pragma unroll
   for (int ot = 0; ot < 4; ++ot) {
     f4 v;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) v[ks] = tG[(4 * g + ks) * ROWT + e + 16 * ot] * sc;
-    bsum[ot] += (v[0] + v[1]) + (v[2] + v[3]);
+    for (int ks = 0; ks < 4; ++ks) v[ks] = tG[(4 * g + ks) * ROWT + ce[ot]] * sc;
     h4 gh, gl;
     h4_split(v, gh, gl);
+    if constexpr (AG) {
+      amfma16_block(acc[ot], gl, gh, ah, al);   // G_lo A_hi + G_hi A_lo + G_hi A_hi
+    } else {
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      acc[ot][it] = mfma16k16(gl, ah[it], acc[ot][it]);
-      acc[ot][it] = mfma16k16(gh, al[it], acc[ot][it]);
-      acc[ot][it] = mfma16k16(gh, ah[it], acc[ot][it]);
+      for (int it = 0; it < 4; ++it) {
+        acc[ot][it] = mfma16k16(gl, ah[it], acc[ot][it]);
+        acc[ot][it] = mfma16k16(gh, al[it], acc[ot][it]);
+        acc[ot][it] = mfma16k16(gh, ah[it], acc[ot][it]);
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();
+}
+
+// ---- two units at a time (pair path): K = 32 weight-gradient MFMAs from fp16 LDS images ----------
+// A pair's two 16-edge units are the 32 rows (edges) of an fp16 image [edge][64 channels], one image for
+// the hi and one for the lo parts (4 KB each, per wave). Lane (e, g) writes the 8 halves of its h8
+// hi[s] / lo[s] split (channels 16 (2s + (j >> 2)) + 4g + (j & 3), j = 0..7) as one 16-byte chunk at
+// image column 32s + 8g: image column 16t + i therefore holds channel chan_img(t, i) below. The tile is
+// read back transposed with ds_read_b64_tr_b16 (16 lanes: 4 edges x 16 image columns, column i to lane
+// i), which gives the K = 32 operands of v_mfma_f32_16x16x32_f16 directly: lane l supplies edges
+// 8 (l >> 4) .. + 7 of image column 16t + (l & 15). The weight gradient is therefore accumulated in
+// image-column order on both axes and un-permuted when it is written out (put_pair).
+// Chunks are XOR-swizzled per row (chunk ^ img_swz(row)): conflict-free transposed reads and 2-way
+// b128 writes (the minimum for 16 lanes x 16 bytes on 32 banks).
+constexpr int IMG_HALVES = 32 * 64;   // one image (hi or lo): 32 rows x 64 halves
+__device__ __forceinline__ int img_swz(int r) { return (((r >> 1) & 1) << 1) ^ ((r >> 2) & 1) ^ (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int img_off(int r, int chunk) { return r * 64 + 8 * (chunk ^ img_swz(r)); }   // halves
+typedef short s4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h8 tr_read8(const _Float16* img, int t, int lane) {
+  // lane 4q + p of group gq reads row 8 gq + q (+ 4), image columns 16 t + 4p .. + 3
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = 16 * t + 4 * p;                     // image column of the 4 halves
+  const int r0 = 8 * gq + q, r1 = r0 + 4;
+  const _Float16* a0 = img + img_off(r0, c >> 3) + (c & 7);
+  const _Float16* a1 = img + img_off(r1, c >> 3) + (c & 7);
+  const s4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+  const s4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a1));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  const s8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(h8, v);
+}
+// lane (e, g) writes its split of unit `u` (rows 16 u + e)
+__device__ __forceinline__ void img_put(_Float16* hi_img, _Float16* lo_img, const h8 (&hi)[2], const h8 (&lo)[2],
+                                        int u, int e, int g) {
+  const int r = 16 * u + e;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    *reinterpret_cast<h8*>(hi_img + img_off(r, 4 * s + g)) = hi[s];
+    *reinterpret_cast<h8*>(lo_img + img_off(r, 4 * s + g)) = lo[s];
+  }
+}
+// accP[ot][it] += sum over the pair's 32 edges of G[e] (x) A[e] in image-column order (lane (i, g) of
+// accP[ot][it][q] = dW[chan_img(ot, 4g + q)][chan_img(it, i)]), fp16x3 on v_mfma_f32_16x16x32_f16.
+// A: the pair's activations, already split (the forward product's split); G: the pair's gradients,
+// multiplied by the wave-uniform running scale sc here and split. img: this wave's 8 KB (hi | lo).
+__device__ __forceinline__ void wgrad_pair(f4 (&acc)[4][4], float& sc, const f4 (&G0)[4], const f4 (&G1)[4],
+                                           const h8 (&a0h)[2], const h8 (&a0l)[2], const h8 (&a1h)[2],
+                                           const h8 (&a1l)[2], _Float16* img, int e, int g, int lane, float cm) {
+  _Float16* ih = img;
+  _Float16* il = img + IMG_HALVES;
+  img_put(ih, il, a0h, a0l, 0, e, g);
+  img_put(ih, il, a1h, a1l, 1, e, g);
+  // wave-uniform running scale (as wgrad_h16): cm is the larger of the two units' column maxima
+  wgrad_rescale(acc, sc, cm);
+  __builtin_amdgcn_wave_barrier();
+  h8 bh[4], bl[4];   // B operand (activations) fragments, image columns 16 it + (lane & 15)
+#pragma unroll
+  for (int it = 0; it < 4; ++it) { bh[it] = tr_read8(ih, it, lane); bl[it] = tr_read8(il, it, lane); }
+  // the G image overwrites the A image: every lane's A reads were issued before (LDS is in order per wave)
+  __builtin_amdgcn_wave_barrier();
+  {
+    f4 gs[4];
+    h8 gh[2], gl[2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) gs[mt] = G0[mt] * sc;
+    h16_split(gs, gh, gl);
+    img_put(ih, il, gh, gl, 0, e, g);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) gs[mt] = G1[mt] * sc;
+    h16_split(gs, gh, gl);
+    img_put(ih, il, gh, gl, 1, e, g);
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int ot = 0; ot < 4; ++ot) {
+    const h8 ah = tr_read8(ih, ot, lane), al = tr_read8(il, ot, lane);
+    amfma32_block(acc[ot], al, ah, bh, bl);   // G_lo A_hi + G_hi A_lo + G_hi A_hi
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+// two units through one LDS-resident fp16x3 matrix: each fragment read feeds both units' MFMAs
+__device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
+                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2], int lane,
+                                           unsigned us) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    h8 ah[4], al[4];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
+      al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
+    }
+    const h8 x0s = h8_scale(x0h[s], us), x1s = h8_scale(x1h[s], us);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1h[s], acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(al[mo], x0s, acc0[mo]); acc1[mo] = mfma16(al[mo], x1s, acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1l[s], acc1[mo]); }
+  }
+}
+// out0/1 += W x0/1 for two gradient column sets, each column scaled to [2^11, 2^12) before the split
+// (mm64_cs for two units sharing the fragment reads)
+__device__ __forceinline__ void mm64_cs2(f4 (&out0)[4], f4 (&out1)[4], const h8* wh, const f4 (&x0)[4],
+                                         const f4 (&x1)[4], int lane, unsigned us, float cm0, float cm1) {
+  const float sc0 = p2scale(cm0), sc1 = p2scale(cm1);
+  const float inv0 = 1.f / sc0, inv1 = 1.f / sc1;   // exact (powers of two)
+  f4 xs[4], acc0[4], acc1[4];
+  h8 x0h[2], x0l[2], x1h[2], x1l[2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { xs[mt] = x0[mt] * sc0; acc0[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
+  h16_split(xs, x0h, x0l);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { xs[mt] = x1[mt] * sc1; acc1[mt] = f4{0.f, 0.f, 0.f, 0.f}; }
+  h16_split(xs, x1h, x1l);
+  mfma_h16x2(acc0, acc1, wh, x0h, x0l, x1h, x1l, lane, us);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) { out0[mt] += acc0[mt] * inv0; out1[mt] += acc1[mt] * inv1; }
 }
 
 // dst[o] = sum of the block's four wave partials (LDS, EW_STRIDE apart) for o in [o0, o1)
@@ -562,6 +788,8 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int NW = 4;
   constexpr int NF = 1 + NE;   // scalar inputs of edge W1: |r|^2, e_0 .. e_{NE-1}
+  // two units per iteration (the pair loops below; else one unit at a time throughout)
+  constexpr bool PAIRS = PASS == 0 ? NONODE_PAIR_A != 0 : NONODE_PAIR_B != 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
   const int rows = p.ct * 16;
@@ -600,7 +828,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   const h8* hW2T = reinterpret_cast<const h8*>(sH);
   const h8* hWc1T = reinterpret_cast<const h8*>(sH + 8192);   // pass A only
   float scW = 0x1p112f;   // running scale of the accW / sB sums (wgrad_h16)
-  f4 accW[4][4];   // PASS 0: dWc1, PASS 1: dW2
+  f4 accW[4][4];   // PASS 0: dWc1 (AGPRs in the pair path: amfma32_block), PASS 1: dW2
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -612,7 +840,8 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
 #pragma unroll
   for (int f = 0; f < NF; ++f) zero4(accFe[f]);
   zero4(sWC2);
-  float sB[4] = {0.f, 0.f, 0.f, 0.f};   // PASS 0: dbc1, PASS 1: db2
+  f4 bsE[4];   // PASS 0: dbc1, PASS 1: db2, per lane in ECL (summed over the lane group's edges at the end)
+  zero4(bsE);
   float sGC = 0.f;
   const int G = gridDim.x;
   const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;
@@ -742,22 +971,10 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         cn = p.stash_c[su + e];
       }
     };
-    if (U > 0) prefetch(wave < U ? wave : U - 1);
-    for (int u = wave; u < U; u += NW) {
-      // the weight fragments are loop-invariant: without this barrier the compiler hoists all four
-      // 64x64 matrices (256 VGPRs) out of the loop and spills
-      asm volatile("" ::: "memory");
-      float fe_in[NE > 0 ? NE : 1];
-#pragma unroll
-      for (int kk = 0; kk < NE; ++kk) fe_in[kk] = efn[kk];
-      f4 gz_in[4];
-      float c_in = 0.f;
-      if constexpr (PASS == 1) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) gz_in[mt] = gzn[mt];
-        c_in = cn;
-      }
-      prefetch(u + NW < U ? u + NW : u);
+    constexpr int NEP = NE > 0 ? NE : 1;
+    // one unit (16 edges) through the whole reverse pass of this PASS (the single-unit form: every
+    // unit of pass B, pass A's odd last unit and its pairs whose activations leave the fp16 range)
+    auto unit_one = [&](int u, const float (&fe_in)[NEP], const f4 (&gz_in)[4], float c_in) __attribute__((always_inline)) {
       const int tau = u / Nm1, k = u - tau * Nm1 + 1;
       const int rl = 16 * tau + e;
       const int r = rbase + rl;
@@ -876,7 +1093,9 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           f4 m[4];
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt] * sg2[mt];
-          wgrad_h16(accW, sB, scW, gz3, m, tile, g, e, bigM, cm3);
+          wgrad_h16<PAIRS>(accW, scW, gz3, m, tile, g, e, bigM, cm3);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) bsE[mt] += gz3[mt];
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
@@ -896,7 +1115,7 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           if (g == 0) p.stash_c[sunit + e] = c;
         }
         STAMP(4);
-        continue;
+        return;
       } else {
         f4 a[4];
         STAMP(0);
@@ -922,7 +1141,9 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         f4 a[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
-        wgrad_h16(accW, sB, scW, gz2, a, tile, g, e, bigA, cm2);
+        wgrad_h16<PAIRS>(accW, scW, gz2, a, tile, g, e, bigA, cm2);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) bsE[mt] += gz2[mt];
       }
       STAMP(5);
       f4 gz1[4];
@@ -965,6 +1186,392 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         }
       }
       STAMP(7);
+    };
+    // ---- shared by both passes' two-unit loops ----
+    struct UnitGeo {
+      int rl, sl, tau;   // receiver row (chunk), sender row (chunk tables), tile
+      bool rv;           // receiver row in range
+      float q0, q1, q2;  // r = x_r - x_s
+      float s2;          // |r|^2
+      float fe[NF];      // scalar edge inputs [|r|^2 (or its normalisation), e ...]
+      size_t su;         // handoff block
+    };
+    auto load_ef = [&](int uu, float (&dst)[NEP]) __attribute__((always_inline)) {
+      const float* ep;
+      size_t su;
+      unit_src(uu, ep, su);
+#pragma unroll
+      for (int kk = 0; kk < NE; ++kk) dst[kk] = ep[kk];
+    };
+    // z1 = P_r + Q_s + W1[:, s|e] [s, e] of unit uu, and its geometry
+    auto head_u = [&](int uu, const float (&fin)[NEP], f4 (&z1)[4], UnitGeo& o) __attribute__((always_inline)) {
+      const int tau = uu / Nm1, k = uu - tau * Nm1 + 1;
+      const int rl = 16 * tau + e;
+      const int r = rbase + rl;
+      const bool rvalid = r < nend;
+      const int rc = rvalid ? r : nend - 1;
+      const int gr = rc / N, n = rc - gr * N;
+      int j = n + k;
+      j = (j >= N) ? j - N : j;
+      const int sb = gr * N - s0;
+      const int sl = sb + j, rls = sb + n;
+      o.q0 = sX[rls * 4 + 0] - sX[sl * 4 + 0];
+      o.q1 = sX[rls * 4 + 1] - sX[sl * 4 + 1];
+      o.q2 = sX[rls * 4 + 2] - sX[sl * 4 + 2];
+      const float s2 = fmaf(o.q0, o.q0, fmaf(o.q1, o.q1, o.q2 * o.q2));
+      o.s2 = s2;
+      o.fe[0] = s2;
+      if constexpr (rnorm) o.fe[0] = radial_norm(s2);
+#pragma unroll
+      for (int kk = 0; kk < NE; ++kk) o.fe[1 + kk] = fin[kk];
+      float ev[2];
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf) {
+        const int fi = 4 * kf + g;
+        ev[kf] = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < NF; ++kk) ev[kf] = (fi == kk) ? o.fe[kk] : ev[kf];
+      }
+      f4 q4[4];
+      load_ecl(z1, sP + rl * ROWP, g);
+      load_ecl(q4, sQ + sl * ROWP, g);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) z1[mt] += q4[mt];
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf) {
+        if (kf * 4 < NF) {
+          const f4 wf = *reinterpret_cast<const f4*>(sV + kf * 256 + lane * 4);
+#pragma unroll
+          for (int mo = 0; mo < 4; ++mo) z1[mo] = mfma(wf[mo], ev[kf], z1[mo]);
+        }
+      }
+      o.rl = rl;
+      o.sl = sl;
+      o.tau = tau;
+      o.rv = rvalid;
+      o.su = (size_t)(k - 1) * ((size_t)p.n_graphs * N + 16 * gridDim.x) + rbase + 16 * tau + 16 * blockIdx.x;
+    };
+    // dL/dr c-part gF masked (SEGNO: the per-edge clamp passes the gradient only where |r_d c| <= 100)
+    auto grad_f = [&](const UnitGeo& o, float c, float& f0, float& f1, float& f2) __attribute__((always_inline)) {
+      f0 = sGF[o.rl * 4 + 0]; f1 = sGF[o.rl * 4 + 1]; f2 = sGF[o.rl * 4 + 2];
+      if (segno) {
+        f0 = fabsf(o.q0 * c) <= 100.f ? f0 : 0.f;
+        f1 = fabsf(o.q1 * c) <= 100.f ? f1 : 0.f;
+        f2 = fabsf(o.q2 * c) <= 100.f ? f2 : 0.f;
+      }
+    };
+    // dL/dc of a unit (f = r c; tanh option)
+    auto grad_c = [&](const UnitGeo& o, float c) __attribute__((always_inline)) {
+      float f0, f1, f2;
+      grad_f(o, c, f0, f1, f2);
+      float gc = o.rv ? (f0 * o.q0 + f1 * o.q1 + f2 * o.q2) : 0.f;
+      if constexpr (ctanh) gc *= 1.f - c * c;
+      return gc;
+    };
+    int u_first = wave;
+    unsigned long long bigmask = 0;   // pass A: this wave's pairs (local index) left to the single-unit form
+    if constexpr (PASS == 0 && PAIRS) {
+      // ---- pass A, two units per iteration: units 2i and 2i + 1 of the chunk (any two units, possibly
+      // of two tiles), pair i on wave i % NW. Each LDS fragment read feeds both units' MFMAs, the
+      // two dependent chains interleave, and dWc1 takes the K = 32 form (wgrad_pair) with m's split
+      // from the forward Wc1 product as its operand. An odd last unit runs in the single-unit loop.
+      const int npair = U >> 1;   // <= 4 * 64 pairs per chunk (ct <= 8 tiles, N <= 32): bigmask below
+      u_first = ((U & 1) && wave == npair % NW) ? U - 1 : U;
+      _Float16* img = reinterpret_cast<_Float16*>(tile);
+      const unsigned us_w2 = h16_us(bb + BOFF_SCAL, BH_W2), us_wc1 = h16_us(bb + BOFF_SCAL, BH_WC1);
+      const unsigned us_wc1t = h16_us(bb + BOFF_SCAL, BH_WC1T);
+      const float* vB2 = sV + (BOFF_VEC - BOFF_FEAT) + BV_B2 * 64;
+      const float* vBC1 = sV + (BOFF_VEC - BOFF_FEAT) + BV_BC1 * 64;
+      const float* vWC2 = sV + (BOFF_VEC - BOFF_FEAT) + BV_WC2 * 64;
+      float fa[NEP], fb[NEP];
+      if (wave < npair) {
+        load_ef(2 * wave, fa);
+        load_ef(2 * wave + 1, fb);
+      }
+      for (int ip = wave; ip < npair; ip += NW) {
+        asm volatile("" ::: "memory");   // keep the fragment reads in the loop (see below)
+        float ea[NEP], eb[NEP];
+#pragma unroll
+        for (int kk = 0; kk < NEP; ++kk) { ea[kk] = fa[kk]; eb[kk] = fb[kk]; }
+        {
+          const int ipn = ip + NW < npair ? ip + NW : ip;
+          load_ef(2 * ipn, fa);
+          load_ef(2 * ipn + 1, fb);
+        }
+        f4 z1a[4], z1b[4];
+        UnitGeo ga, gb;
+        head_u(2 * ip, ea, z1a, ga);
+        head_u(2 * ip + 1, eb, z1b, gb);
+        STAMP(13);
+        // forward recompute: a = SiLU(z1); z2 = W2 a + b2; m = SiLU(z2); z3 = Wc1 m + bc1 (fp16x3; exact
+        // f32 MFMAs for a pair whose activations leave the fp16 range)
+        // a = SiLU(z1) (dead after its split: the fallback below recomputes it)
+        f4 z2a[4], z2b[4];
+        float amx;
+        {
+          h8 xah[2], xal[2], xbh[2], xbl[2];
+          silu_true(z1a);
+          silu_true(z1b);
+          amx = fmaxf(amax16(z1a), amax16(z1b));
+          h16_split(z1a, xah, xal);
+          h16_split(z1b, xbh, xbl);
+          load_vp(z2a, vB2, g);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) z2b[mt] = z2a[mt];
+          mfma_h16x2(z2a, z2b, hW2, xah, xal, xbh, xbl, lane, us_w2);
+        }
+        PAIR_FENCE();
+        // m = SiLU(z2); d2 = SiLU'(z2) kept for gz2
+        f4 d2a[4], d2b[4];
+        h8 mah[2], mal[2], mbh[2], mbl[2];   // m's split: the Wc1 product's B operand and dWc1's A operand
+        float mmx;
+        {
+          f4 ma[4], mb[4];
+          silu_dsilu(z2a, ma, d2a);
+          silu_dsilu(z2b, mb, d2b);
+          mmx = fmaxf(amax16(ma), amax16(mb));
+          h16_split(ma, mah, mal);
+          h16_split(mb, mbh, mbl);
+        }
+        f4 z3a[4], z3b[4];
+        load_vp(z3a, vBC1, g);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) z3b[mt] = z3a[mt];
+        mfma_h16x2(z3a, z3b, hWc1, mah, mal, mbh, mbl, lane, us_wc1);
+        PAIR_FENCE();
+        if (__builtin_expect(__any(fmaxf(amx, mmx) > H16_LIMIT), 0)) {
+          // an activation beyond the fp16 range (a diverged state): the pair is redone after the loop by
+          // the single-unit form, whose forward and weight gradient take exact f32 MFMAs there
+          bigmask |= 1ull << ((ip - wave) / NW);
+          continue;
+        }
+        // c1 = SiLU(z3), d3 = SiLU'(z3); c = wc2 . c1 + bc2
+        f4 c1a[4], c1b[4], d3a[4], d3b[4];
+        silu_dsilu(z3a, c1a, d3a);
+        silu_dsilu(z3b, c1b, d3b);
+        float ca = dot_vp(c1a, vWC2, g) + bc2, cb = dot_vp(c1b, vWC2, g) + bc2;
+        if constexpr (ctanh) { ca = tanhf(ca); cb = tanhf(cb); }
+        STAMP(2);
+        // reverse: gz3 = gc wc2 SiLU'(z3); dwc2 += gc c1; dbc2 += gc; dbc1 += gz3
+        const float gca = grad_c(ga, ca), gcb = grad_c(gb, cb);
+        f4 gz3a[4], gz3b[4];
+        load_vp(gz3a, vWC2, g);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          gz3b[mt] = gz3a[mt] * gcb * d3b[mt];
+          gz3a[mt] = gz3a[mt] * gca * d3a[mt];
+          sWC2[mt] += gca * c1a[mt];
+          sWC2[mt] += gcb * c1b[mt];
+          bsE[mt] += gz3a[mt];
+          bsE[mt] += gz3b[mt];
+        }
+        sGC += gca;
+        sGC += gcb;
+        const float cma = col_max(amax16(gz3a)), cmb = col_max(amax16(gz3b));
+        // dWc1 += gz3 (x) m over the pair's 32 edges (K = 32); first, so that m's split dies here
+        wgrad_pair(accW, scW, gz3a, gz3b, mah, mal, mbh, mbl, img, e, g, lane, fmaxf(cma, cmb));
+        STAMP(15);
+        PAIR_FENCE();
+        // z3 = Wc1 m + bc1: gm = Wc1^T gz3 + gM_r (M = sum_j m); gz2 = gm SiLU'(z2) -> pass B
+        f4 gz2a[4], gz2b[4];
+        load_ecl(gz2a, sGM + ga.rl * ROWP, g);
+        load_ecl(gz2b, sGM + gb.rl * ROWP, g);
+        if (!ga.rv) zero4(gz2a);
+        if (!gb.rv) zero4(gz2b);
+        mm64_cs2(gz2a, gz2b, hWc1T, gz3a, gz3b, lane, us_wc1t, cma, cmb);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) { gz2a[mt] *= d2a[mt]; gz2b[mt] *= d2b[mt]; }
+        STAMP(3);
+        PAIR_FENCE();
+        {   // the handoff blocks (rows past the range too: their slots lie inside the unit's block)
+          float* da = p.stash + ga.su * HID;
+          float* db = p.stash + gb.su * HID;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            *reinterpret_cast<f4*>(da + mt * 256 + e * 16 + 4 * g) = gz2a[mt];
+            *reinterpret_cast<f4*>(db + mt * 256 + e * 16 + 4 * g) = gz2b[mt];
+          }
+          if (g == 0) {
+            p.stash_c[ga.su + e] = ca;
+            p.stash_c[gb.su + e] = cb;
+          }
+        }
+        STAMP(4);
+        STAMP(15);
+      }
+    }
+    if constexpr (PASS == 1 && PAIRS) {
+      // ---- pass B, two units per iteration (as pass A): dW2 in the K = 32 form with a's split as its
+      // operand, W2^T gz2 for both units through shared fragment reads; the per-unit sums (scalar
+      // columns, GA / GB / GX tables) in unit order afterwards
+      const int npair = U >> 1;
+      u_first = ((U & 1) && wave == npair % NW) ? U - 1 : U;
+      _Float16* img = reinterpret_cast<_Float16*>(tile);
+      const unsigned us_w2t = h16_us(bb + BOFF_SCAL, BH_W2T);
+      const float* vWS = sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64;
+      auto load_h = [&](int uu, f4 (&gz)[4], float& c) __attribute__((always_inline)) {
+        const float* ep;
+        size_t su;
+        unit_src(uu, ep, su);
+        const float* sb16 = p.stash + su * HID;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) gz[mt] = *reinterpret_cast<const f4*>(sb16 + mt * 256 + e * 16 + 4 * g);
+        c = p.stash_c[su + e];
+      };
+      float fa[NEP], fb[NEP];
+      f4 gna[4], gnb[4];
+      float cna = 0.f, cnb = 0.f;
+      if (wave < npair) {
+        load_ef(2 * wave, fa);
+        load_ef(2 * wave + 1, fb);
+        load_h(2 * wave, gna, cna);
+        load_h(2 * wave + 1, gnb, cnb);
+      }
+      // per unit, in unit order: W1 scalar-column and |r|^2 gradients, r gradient, GA / GB / GX
+      auto finish = [&](const UnitGeo& o, const f4 (&gz1)[4], float c) __attribute__((always_inline)) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) accFe[f][mt] += o.fe[f] * gz1[mt];
+        float gs = dot_vp(gz1, vWS, g);
+        if constexpr (rnorm) gs = o.s2 < 1e-12f ? gs * 1e12f : 0.f;
+        float f0, f1, f2;
+        grad_f(o, c, f0, f1, f2);
+        const float gr0 = fmaf(2.f * gs, o.q0, c * f0);
+        const float gr1 = fmaf(2.f * gs, o.q1, c * f1);
+        const float gr2 = fmaf(2.f * gs, o.q2, c * f2);
+        if (o.tau != cur_tau) {   // wave-uniform
+          if (cur_tau >= 0) flush_ga(cur_tau);
+          cur_tau = o.tau;
+        }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) gaR[mt] += gz1[mt];
+        gxR0 += gr0;
+        gxR1 += gr1;
+        gxR2 += gr2;
+        if (o.rv) {
+          f4 t[4];
+          load_ecl(t, myGB + o.sl * ROWP, g);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
+          store_ecl(myGB + o.sl * ROWP, t, g);
+          if (g == 0) {
+            f4* xs = reinterpret_cast<f4*>(myGX + o.sl * 4);
+            *xs -= f4{gr0, gr1, gr2, 0.f};
+          }
+        }
+      };
+      for (int ip = wave; ip < npair; ip += NW) {
+        asm volatile("" ::: "memory");   // keep the fragment reads in the loop
+        float ea[NEP], eb[NEP];
+        f4 gz2a[4], gz2b[4];
+        const float ca = cna, cb = cnb;
+#pragma unroll
+        for (int kk = 0; kk < NEP; ++kk) { ea[kk] = fa[kk]; eb[kk] = fb[kk]; }
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) { gz2a[mt] = gna[mt]; gz2b[mt] = gnb[mt]; }
+        {
+          const int ipn = ip + NW < npair ? ip + NW : ip;
+          load_ef(2 * ipn, fa);
+          load_ef(2 * ipn + 1, fb);
+          load_h(2 * ipn, gna, cna);
+          load_h(2 * ipn + 1, gnb, cnb);
+        }
+        f4 z1a[4], z1b[4];
+        UnitGeo ga, gb;
+        head_u(2 * ip, ea, z1a, ga);
+        head_u(2 * ip + 1, eb, z1b, gb);
+        STAMP(0);
+        // a = SiLU(z1) (split: dW2's operand), d1 = SiLU'(z1)
+        f4 d1a[4], d1b[4];
+        h8 aah[2], aal[2], abh[2], abl[2];
+        float amx;
+        {
+          f4 aa[4], ab[4];
+          silu_dsilu(z1a, aa, d1a);
+          silu_dsilu(z1b, ab, d1b);
+          amx = fmaxf(amax16(aa), amax16(ab));
+          h16_split(aa, aah, aal);
+          h16_split(ab, abh, abl);
+        }
+        if (__builtin_expect(__any(amx > H16_LIMIT), 0)) {
+          // an activation beyond the fp16 range: redone after the loop by the single-unit form (exact f32)
+          bigmask |= 1ull << ((ip - wave) / NW);
+          continue;
+        }
+        if (!ga.rv) zero4(gz2a);   // zero gradient for receivers past the range
+        if (!gb.rv) zero4(gz2b);
+        STAMP(1);
+        const float cma = col_max(amax16(gz2a)), cmb = col_max(amax16(gz2b));
+        // dW2 += gz2 (x) a over the pair's 32 edges (K = 32); db2 += gz2
+        wgrad_pair(accW, scW, gz2a, gz2b, aah, aal, abh, abl, img, e, g, lane, fmaxf(cma, cmb));
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          bsE[mt] += gz2a[mt];
+          bsE[mt] += gz2b[mt];
+        }
+        STAMP(5);
+        PAIR_FENCE();
+        // gz1 = (W2^T gz2) SiLU'(z1)
+        f4 gz1a[4], gz1b[4];
+        zero4(gz1a);
+        zero4(gz1b);
+        mm64_cs2(gz1a, gz1b, hW2T, gz2a, gz2b, lane, us_w2t, cma, cmb);
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) { gz1a[mt] *= d1a[mt]; gz1b[mt] *= d1b[mt]; }
+        STAMP(6);
+        PAIR_FENCE();
+        finish(ga, gz1a, ca);
+        finish(gb, gz1b, cb);
+        STAMP(7);
+      }
+    }
+    if constexpr (PAIRS) {
+      // the single-unit form after the pair loop: the units of pairs flagged in bigmask, then the odd
+      // last unit
+      const int nbig = 2 * __builtin_popcountll(bigmask);
+      const int nrun = nbig + (u_first < U ? 1 : 0);
+      for (int t = 0; t < nrun; ++t) {
+        int uu = u_first;
+        if (t < nbig) {
+          unsigned long long mm = bigmask;
+          for (int b = 0; b < (t >> 1); ++b) mm &= mm - 1;
+          uu = 2 * (wave + NW * __builtin_ctzll(mm)) + (t & 1);
+        }
+        prefetch(uu);
+        float fe_in[NEP];
+#pragma unroll
+        for (int kk = 0; kk < NEP; ++kk) fe_in[kk] = efn[kk];
+        f4 gz_in[4];
+        float c_in = 0.f;
+        if constexpr (PASS == 1) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) gz_in[mt] = gzn[mt];
+          c_in = cn;
+        } else {
+          zero4(gz_in);
+        }
+        unit_one(uu, fe_in, gz_in, c_in);
+      }
+    } else {
+      if (u_first < U) prefetch(u_first);
+      for (int u = u_first; u < U; u += NW) {
+        // the weight fragments are loop-invariant: without this barrier the compiler hoists all four
+        // 64x64 matrices (256 VGPRs) out of the loop and spills
+        asm volatile("" ::: "memory");
+        float fe_in[NEP];
+#pragma unroll
+        for (int kk = 0; kk < NEP; ++kk) fe_in[kk] = efn[kk];
+        f4 gz_in[4];
+        float c_in = 0.f;
+        if constexpr (PASS == 1) {
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) gz_in[mt] = gzn[mt];
+          c_in = cn;
+        }
+        prefetch(u + NW < U ? u + NW : u);
+        unit_one(u, fe_in, gz_in, c_in);
+      }
     }
     if (PASS == 1 && cur_tau >= 0) flush_ga(cur_tau);
     STAMP(PASS ? 7 : 15);
@@ -996,21 +1603,26 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   // ---- D: weight-gradient partials: each wave's to LDS, then one per block (waves added in order) ----
   __syncthreads();   // the last chunk's tables are dead: reuse the LDS
   float* wp = smem + wave * EW_STRIDE;
-  auto put = [&](const f4 (&acc)[4][4], const float (&sb)[4], float sc, int wo) {
+  auto put = [&](const f4 (&acc)[4][4], const f4 (&bs)[4], float sc, int wo) {
     const float inv_sc = 1.f / sc;   // exact (power of two)
+    // acc is in image-column order on both axes (wgrad_h16 / wgrad_pair): un-permuted here
 #pragma unroll
     for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
       for (int it = 0; it < 4; ++it)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = acc[ot][it][q] * inv_sc;
+        for (int q = 0; q < 4; ++q)
+          wp[wo + chan_img(ot, 4 * g + q) * 65 + chan_img(it, e)] = acc[ot][it][q] * inv_sc;
+    // bias: lane (e, g) holds channel 16 mt + 4 g + q summed over its edges; add the 16 edges
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const float bs = group_sum(sb[t]) * inv_sc;
-      if (g == 0) wp[wo + (16 * t + e) * 65 + 64] = bs;
-    }
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float b = edge_sum16(bs[mt][q]);
+        if (e == 0) wp[wo + (16 * mt + 4 * g + q) * 65 + 64] = b;
+      }
   };
-  put(accW, sB, scW, PASS == 0 ? EW_WC1 : EW_W2);
+  put(accW, bsE, scW, PASS == 0 ? EW_WC1 : EW_W2);
   if (PASS == 1) {
 #pragma unroll
     for (int f = 0; f < NF; ++f)
@@ -1172,11 +1784,19 @@ struct TconvBwdArgs {
   const unsigned long long* mask;   // the forward's LeakyReLU decisions (TconvArgs::mask_out layout)
 };
 
+// LDS: sX [2 MM - 1][16][ROWP] (Xr_0, (Xr_m, Xs_m)), sG [2 MM][16][ROWP] ((gYr_m, gYi_m)), sCos / sSin
+// [MM * TMAX]: dynamic (83 KB at 5 modes, 152 KB at 9: beyond the 64 KB of static LDS)
+constexpr size_t tconv_bwd_lds_bytes(int MM) {
+  return ((size_t)(4 * MM - 1) * 16 * ROWP + 2 * (size_t)MM * TMAX) * sizeof(float);
+}
 template <int MM>
 __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
-  __shared__ __attribute__((aligned(16))) float sX[2 * MM - 1][16][ROWP];   // Xr_0, (Xr_m, Xs_m)
-  __shared__ __attribute__((aligned(16))) float sG[2 * MM][16][ROWP];       // (gYr_m, gYi_m)
-  __shared__ float sCos[MM * TMAX], sSin[MM * TMAX];
+  extern __shared__ __attribute__((aligned(16))) float tb_smem[];
+  typedef float Row[16][ROWP];
+  Row* sX = reinterpret_cast<Row*>(tb_smem);
+  Row* sG = sX + (2 * MM - 1);
+  float* sCos = reinterpret_cast<float*>(sG + 2 * MM);
+  float* sSin = sCos + MM * TMAX;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int T = p.T, BN = p.BN;
   if (tid < MM * T) {
@@ -1331,22 +1951,25 @@ __global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
 // the slices in order and writes g_tconvx [2][2][Mfull][2] whole (modes >= M zero), replacing a
 // memset and four copies
 __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int nb, int M, int Mfull, float* dst) {
-  __shared__ float red[8][33];
-  constexpr int cnt = 2 * 2 * MMAX_T * 2;
-  const int o = threadIdx.x & 31, lanei = threadIdx.x >> 5;
-  float s4[4] = {0.f, 0.f, 0.f, 0.f};   // independent sums: several partial rows in flight
-  for (int r = lanei; r < nb; r += 32)
+  constexpr int cnt = 2 * 2 * MMAX_T * 2;   // partial row length (72)
+  constexpr int NL = 256 / cnt;             // partial lanes per output (3)
+  __shared__ float red[NL][cnt];
+  const int o = threadIdx.x % cnt, lanei = threadIdx.x / cnt;
+  if (lanei < NL) {
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};   // independent sums: several partial rows in flight
+    for (int r = lanei; r < nb; r += 4 * NL)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (r + 8 * j < nb) s4[j] += part[(size_t)(r + 8 * j) * cnt + o];
-  red[lanei][o] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+      for (int j = 0; j < 4; ++j)
+        if (r + NL * j < nb) s4[j] += part[(size_t)(r + NL * j) * cnt + o];
+    red[lanei][o] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  }
   __syncthreads();
   for (int d = threadIdx.x; d < 4 * Mfull * 2; d += 256) {
     const int io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
     float v = 0.f;
     if (m < M) {
       const int k = (io * MMAX_T + m) * 2 + c;
-      for (int q = 0; q < 8; ++q) v += red[q][k];
+      for (int q = 0; q < NL; ++q) v += red[q][k];
     }
     dst[d] = v;
   }
@@ -1377,11 +2000,25 @@ __global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int
 }
 
 int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
+  auto go = [&](auto mm) {
+    constexpr int MM = decltype(mm)::value;
+    static std::once_flag once;
+    std::call_once(once, [] {
+      hipFuncSetAttribute((const void*)tconv_bwd_kernel<MM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)tconv_bwd_lds_bytes(MM));
+    });
+    hipLaunchKernelGGL(tconv_bwd_kernel<MM>, dim3(G), dim3(256), tconv_bwd_lds_bytes(MM), s, a);
+  };
   switch (M) {
-    case 1: hipLaunchKernelGGL(tconv_bwd_kernel<1>, dim3(G), dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(tconv_bwd_kernel<2>, dim3(G), dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL(tconv_bwd_kernel<3>, dim3(G), dim3(256), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(tconv_bwd_kernel<4>, dim3(G), dim3(256), 0, s, a); break;
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 3: go(std::integral_constant<int, 3>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 5: go(std::integral_constant<int, 5>{}); break;   // num_modes = 5 (model_confs.yaml:12)
+    case 6: go(std::integral_constant<int, 6>{}); break;
+    case 7: go(std::integral_constant<int, 7>{}); break;
+    case 8: go(std::integral_constant<int, 8>{}); break;
+    case 9: go(std::integral_constant<int, 9>{}); break;
     default: return fail(NONODE_EUNSUPPORTED, "tconv_bwd: modes=%d", M);
   }
   return check_launch("tconv_bwd_kernel");
@@ -1391,14 +2028,15 @@ int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
 // One thread per (column c, coordinate d); the block sums its threads' weight-gradient terms in a
 // fixed order and writes one row of 2*2*MMAX_T*2 partials (tconvx_grad_finish adds the blocks' rows).
 constexpr int TX_THREADS = 128;
+template <int MM>
 __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x,
                                                                 const float* v, const float* lm, const float* gxo,
                                                                 const float* gvo, const float* w, float* gx,
                                                                 float* gv, float* part, int frames) {
-  constexpr int CNT = 2 * 2 * MMAX_T * 2;
+  constexpr int CNT = 2 * 2 * MM * 2;   // this build's partials; the row written is [io][MMAX_T][2]
   // twiddles cos / sin(pi 2 m t / T) once per block in LDS (the same float values a per-thread double
   // cospi / sinpi gave; that software double trig per thread had made this kernel ~38 us at C4)
-  __shared__ float sCs[MMAX_T * TMAX], sSn[MMAX_T * TMAX];
+  __shared__ float sCs[MM * TMAX], sSn[MM * TMAX];
   __shared__ float red[TX_THREADS][CNT + 1];
   for (int i = threadIdx.x; i < M * T; i += blockDim.x) {
     const int m = i / T, t = i - m * T;
@@ -1423,7 +2061,7 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
       GO[1][t] = G[1][t] = gvo[row * 3 + d];
     }
 #pragma unroll
-    for (int m = 0; m < MMAX_T; ++m) {
+    for (int m = 0; m < MM; ++m) {
       if (m >= M) break;
       const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
       float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f}, gYr[2] = {0.f, 0.f}, gYi[2] = {0.f, 0.f};
@@ -1443,8 +2081,8 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
           const float wr = w[((i * 2 + o) * Mfull + m) * 2 + 0], wi = w[((i * 2 + o) * Mfull + m) * 2 + 1];
           gxr += gYr[o] * wr + gYi[o] * wi;
           gxi += -gYr[o] * wi + gYi[o] * wr;
-          pp[((i * 2 + o) * MMAX_T + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
-          pp[((i * 2 + o) * MMAX_T + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
+          pp[((i * 2 + o) * MM + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
+          pp[((i * 2 + o) * MM + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
         }
         for (int t = 0; t < T; ++t) G[i][t] += gxr * sCs[m * TMAX + t] - gxi * sSn[m * TMAX + t];
       }
@@ -1461,7 +2099,8 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
   if (threadIdx.x < CNT) {
     float acc = 0.f;
     for (int r = 0; r < TX_THREADS; ++r) acc += red[r][threadIdx.x];
-    part[(size_t)blockIdx.x * CNT + threadIdx.x] = acc;
+    const int io = threadIdx.x / (MM * 2), rest = threadIdx.x - io * (MM * 2);   // rest = 2 m + c
+    part[(size_t)blockIdx.x * (2 * 2 * MMAX_T * 2) + io * (MMAX_T * 2) + rest] = acc;
   }
 }
 
@@ -2024,7 +2663,9 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   const int BN = r.BN, T = r.T, M = r.M, modes = r.modes;
   // g_txw [2][2][Mfull][2]: one partial row per tconvx block, added in block order (modes >= M zero)
   const int nbx = (BN * 3 + TX_THREADS - 1) / TX_THREADS;
-  hipLaunchKernelGGL(tconvx_bwd_kernel, dim3(nbx), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
+  // mode-bound builds: 2 (C4), 4, 9 (registers of the per-thread partials)
+  auto txk = M <= 2 ? tconvx_bwd_kernel<2> : (M <= 4 ? tconvx_bwd_kernel<4> : tconvx_bwd_kernel<MMAX_T>);
+  hipLaunchKernelGGL(txk, dim3(nbx), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
                      r.lm, r.gx, r.gv, r.txw, r.g_xin, r.g_vin, w.xpart, r.frames);
   if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
   hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, w.xpart, nbx, M, modes, r.g_txw);

@@ -24,7 +24,8 @@ What each fixture pins (reference file:line):
                       through forward_step (the integrator the shadowed forward intends).
   segno_gravity.npz   forward_step at N=100, B=2, T=5 on GravitySim-style inputs
                       (synthetic_sim.py:360-404).
-  egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8 (5 spectral modes incl. the
+  egno_m5.npz         EGNO.forward with num_modes=5, num_timesteps=8, and one training step's loss and
+                      gradients there (5 spectral modes incl. the
                       Nyquist bin; model_confs.yaml:12's alternative), seed-0 weights.
   egno_multi.npz      EGNO.forward with num_inputs=3 (multi-input branch, egno.py:44-96), seed-0 weights,
                       and one training step's parameter gradients; egno_multi_rollout.npz: its
@@ -419,6 +420,22 @@ def make_egno_modes(B=2, N=5, T=8, modes=5):
         "in::row": _np(edges[0]), "in::col": _np(edges[1]), "in::t_out": _np(t_out),
         "out::x": _np(x_out), "out::v": _np(v_out), "out::h": _np(h_out),
     })
+    # one training step's gradients at this configuration (main_simulation_simple_no.py:267-280, as
+    # make_egno): the reverse of TimeConv / TimeConv_x at 5 modes
+    model.train()
+    model.zero_grad()
+    loc_true = torch.tensor(loc_all[:, start + 1:start + 1 + T]).transpose(1, 2)  # [B,N,T,3]
+    crit = torch.nn.MSELoss(reduction="none")
+    loc_pred, _, _ = model(loc_p, nodes, edges, edge_attr, v=vel_p, loc_mean=loc_mean, timesteps_out=t_out)
+    loc_pred = loc_pred.reshape(T, -1, 3).transpose(0, 1)
+    loc_pred = _to_dense_batch(loc_pred, torch.arange(B).repeat_interleave(N))[0]
+    losses = crit(loc_pred, loc_true[:, :, :loc_pred.size(2)]).mean((0, 1, 3))
+    loss = losses.mean()
+    loss.backward()
+    fx.update({"grad::" + k: (_np(p.grad) if p.grad is not None else np.zeros(tuple(p.shape), np.float32))
+               for k, p in model.named_parameters()})
+    fx["out::loss"] = _np(loss)
+    fx["in::loc_true"] = _np(loc_true)
     np.savez_compressed(os.path.join(HERE, "egno_m5.npz"), **fx)
 
 

@@ -106,7 +106,7 @@ def test_rccl_world1_flatgrads_barrier_and_scalar_reductions(tmp_path):
     res = json.load(open(path))
     print("rccl:", res)
     assert res["ok"] and res["backend"] == "nccl" and res["world"] == 1
-    assert res["flat_device"].startswith("cuda") and res["flat_nonzero"] > 0.9 * res["flat_numel"]
+    assert res["flat_device"].startswith("cuda") and res["flat_nonzero"] > 0.5 * res["flat_numel"]
     assert res["flat_bitwise_unchanged"] and res["grads_are_views"]
     assert res["max_device"] == 3.25 and res["sum_device"] == 1.5 and res["max_over_ranks"] == 2.0
     assert res["allreduce_values_unchanged"]

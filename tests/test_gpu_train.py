@@ -189,3 +189,61 @@ def test_egno_c4_shard_gradients_match_f64_reference():
             assert q.grad is None or float(q.grad.abs().max()) == 0, k
         else:
             check_rel(f"C4 shard grad {k}", q.grad, ref, GTOL_F64)
+
+
+def test_egno_five_mode_gradients_match_reference_golden():
+    """num_modes = 5 (model_confs.yaml:12's alternative) at num_timesteps = 8: 5 spectral modes incl.
+    the Nyquist bin through the TimeConv / TimeConv_x reverse (tconv_bwd_kernel<5>,
+    tconvx_bwd_kernel<9>), against the reference's autograd gradients of one training step
+    (tests/golden/egno_m5.npz, seed-0 weights)."""
+    fx = load_golden("egno_m5")
+    B, N, T, modes = (int(fx[f"cfg::{k}"]) for k in ("B", "N", "T", "modes"))
+    m = _egno(T=T, modes=modes, seed=0)
+    for k, q in m.state_dict().items():   # the seed-0 initialisation is the fixture's
+        assert abs(float(q.double().sum()) - float(fx["wsum::" + k])) <= 1e-6 * max(1.0, abs(float(fx["wsum::" + k]))), k
+    inp = {k: _dev(fx["in::" + k]) for k in ("x", "h", "row", "col", "edge_attr", "v", "loc_mean", "t_out")}
+    inp["edge_fea"] = inp.pop("edge_attr")
+    loss, _, g, _ = _train_step_grads(m, inp, _dev(fx["in::loc_true"]), T, B, N)
+    assert abs(float(loss.detach()) - float(fx["out::loss"])) <= 1e-5 * abs(float(fx["out::loss"]))
+    for k, got in g.items():
+        ref = fx["grad::" + k]
+        if np.abs(ref).max() == 0:
+            assert got is None or np.abs(got).max() <= 1e-6, k
+        else:
+            check_rel(f"m5 grad {k}", got, ref, GTOL)
+
+
+def test_egno_five_mode_gradients_at_b512_match_f64_reference():
+    """num_modes = 5, T = 8 at the C4 shard size B = 512 (N = 20): every parameter gradient against
+    float64 torch autograd of the op-by-op restatement (oracle/torch_ref.py)."""
+    from oracle import torch_ref as tr
+    from tests.test_gpu_parity import _egno_full
+    B, N, T, modes = 512, 20, 8, 5
+    m = _egno(T=T, modes=modes, seed=31).train()
+    x, nodes, edges, ea, v, lm, t, _ = _egno_full(B, N, T, seed=32)
+    loc_true = torch.randn(B, N, T, 3, generator=torch.Generator().manual_seed(33))
+    m.zero_grad(set_to_none=True)
+    xo, _, _ = m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)
+    loss, _ = _loss_like_reference(xo, loc_true.to(x.device), T, B, N)
+    loss.backward()
+    torch.cuda.synchronize()
+    p = {k: q.detach().cpu().double().requires_grad_(True) for k, q in m.state_dict().items()}
+    r, c = tr.full_edges(B, N)
+    d = lambda a: a.detach().cpu().double()  # noqa: E731
+    xr, _, _ = tr.egno_forward(p, d(x), d(nodes), r, c, d(ea), d(v), d(lm), t.cpu(), T=T)
+    lr, _ = _loss_like_reference(xr, loc_true.double(), T, B, N)
+    lr.backward()
+    assert abs(float(loss.detach()) - float(lr.detach())) <= 1e-6 * abs(float(lr.detach()))
+    # the same autograd in fp32: the conditioning of each gradient at this size (the last layer's
+    # TimeConv weights sum ~1e5 LeakyReLU-gated products per element); bar = max(1e-5, 2x its error)
+    p32 = {k: q.detach().cpu().float().requires_grad_(True) for k, q in m.state_dict().items()}
+    f = lambda a: a.detach().cpu().float()  # noqa: E731
+    x32, _, _ = tr.egno_forward(p32, f(x), f(nodes), r, c, f(ea), f(v), f(lm), t.cpu(), T=T)
+    _loss_like_reference(x32, loc_true.float(), T, B, N)[0].backward()
+    for k, q in m.named_parameters():
+        ref = p[k].grad
+        if ref is None or float(ref.abs().max()) == 0:
+            assert q.grad is None or float(q.grad.abs().max()) == 0, k
+        else:
+            own = maxnorm_rel(p32[k].grad.numpy(), ref.numpy())
+            check_rel(f"m5 B=512 grad {k}", q.grad, ref, max(GTOL_F64, 2.0 * own))

@@ -194,6 +194,30 @@ def test_egno_five_modes_matches_reference():
     assert maxnorm_rel(h, fx["out::h"]) < TOL32
 
 
+def test_oracle_gradients_five_modes_match_reference_golden():
+    """The reverse pass at num_modes=5, num_timesteps=8 (model_confs.yaml:12's alternative: 5 spectral
+    modes incl. the Nyquist bin) against the reference's autograd gradients in egno_m5.npz."""
+    import torch
+    import no_node_comparison_amd as pkg
+    from oracle import egno_grad as og
+    fx = load_golden("egno_m5")
+    T, modes = int(fx["cfg::T"]), int(fx["cfg::modes"])
+    torch.manual_seed(0)
+    m = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=modes,
+                 num_timesteps=T, time_emb_dim=32)
+    p = {k: v.detach().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    i = lambda k: fx["in::" + k].astype(np.float64)  # noqa: E731
+    loss, _, g = og.egno_loss_and_grads(p, i("x"), i("h"), fx["in::row"], fx["in::col"], i("edge_attr"), i("v"),
+                                        i("loc_mean"), fx["in::t_out"], i("loc_true"), T=T)
+    assert abs(loss - float(fx["out::loss"])) <= 1e-5 * abs(float(fx["out::loss"]))
+    for k in p:
+        ref = fx["grad::" + k]
+        if np.abs(ref).max() == 0:
+            assert np.abs(g[k]).max() == 0, k
+        else:
+            assert maxnorm_rel(g[k], ref) < 2e-6, k
+
+
 def test_egno_multi_input_matches_reference():
     """num_inputs=3 (egno.py:44-96 multi-input branch): seed-0 initialisation of the drop-in equals
     the reference's (per-tensor sums), and the oracle's multi-input forward reproduces the
