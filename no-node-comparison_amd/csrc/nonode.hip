@@ -74,9 +74,23 @@ __device__ __forceinline__ float radial_norm(float s) {
   return s < 1e-12f ? s * 1e12f : (__builtin_isfinite(s) ? 1.f : s - s);
 }
 static_assert(OFF_SCAL + 64 == OFF_H16, "blob layout");
-constexpr int BLOB_FLOATS = OFF_H16N + H_COUNT * 4096;
+// The pair loop's 32-column form (v_mfma_f32_32x32x16_f16: both units of a pair in one MFMA column
+// set; lane l = 32 h + n holds column n (unit n >> 4, receiver n & 15) and, of a 64-channel activation,
+// channels 32 mo2 + 8 j4 + 4 h + q in register 4 (4 mo2 + j4) + q: the accumulator layout of the 32x32
+// MFMA, and, k-step s4 taking registers 8 s4 .. 8 s4 + 7, its next B operand):
+constexpr int OFF_H32 = OFF_H16N + H_COUNT * 4096;   // W2 | Wc1 hi/lo fragments [mat][s4][mo2][hl][lane][8 halves]:
+                                                     // half j of lane l = W[32 mo2 + (l & 31)][16 s4 + 8 (j >> 2) + 4 (l >> 5) + (j & 3)]
+constexpr int OFF_F32 = OFF_H32 + 8192;   // scalar-input columns [kk][mo2][lane] = W1[32 mo2 + (l & 31)][feature 2 kk + (l >> 5)]
+constexpr int OFF_V32 = OFF_F32 + 512;    // b2 | bc1 | wc2 [3][h][mo2][j4][q] (channel 32 mo2 + 8 j4 + 4 h + q)
+constexpr int BLOB_FLOATS = OFF_V32 + 256;
 constexpr float H16_LIMIT = 16384.f;   // |activation| above this takes the exact f32 MFMA path
 constexpr int EDGE_STAGE_FLOATS = 512 + 3 * 64;   // FEAT | b2 | bc1 | wc2 (contiguous) staged to LDS
+constexpr int EDGE_STAGE32 = 512 + 192;            // the 32-column form's F32 | V32 (contiguous in the blob)
+#ifndef NONODE_PAIR32
+// the pair loop in the 32-column form (v_mfma_f32_32x32x16_f16) where a tile is unpacked: correct (GPU
+// tests green) but slower (C2 layer 236 vs 216 us), so off
+#define NONODE_PAIR32 0
+#endif
 
 thread_local std::string g_err;
 
@@ -360,6 +374,130 @@ __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H
   }
 }
 
+// ---- the 32-column form of the pair loop (v_mfma_f32_32x32x16_f16, OFF_H32 layout) -------------
+// A pair's two units are the 32 columns of one MFMA: lane l = 32 h + n, n = 16 u + e (unit u, receiver
+// column e), h = lane half. A 64-channel activation is two 16-float accumulators x[mo2] (channels
+// 32 mo2 + 8 j4 + 4 h + q in element 4 j4 + q): the output layout of the 32x32 MFMA and, k-step s4 being
+// elements 8 (s4 & 1) .. + 7 of x[s4 >> 1], the B-operand layout of the next product. So one product is
+// 8 MFMAs per fp16x3 term for both units (the 16-column form issues 16), and a 64-channel dot product
+// is 32 lane-local FMAs and one lane-half swap.
+typedef float f16v __attribute__((ext_vector_type(16)));
+struct H32Frags {
+  h8 hi[4][2], lo[4][2];   // [s4][mo2]
+};
+__device__ __forceinline__ void load_h32frags(H32Frags& f, const h8* wf, int lane) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+    for (int mo2 = 0; mo2 < 2; ++mo2) {
+      f.hi[s4][mo2] = wf[((s4 * 2 + mo2) * 2 + 0) * 64 + lane];
+      f.lo[s4][mo2] = wf[((s4 * 2 + mo2) * 2 + 1) * 64 + lane];
+    }
+}
+__device__ __forceinline__ void pin_agpr32(H32Frags& f) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+    for (int mo2 = 0; mo2 < 2; ++mo2) {
+      asm volatile("" : "+a"(f.hi[s4][mo2]));
+      asm volatile("" : "+a"(f.lo[s4][mo2]));
+    }
+}
+__device__ __forceinline__ f16v mfma32x16(h8 a, h8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16v mfma32x2(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+// fp16 hi / lo split of a 32-column activation into its four k-steps
+__device__ __forceinline__ void h32_split(const f16v (&x)[2], h8 (&hi)[4], h8 (&lo)[4]) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const int mo2 = s4 >> 1, b = 8 * (s4 & 1);
+    const f8 v = {x[mo2][b + 0], x[mo2][b + 1], x[mo2][b + 2], x[mo2][b + 3],
+                  x[mo2][b + 4], x[mo2][b + 5], x[mo2][b + 6], x[mo2][b + 7]};
+    hi[s4] = __builtin_convertvector(v, h8);
+    const auto hw = __builtin_bit_cast(u4, hi[s4]);
+    f8 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      r[2 * i] = resid_lo(hw[i], v[2 * i]);
+      r[2 * i + 1] = resid_hi(hw[i], v[2 * i + 1]);
+    }
+    lo[s4] = __builtin_convertvector(r, h8);
+  }
+}
+// acc += W x (both units, fp16x3; the chain starts with W_hi x_hi, see mfma_h16)
+__device__ __forceinline__ void mfma_h32(f16v (&acc)[2], const H32Frags& f, const h8 (&xh)[4], const h8 (&xl)[4],
+                                         unsigned us) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const h8 xs = h8_scale(xh[s4], us);
+#pragma unroll
+    for (int mo2 = 0; mo2 < 2; ++mo2) acc[mo2] = mfma32x16(f.hi[s4][mo2], xh[s4], acc[mo2]);
+#pragma unroll
+    for (int mo2 = 0; mo2 < 2; ++mo2) acc[mo2] = mfma32x16(f.lo[s4][mo2], xs, acc[mo2]);
+#pragma unroll
+    for (int mo2 = 0; mo2 < 2; ++mo2) acc[mo2] = mfma32x16(f.hi[s4][mo2], xl[s4], acc[mo2]);
+  }
+}
+__device__ __forceinline__ void silu32(f16v (&x)[2]) {
+#pragma unroll
+  for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[mo2][i] = silu(x[mo2][i]);
+}
+// a 32-column vector (OFF_V32 layout: 32 floats per lane half) into both accumulators
+__device__ __forceinline__ void load_v32(f16v (&x)[2], const float* v32, int h) {
+#pragma unroll
+  for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const f4 t = *reinterpret_cast<const f4*>(v32 + 32 * h + 16 * mo2 + 4 * j4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[mo2][4 * j4 + q] = t[q];
+    }
+}
+// sum over the lane halves (lanes l, l ^ 32): the two halves of a column's 64 channels
+__device__ __forceinline__ float half_sum(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+__device__ __forceinline__ float half_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+}
+// sum over the two units of a receiver (lanes l, l ^ 16)
+__device__ __forceinline__ float unit_sum(float v) {
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+// acc += W x with every column scaled by 2^-s (s: the smallest shift bringing its largest |value| below
+// 2^13) around the fp16x3 product: the guard path (as mm64_scaled)
+__device__ __forceinline__ void mm32_scaled(f16v (&acc)[2], const H32Frags& f, const f16v (&x)[2], unsigned us) {
+  float m = 0.f;
+#pragma unroll
+  for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, fabsf(x[mo2][i]));
+  const float cmax = half_max(m);
+  const int s = max(__builtin_amdgcn_frexp_expf(cmax) - 13, 0);
+  const float dn = __uint_as_float((unsigned)(127 - s) << 23), up = __uint_as_float((unsigned)(127 + min(s, 127)) << 23);
+  f16v xs[2], t[2];
+#pragma unroll
+  for (int mo2 = 0; mo2 < 2; ++mo2) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { xs[mo2][i] = x[mo2][i] * dn; t[mo2][i] = 0.f; }
+  }
+  h8 xh[4], xl[4];
+  h32_split(xs, xh, xl);
+  mfma_h32(t, f, xh, xl, us);
+#pragma unroll
+  for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[mo2][i] += t[mo2][i] * up;
+}
+
 // f4 sum as four plain v_add_f32: the backend would emit two v_pk_add_f32, which cost more than the
 // plain ops they replace when issued beside MFMAs (MI355X_MICROARCH.md constants table)
 __device__ __forceinline__ f4 add4(f4 a, f4 b) {
@@ -604,6 +742,15 @@ __device__ __forceinline__ void pack_h16(_Float16* dst, const float* W, int d, i
   // fp16 subnormals)
   dst[d] = hl == 0 ? h : (_Float16)__builtin_ldexpf(w - (float)h, k);
 }
+// the 32-column form's fragments (OFF_H32 layout), lo part x 2^k as pack_h16
+__device__ __forceinline__ void pack_h32(_Float16* dst, const float* W, int d, int k) {
+  const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo2 = (d >> 10) & 1, s4 = d >> 11;
+  const int row = 32 * mo2 + (lane & 31);
+  const int col = 16 * s4 + 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3);
+  const float w = W[row * 64 + col];
+  const _Float16 h = (_Float16)w;
+  dst[d] = hl == 0 ? h : (_Float16)__builtin_ldexpf(w - (float)h, k);
+}
 // pack_h16 of one matrix and its shift (slot idx of the scalar table `scal`)
 __device__ __forceinline__ void pack_h16_shifted(_Float16* dst, float* scal, int idx, const float* W, int d,
                                                  int ld = 64, int col0 = 0, float scale = 1.f) {
@@ -621,6 +768,24 @@ __global__ void pack_kernel(PackArgs a) {
   switch (sec) {
     case 8: pack_h16_shifted(reinterpret_cast<_Float16*>(B + OFF_H16), S, HS_W2, a.w2, d); break;
     case 9: pack_h16_shifted(reinterpret_cast<_Float16*>(B + OFF_H16 + 4096), S, HS_WC1, a.cw1, d); break;
+    // the 32-column form of W2 / Wc1 (same lo shift as sections 8 / 9: the same reduction)
+    case 16: pack_h32(reinterpret_cast<_Float16*>(B + OFF_H32), a.w2, d, h16_lo_shift(a.w2, 64, 0, 1.f)); break;
+    case 17: pack_h32(reinterpret_cast<_Float16*>(B + OFF_H32 + 4096), a.cw1, d, h16_lo_shift(a.cw1, 64, 0, 1.f)); break;
+    case 18:
+      if (d < 512) {   // 32-column feature k-steps (x -log2e, as OFF_FEAT)
+        const int kk = d >> 7, mo2 = (d >> 6) & 1, l = d & 63;
+        const int row = 32 * mo2 + (l & 31), fi = 2 * kk + (l >> 5);
+        float val = 0.f;
+        if (fi == 0) val = a.w1[row * a.ld1 + a.colS];
+        else if (fi - 1 < a.ne) val = a.w1[row * a.ld1 + 2 * HID + 1 + (fi - 1)];
+        B[OFF_F32 + d] = val * NEG_LOG2E;
+      } else if (d < 512 + 192) {   // b2, bc1 (x -log2e), wc2 (x -ln2) in the 32-column lane order
+        const int dd = d - 512, v = dd >> 6, i = dd & 63;
+        const int h = i >> 5, mo2 = (i >> 4) & 1, j4 = (i >> 2) & 3, q = i & 3;
+        const int ch = 32 * mo2 + 8 * j4 + 4 * h + q;
+        B[OFF_V32 + dd] = v == 0 ? a.b2[ch] * NEG_LOG2E : (v == 1 ? a.cb1[ch] * NEG_LOG2E : a.cw2[ch] * NEG_LN2);
+      }
+      break;
     case 10: pack_h16_shifted(HN + H_WA * 8192, S, HS_N + H_WA, a.w1, d, a.ld1, a.colA, NEG_LOG2E); break;
     case 11: pack_h16_shifted(HN + H_WB * 8192, S, HS_N + H_WB, a.w1, d, a.ld1, a.colB, NEG_LOG2E); break;
     case 12: pack_h16_shifted(HN + H_WV1 * 8192, S, HS_N + H_WV1, a.vw1, d, 64, 0, NEG_LOG2E); break;
@@ -937,7 +1102,7 @@ struct LayerArgs {
 
 // LDS of one chunk: ct receiver tiles (P, two message-sum slots, two force-sum slots) and s_rows senders
 size_t layer_lds_floats(int ct, int s_rows, int keep = 0) {
-  return 8192 + EDGE_STAGE_FLOATS + (size_t)ct * 16 * ROWP * 3 + (size_t)s_rows * (ROWP + 4) +
+  return 8192 + EDGE_STAGE_FLOATS + EDGE_STAGE32 + (size_t)ct * 16 * ROWP * 3 + (size_t)s_rows * (ROWP + 4) +
          (size_t)ct * 16 * 4 * 2 + (keep ? (size_t)ct * 16 * (ROWP + 4) : 0);
 }
 
@@ -974,7 +1139,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   const int N = p.N, Nm1 = N - 1;
   float* sW = smem;                              // W2 | Wc1 fp16 hi/lo fragments (8192 floats)
   float* sV = sW + 8192;                         // feat k-steps (512) | b2 | bc1 | wc2 (vp order)
-  float* sP = sV + EDGE_STAGE_FLOATS;            // [ct*16][ROWP]
+  float* sV32 = sV + EDGE_STAGE_FLOATS;          // F32 (512) | V32 (192): the 32-column form's vectors
+  float* sP = sV32 + EDGE_STAGE32;               // [ct*16][ROWP]
   float* sQ = sP + p.ct * 16 * ROWP;             // [s_rows][ROWP]
   float* sX = sQ + p.s_rows * ROWP;              // [s_rows][4]
   float* sM = sX + p.s_rows * 4;                 // [2][ct*16][ROWP] message sums (slots 0 | 1)
@@ -988,6 +1154,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   for (int i = tid; i < 2048; i += NW * 64) reinterpret_cast<f4*>(sW)[i] = reinterpret_cast<const f4*>(p.blob + OFF_H16)[i];
   if (tid < EDGE_STAGE_FLOATS / 4)
     reinterpret_cast<f4*>(sV)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_FEAT)[tid];
+  if (tid < EDGE_STAGE32 / 4)
+    reinterpret_cast<f4*>(sV32)[tid] = reinterpret_cast<const f4*>(p.blob + OFF_F32)[tid];
   const float bc2 = p.blob[OFF_SCAL + 0];
   const float bv2 = p.blob[OFF_SCAL + 1];
   const unsigned us_w2 = h16_us(p.blob + OFF_SCAL, HS_W2), us_wc1 = h16_us(p.blob + OFF_SCAL, HS_WC1);
@@ -1306,7 +1474,183 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         const h8* w2h = reinterpret_cast<const h8*>(sW);
         const h8* wc1h = reinterpret_cast<const h8*>(sW + 4096);
         int k = k_lo;
-        if constexpr (PAIR) {
+        if constexpr (PAIR && NONODE_PAIR32) {
+          if (P == 1) {   // wave-uniform: an unpacked tile -> the 32-column pair loop
+            // Pairs (k, k + 1) as the 32 columns of v_mfma_f32_32x32x16_f16 (lane: unit u = lane bit 4,
+            // half h = lane >> 5); fragments in the OFF_H32 layout, pinned in AGPRs for the segment.
+            // The unit sums (message and force) are per lane until the segment's last pair, then folded
+            // into the 16-column accumulators msum / fs (unit_sum, lane-half exchange) that the
+            // single-unit loop and the flush use.
+            const int u = (lane >> 4) & 1, h = lane >> 5;
+            const float* v32 = sV32 + 512;   // b2 | bc1 | wc2, 64 floats each
+            H32Frags q2, qc1;
+            {
+              int off32 = 0;
+              asm volatile("" : "+v"(off32));   // loaded per segment (not hoisted to the chunk start)
+              const h8* w32 = reinterpret_cast<const h8*>(blob + OFF_H32 + off32);
+              load_h32frags(q2, w32, lane);
+              load_h32frags(qc1, w32 + 4096 / 4, lane);
+            }
+            pin_agpr32(q2);
+            pin_agpr32(qc1);
+            f4 pr32[2][4];   // receiver projection, fixed for the segment
+#pragma unroll
+            for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+              for (int j4 = 0; j4 < 4; ++j4)
+                pr32[mo2][j4] = *reinterpret_cast<const f4*>(Prow + 32 * mo2 + 8 * j4 + 4 * h);
+            constexpr int KK = 2 * KF;   // k-steps of two scalar features
+            int efl32[KK];
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) efl32[kk] = n * p.ne + min(max(2 * kk + h - 1, 0), p.ne - 1);
+            auto fetch32 = [&](int ku, float (&ev)[KK]) __attribute__((always_inline)) {
+              const int sub = (n + ku >= N) ? ne_wrap : p.ne;
+              const int kne = ku * p.ne;
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) ev[kk] = ef_seg[efl32[kk] + kne - sub];
+            };
+            auto head32 = [&](int ku, const float (&ev)[KK], f16v (&a)[2], float& r0, float& r1, float& r2,
+                              bool& ok) __attribute__((always_inline)) {
+              int j = n + ku;
+              j = (j >= N) ? j - N : j;
+              const int sl = sb + j;
+              const f4 xs = *reinterpret_cast<const f4*>(sX + sl * 4);
+              r0 = xr0 - xs[0]; r1 = xr1 - xs[1]; r2 = xr2 - xs[2];
+              float d2 = fmaf(r0, r0, fmaf(r1, r1, r2 * r2));
+              ok = xs[3] * xr3 != 0.f && __builtin_isfinite(d2);
+              if constexpr (rnorm) d2 = radial_norm(d2);
+#pragma unroll
+              for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+                for (int j4 = 0; j4 < 4; ++j4) {
+                  const f4 t = add4(*reinterpret_cast<const f4*>(sQ + sl * ROWP + 32 * mo2 + 8 * j4 + 4 * h),
+                                    pr32[mo2][j4]);
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) a[mo2][4 * j4 + q] = t[q];
+                }
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) {
+                const int fi = 2 * kk + h;
+                const float bv = (fi == 0) ? d2 : ((fi - 1 < p.ne) ? ev[kk] : 0.f);
+#pragma unroll
+                for (int mo2 = 0; mo2 < 2; ++mo2) a[mo2] = mfma32x2(sV32[kk * 128 + mo2 * 64 + lane], bv, a[mo2]);
+              }
+            };
+            f16v ms32[2];   // this lane's (unit, receiver, half) message sum over the segment's pairs
+#pragma unroll
+            for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) ms32[mo2][i] = 0.f;
+            float gs0 = 0.f, gs1 = 0.f, gs2 = 0.f;
+            float ev[KK];
+            fetch32(min(k + u, k_hi), ev);
+#pragma unroll 1
+            for (; k + 1 <= k_hi; k += 2) {
+              float evn[KK];
+              fetch32(min(k + 2 + u, k_hi), evn);
+              f16v a[2], m[2], c1[2];
+              float r0, r1, r2;
+              bool ok;
+              head32(k + u, ev, a, r0, r1, r2, ok);
+              STAMP(0);
+              silu32(a);
+              load_v32(m, v32, h);   // b2
+              {
+                h8 xh[4], xl[4];
+                h32_split(a, xh, xl);
+                mfma_h32(m, q2, xh, xl, us_w2);
+              }
+              STAMP(1);
+              silu32(m);
+              load_v32(c1, v32 + 64, h);   // bc1
+              {
+                h8 xh[4], xl[4];
+                h32_split(m, xh, xl);
+                mfma_h32(c1, qc1, xh, xl, us_wc1);
+              }
+              STAMP(2);
+              silu32(c1);
+              float c;
+              {
+                float d = 0.f;
+#pragma unroll
+                for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+                  for (int j4 = 0; j4 < 4; ++j4) {
+                    const f4 w = *reinterpret_cast<const f4*>(v32 + 128 + 32 * h + 16 * mo2 + 4 * j4);   // wc2
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) d = fmaf(c1[mo2][4 * j4 + q], w[q], d);
+                  }
+                c = half_sum(d) + bc2;   // the guard tests c before the tanh (tanh(inf) = 1)
+              }
+              if (__builtin_expect(__any(ok && !__builtin_isfinite(c)), 0)) {
+                // the guard (see the 16-column loop): the pair recomputed with column-scaled products
+                int kg = k;
+                asm volatile("" : "+v"(kg));
+                head32(kg + u, ev, a, r0, r1, r2, ok);
+                silu32(a);
+                load_v32(m, v32, h);
+                mm32_scaled(m, q2, a, us_w2);
+                silu32(m);
+                load_v32(c1, v32 + 64, h);
+                mm32_scaled(c1, qc1, m, us_wc1);
+                silu32(c1);
+                float d = 0.f;
+#pragma unroll
+                for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+                  for (int j4 = 0; j4 < 4; ++j4) {
+                    const f4 w = *reinterpret_cast<const f4*>(v32 + 128 + 32 * h + 16 * mo2 + 4 * j4);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) d = fmaf(c1[mo2][4 * j4 + q], w[q], d);
+                  }
+                c = half_sum(d) + bc2;
+              }
+              float ct = c;
+              if constexpr (ctanh) ct = tanhf(c);
+              float f0 = r0 * ct, f1 = r1 * ct, f2 = r2 * ct;
+              if (VARIANT == SEGNO) {   // gcl.py:99-100
+                f0 = fminf(fmaxf(f0, -100.f), 100.f);
+                f1 = fminf(fmaxf(f1, -100.f), 100.f);
+                f2 = fminf(fmaxf(f2, -100.f), 100.f);
+              }
+              gs0 += f0; gs1 += f1; gs2 += f2;
+#pragma unroll
+              for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+                for (int i = 0; i < 16; i += 4) {
+                  const f4 ms = {ms32[mo2][i], ms32[mo2][i + 1], ms32[mo2][i + 2], ms32[mo2][i + 3]};
+                  const f4 mm = {m[mo2][i], m[mo2][i + 1], m[mo2][i + 2], m[mo2][i + 3]};
+                  const f4 t = add4(ms, mm);
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) ms32[mo2][i + q] = t[q];
+                }
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk) ev[kk] = evn[kk];
+              STAMP(3);
+            }
+            // fold into the 16-column accumulators: units summed (lanes l, l ^ 16), then lane (e, g) of
+            // msum[mt][q] = channel 16 mt + 4 g + q from the half h = g & 1 holding it (lanes of g = 1 / 2
+            // read across the lane halves)
+#pragma unroll
+            for (int mo2 = 0; mo2 < 2; ++mo2)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) ms32[mo2][i] = unit_sum(ms32[mo2][i]);
+            fs0 += unit_sum(gs0); fs1 += unit_sum(gs1); fs2 += unit_sum(gs2);
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float x0 = ms32[mt >> 1][4 * (2 * (mt & 1)) + q];       // j4 even
+                const float x1 = ms32[mt >> 1][4 * (2 * (mt & 1) + 1) + q];   // j4 odd
+                const auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x0), false, false);
+                const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x1), __float_as_uint(x1), false, false);
+                const float v = g == 0 ? x0 : (g == 1 ? __uint_as_float(s0[1]) : (g == 2 ? __uint_as_float(s1[0]) : x1));
+                msum[mt][q] += v;
+              }
+          }
+        }
+        if constexpr (PAIR) if (!(NONODE_PAIR32 && P == 1)) {
           // Two units (32 edges, same receivers) per iteration. The hot body is ONE basic block:
           // both units always take the fp16x3 path while the largest |activation| is tracked, and
           // only if it exceeded the fp16 range (rare) is the pair recomputed on exact f32 MFMAs
@@ -2231,7 +2575,8 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   const int keep = fuse && layer_lds_floats(ct, s_rows, 1) * 4 <= LDS_MAX && !getenv_int("NONODE_NO_KEEP");
   size_t lds = layer_lds_floats(ct, s_rows, keep) * 4;
   if (tcf) {   // the fused TimeConv's tile (sX, twiddles) in the chunk tables' space
-    const size_t need = (8192 + EDGE_STAGE_FLOATS + (size_t)(2 * TCF_MM - 1) * 16 * ROWP + 2 * TCF_MM * TMAX) * 4;
+    const size_t need = (8192 + EDGE_STAGE_FLOATS + EDGE_STAGE32 + (size_t)(2 * TCF_MM - 1) * 16 * ROWP +
+                         2 * TCF_MM * TMAX) * 4;
     lds = lds > need ? lds : need;
   }
   LayerArgs a;
@@ -2349,7 +2694,7 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
   a.ne = n_edge_feat;
   a.flags = flags;
   a.blob = blob;
-  hipLaunchKernelGGL(pack_kernel, dim3(32, 16), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_kernel, dim3(32, 19), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_kernel");
 }
 
@@ -2466,9 +2811,10 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
     return NONODE_OK;
   }
   // fused TimeConv (TcFuse): sample-major layer launches that run their TimeConv first (2 modes,
-  // T <= 10, N < 64: the C2 configuration); NONODE_NO_TCFUSE=1 keeps the separate tconv launches
+  // T <= 10, N < 64: the C2 configuration), opt-in NONODE_TCFUSE=1: measured slower than the separate
+  // launches (C2 1.002 vs 0.939 ms)
   const int Me = effective_modes(T, modes);
-  if (Me <= TCF_MM && T <= TCF_TB && N < 64 && !getenv_int("NONODE_NO_TCFUSE")) {
+  if (Me <= TCF_MM && T <= TCF_TB && N < 64 && getenv_int("NONODE_TCFUSE")) {
     for (int l = 0; l < n_layers; ++l) {
       TcFuse f{};
       f.BN = BN; f.T = T; f.M = Me; f.Mfull = modes; f.frames = frames;

@@ -25,7 +25,7 @@ namespace {
 #define NONODE_PAIR_A 1
 #endif
 #ifndef NONODE_PAIR_B
-#define NONODE_PAIR_B 1
+#define NONODE_PAIR_B 0   // pass B in the pair form measured slower (664 vs 524 us per C4 layer: spills)
 #endif
 #ifndef NONODE_PAIR_FENCE
 #define NONODE_PAIR_FENCE 1
@@ -35,7 +35,10 @@ namespace {
 #else
 #define PAIR_FENCE() do {} while (0)
 #endif
-constexpr int MMAX_T = 9;   // training path: every rfft bin of T <= 16 (as the forward, MMAX): tconv_bwd_kernel<1..9>
+#ifndef NONODE_MMAX_T
+#define NONODE_MMAX_T 9
+#endif
+constexpr int MMAX_T = NONODE_MMAX_T;   // training path: every rfft bin of T <= 16 (as the forward, MMAX): tconv_bwd_kernel<1..9>
 
 // ---- backward weight blob (unscaled f32 fragments, forward and transposed) --------------------
 enum : int {
@@ -59,11 +62,16 @@ enum : int {
 };
 enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
 constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2, [SC_*] option flags
-// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the 64x64 edge matrices: the edge backward's
+// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the 64x64 matrices: the edge backward's
 // forward recompute (W2, Wc1), its transposed products (W2^T, Wc1^T) and its chunk tables
-// P = W_A h + b1, Q = W_B h run fp16x3
+// P = W_A h + b1, Q = W_B h; the node backward's WV1, WN1 (h and message columns), their transposes
+// and WN2^T (contiguous, in the order node_bwd_kernel stages them)
 constexpr int BOFF_H16 = BOFF_SCAL + 64;
-enum : int { BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_WA, BH_WB, BH_COUNT };
+enum : int {
+  BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_WA, BH_WB,
+  BH_WV1, BH_WN1A, BH_WN1B, BH_WV1T, BH_WN2T, BH_WN1TH, BH_WN1TM, BH_COUNT
+};
+constexpr int BH_NODE0 = BH_WV1, BH_NODE_COUNT = BH_COUNT - BH_WV1;
 constexpr int BBLOB_FLOATS = BOFF_H16 + BH_COUNT * 4096;
 
 // frag of W^T: value W^T[row][col] = W[col][row0 + row] (W row stride ld)
@@ -74,18 +82,20 @@ __device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, 
   dst[d] = W[col * ld + row0 + row];
 }
 
-// pack_h16 of W^T: W^T[row][col] = W[col][row] (W row stride ld), lo part x 2^k (h8_scale)
+// pack_h16 of W^T: W^T[row][col] = W[col][row] (W row stride ld; null W: zeros), lo part x 2^k (h8_scale)
 __device__ __forceinline__ void pack_h16_t(_Float16* dst, const float* W, int d, int ld, int k) {
   const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s = d >> 12;
   const int row = 16 * mo + (lane & 15);
   const int col = 16 * (2 * s + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
-  const float w = W[col * ld + row];
+  const float w = W ? W[col * ld + row] : 0.f;
   const _Float16 h = (_Float16)w;
   dst[d] = hl == 0 ? h : (_Float16)__builtin_ldexpf(w - (float)h, k);   // (see pack_h16)
 }
-__device__ __forceinline__ void pack_h16_t_shifted(_Float16* dst, float* scal, int idx, const float* W, int d) {
-  const int k = h16_lo_shift(W, 64, 0, 1.f);   // the transpose has the same largest |element|
-  pack_h16_t(dst, W, d, 64, k);
+// (of the 64x64 block W[0..63][col0 .. col0+63])
+__device__ __forceinline__ void pack_h16_t_shifted(_Float16* dst, float* scal, int idx, const float* W, int d,
+                                                   int ld = 64, int col0 = 0) {
+  const int k = h16_lo_shift(W, ld, col0, 1.f);   // the transpose has the same largest |element|
+  pack_h16_t(dst, W ? W + col0 : W, d, ld, k);
   if (blockIdx.x == 0 && threadIdx.x == 0) scal[SC_H16S + idx] = h16_us_bits(k);
 }
 
@@ -100,6 +110,13 @@ __global__ void pack_bwd_kernel(PackArgs a) {
     case 19: pack_h16_t_shifted(H + BH_WC1T * 8192, B + BOFF_SCAL, BH_WC1T, a.cw1, d); break;
     case 20: pack_h16_shifted(H + BH_WA * 8192, B + BOFF_SCAL, BH_WA, a.w1, d, a.ld1, a.colA); break;
     case 21: pack_h16_shifted(H + BH_WB * 8192, B + BOFF_SCAL, BH_WB, a.w1, d, a.ld1, a.colB); break;
+    case 22: pack_h16_shifted(H + BH_WV1 * 8192, B + BOFF_SCAL, BH_WV1, a.vw1, d); break;
+    case 23: pack_h16_shifted(H + BH_WN1A * 8192, B + BOFF_SCAL, BH_WN1A, a.nw1, d, 128, 0); break;
+    case 24: pack_h16_shifted(H + BH_WN1B * 8192, B + BOFF_SCAL, BH_WN1B, a.nw1, d, 128, HID); break;
+    case 25: pack_h16_t_shifted(H + BH_WV1T * 8192, B + BOFF_SCAL, BH_WV1T, a.vw1, d); break;
+    case 26: pack_h16_t_shifted(H + BH_WN2T * 8192, B + BOFF_SCAL, BH_WN2T, a.nw2, d); break;
+    case 27: pack_h16_t_shifted(H + BH_WN1TH * 8192, B + BOFF_SCAL, BH_WN1TH, a.nw1, d, 128, 0); break;
+    case 28: pack_h16_t_shifted(H + BH_WN1TM * 8192, B + BOFF_SCAL, BH_WN1TM, a.nw1, d, 128, HID); break;
     case 0: if (d < 4096) pack_frag(B + BOFF_WA, a.w1, a.ld1, a.colA, 4, d, 1.f); break;
     case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
     case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
@@ -145,7 +162,7 @@ __global__ void pack_bwd_kernel(PackArgs a) {
         else if (i == 1 && a.vb2) val = a.vb2[0];
         else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
         else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
-        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-21
+        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-28
       }
       break;
   }
@@ -218,6 +235,13 @@ __device__ __forceinline__ float col_max(float v) {
   v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float amax16(const f4 (&x)[4]) {
+  float m[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+    m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
+  return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
 }
 // max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors; no LDS round trip)
 template <int C>
@@ -356,11 +380,138 @@ struct NodeBwdArgs {
   float* GB; float* GX;                                              // zeroed for the edge backward
 };
 
-// Persistent: one workgroup (8 waves, two per SIMD) per CU stages the six node-side fragment
-// matrices in LDS once (112 KB: WV1, WN1, WV1^T, WN2^T, WN1^T h / m columns) and its waves walk
-// 16-node tiles. (One tile per wave with the fragments read from L2 moved ~128 KB of fragments per
-// 16 nodes: 92 us per C4 layer, L2-bound.) Also zeroes the edge backward's GB / GX rows.
+// fp16x3 node backward: 82 vs 100 us per C4 layer (default scheduler, same box), but the
+// iterative-ILP machine scheduler that the rest of the library is built with leaves invalid live
+// intervals in it (machine verifier: 'No live segment at use'; the greedy allocator then crashes)
+#ifndef NONODE_NODE_H16
+#define NONODE_NODE_H16 0
+#endif
+// Persistent: one workgroup (8 waves, two per SIMD) per CU stages the node-side matrices in LDS once
+// (112 KB) and its waves walk 16-node tiles. (One tile per wave with the fragments read from L2 moved
+// ~128 KB of fragments per 16 nodes: 92 us per C4 layer, L2-bound.) Also zeroes the edge backward's
+// GB / GX rows.
 constexpr int NB_WAVES = 8;
+#if NONODE_NODE_H16
+// The seven products (WV1 h, WN1 [h, M], WV1^T gt, WN2^T gho, WN1^T gz) run fp16x3 on
+// v_mfma_f32_16x16x32_f16 (24 MFMAs each, against 64 or 128 f32 16x16x4 MFMAs of 4x the cycles):
+// every operand column is scaled by a power of two to [2^11, 2^12) before the split and the product
+// scaled back (cs_split, exact), so activations and gradients of any magnitude take the same path.
+constexpr int NB_LDS_FLOATS = BH_NODE_COUNT * 4096;   // 28672: the seven fp16 hi/lo fragment sets
+// column-scaled fp16x3 split of a 16-column operand (as mm64_cs); returns the inverse scale
+__device__ __forceinline__ float cs_split(const f4 (&x)[4], h8 (&xh)[2], h8 (&xl)[2]) {
+  const float sc = p2scale(col_max(amax16(x)));
+  f4 xs[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) xs[mt] = x[mt] * sc;
+  h16_split(xs, xh, xl);
+  return 1.f / sc;   // exact (power of two)
+}
+// out (+)= inv * W x (W: one staged fragment set)
+template <bool ADD>
+__device__ __forceinline__ void mm_node(f4 (&out)[4], const h8* wh, const h8 (&xh)[2], const h8 (&xl)[2],
+                                        float inv, int lane, unsigned us) {
+  f4 acc[4];
+  zero4(acc);
+  mfma_h16(acc, wh, xh, xl, lane, us);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) out[mt] = ADD ? out[mt] + acc[mt] * inv : acc[mt] * inv;
+}
+__global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
+  {
+    const f4* src = reinterpret_cast<const f4*>(p.bb + BOFF_H16 + BH_NODE0 * 4096);
+    for (int i = threadIdx.x; i < NB_LDS_FLOATS / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem)[i] = src[i];
+  }
+  __syncthreads();
+  const h8* sH_ = reinterpret_cast<const h8*>(smem);
+  const int ntile = (p.n + 15) >> 4;
+#pragma unroll 1
+  for (int tile = blockIdx.x * NB_WAVES + wave; tile < ntile; tile += gridDim.x * NB_WAVES) {
+  // loop-invariant reads stay in the loop (hoisted, the 7 x 64 fragment registers per lane would
+  // not fit): opaque zero offset
+  int off = 0;
+  asm volatile("" : "+v"(off));
+  const float* bb = p.bb + off;
+  const h8* sH = sH_ + off;
+  const auto W = [&](int k) { return sH + (k - BH_NODE0) * 1024; };
+  const auto us = [&](int k) { return h16_us(bb + BOFF_SCAL, k); };
+  const int r0 = tile * 16;
+  const int r = min(r0 + e, p.n - 1);
+  const bool valid = r0 + e < p.n;
+  f4 hr[4], Mr[4];
+  load_ecl(hr, p.h + (size_t)r * HID, g);
+  load_ecl(Mr, p.M + (size_t)r * HID, g);
+  h8 xh[2], xl[2];
+  float inv = cs_split(hr, xh, xl);
+  // phi_v(h) = wv2 . SiLU(WV1 h + bv1) + bv2;  node MLP pre-activation zp = WN1 [h, M] + bn1
+  f4 tp[4], zp[4];
+  load_vp(tp, bb + BOFF_VEC + BV_BV1 * 64, g);
+  mm_node<true>(tp, W(BH_WV1), xh, xl, inv, lane, us(BH_WV1));
+  load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
+  mm_node<true>(zp, W(BH_WN1A), xh, xl, inv, lane, us(BH_WN1A));
+  inv = cs_split(Mr, xh, xl);
+  mm_node<true>(zp, W(BH_WN1B), xh, xl, inv, lane, us(BH_WN1B));
+  f4 t[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) t[mt] = tp[mt];
+  silu_true(t);
+  const float phi = dot_vp(t, bb + BOFF_VEC + BV_WV2 * 64, g) + bb[BOFF_SCAL + 1];
+  const float gx0 = p.gxo[(size_t)r * 3 + 0], gx1 = p.gxo[(size_t)r * 3 + 1], gx2 = p.gxo[(size_t)r * 3 + 2];
+  const float v0 = p.v[(size_t)r * 3 + 0], v1 = p.v[(size_t)r * 3 + 1], v2 = p.v[(size_t)r * 3 + 2];
+  const float gphi = gx0 * v0 + gx1 * v1 + gx2 * v2;
+  // clamp(F / (N-1), +-100) passes the gradient inside [-100, 100]
+  const float finv = 1.f / (float)(p.N - 1);
+  const float F0 = p.F[(size_t)r * 4 + 0] * finv, F1 = p.F[(size_t)r * 4 + 1] * finv, F2 = p.F[(size_t)r * 4 + 2] * finv;
+  const float gF0 = (F0 >= -100.f && F0 <= 100.f) ? gx0 * finv : 0.f;
+  const float gF1 = (F1 >= -100.f && F1 <= 100.f) ? gx1 * finv : 0.f;
+  const float gF2 = (F2 >= -100.f && F2 <= 100.f) ? gx2 * finv : 0.f;
+  // gt_pre = gphi * wv2 (.) silu'(tp);  gh = WV1^T gt_pre
+  f4 gt[4];
+  load_vp(gt, bb + BOFF_VEC + BV_WV2 * 64, g);
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) gt[mt] *= gphi;
+  mul_dsilu(gt, tp);
+  f4 gh[4];
+  inv = cs_split(gt, xh, xl);
+  mm_node<false>(gh, W(BH_WV1T), xh, xl, inv, lane, us(BH_WV1T));
+  // node MLP reverse: gz = WN2^T gho (.) silu'(zp), gh += WN1h^T gz, gM = WN1m^T gz
+  f4 z[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
+  silu_true(z);
+  f4 gho[4], gz[4];
+  load_ecl(gho, p.gho + (size_t)r * HID, g);
+  inv = cs_split(gho, xh, xl);
+  mm_node<false>(gz, W(BH_WN2T), xh, xl, inv, lane, us(BH_WN2T));
+  mul_dsilu(gz, zp);
+  inv = cs_split(gz, xh, xl);
+  mm_node<true>(gh, W(BH_WN1TH), xh, xl, inv, lane, us(BH_WN1TH));
+  f4 gM[4];
+  mm_node<false>(gM, W(BH_WN1TM), xh, xl, inv, lane, us(BH_WN1TM));
+  if (valid) {
+    const size_t o = (size_t)r * HID;
+    store_ecl(p.ghp + o, gh, g);
+    store_ecl(p.gM + o, gM, g);
+    store_ecl(p.op_gt + o, gt, g);
+    store_ecl(p.op_t + o, t, g);
+    store_ecl(p.op_z + o, z, g);
+    store_ecl(p.op_gz + o, gz, g);
+    const f4 z4[4] = {};
+    store_ecl(p.GB + o, z4, g);                          // the edge backward's sender sums start at 0
+    if (g == 0) {
+      p.gv[(size_t)r * 3 + 0] = p.gvo[(size_t)r * 3 + 0] + phi * gx0;
+      p.gv[(size_t)r * 3 + 1] = p.gvo[(size_t)r * 3 + 1] + phi * gx1;
+      p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
+      *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
+      *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = f4{0.f, 0.f, 0.f, 0.f};
+      p.op_gphi[r] = gphi;
+    }
+  }
+  }
+}
+#else
+// exact f32 MFMAs: the six node-side f32 fragment matrices (WV1, WN1, WV1^T, WN2^T, WN1^T h / m)
 constexpr int NB_LDS_FLOATS = (BOFF_WN1 + 8192 - BOFF_WV1) + (BOFF_WN1TM + 4096 - BOFF_WV1T);   // 28672
 __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -470,6 +621,8 @@ __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) 
   }
 }
 
+#endif
+
 int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s) {
   static std::once_flag once;
   std::call_once(once, [] {
@@ -550,20 +703,13 @@ size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
 // unscaled in ECL registers by the caller.
 // exact: A beyond the fp16 range (a diverged rollout) -> the f32 MFMA form for this unit.
 // max |x| over a lane's 16 values as a tree (v_max3), not a 16-long dependent chain
-__device__ __forceinline__ float amax16(const f4 (&x)[4]) {
-  float m[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-    m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
-  return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
-}
 // channel held by image column 16 t + i (see the pair path below)
 __device__ __forceinline__ int chan_img(int t, int i) {
   const int s = t >> 1, g = 2 * (t & 1) + (i >> 3), j = i & 7;
   return 16 * (2 * s + (j >> 2)) + 4 * g + (j & 3);
 }
 // running-scale update shared by both weight-gradient forms: cm = col_max of this step's G
-__device__ __forceinline__ void wgrad_rescale(f4 (&acc)[4][4], float& sc, float cm) {
+__device__ __forceinline__ void wgrad_rescale(f4 (&acc)[4][4], float& sc, float cm, float* bsum = nullptr) {
   const float m = row_max16(cm);
   const float mu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, m)));
   if (mu > 0.f) {
@@ -571,36 +717,45 @@ __device__ __forceinline__ void wgrad_rescale(f4 (&acc)[4][4], float& sc, float 
     if (su < sc) {
       const float r = su / sc;
 #pragma unroll
-      for (int ot = 0; ot < 4; ++ot)
+      for (int ot = 0; ot < 4; ++ot) {
+        if (bsum) bsum[ot] *= r;
 #pragma unroll
         for (int it = 0; it < 4; ++it) acc[ot][it] *= r;
+      }
       sc = su;
     }
   }
 }
 // cm: col_max(amax16(G)), shared with the transposed product of the same G (mm64_cs)
-// AG: the accumulators live in AGPRs (pass A: the asm blocks above, as the pair path); else builtins
+// AG: the accumulators live in AGPRs, in image-column order (the pair path's form, whose asm blocks
+// these use); else builtins in natural channel order (column 16 t + e), with the bias sum of G taken
+// here: bsum[t] += G summed over the lane's four edges at channel 16 t + e, in units of 1/sc (round 3's
+// form, which the single-unit-only pass keeps)
 template <bool AG>
 __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float& sc, const f4 (&G)[4], const f4 (&A)[4],
-                                          float* tile, int g, int e, bool exact, float cm) {
+                                          float* tile, int g, int e, bool exact, float cm, float (&bsum)[4]) {
   // G goes to the transpose tile unscaled, so the wave-wide max / scale below runs beside the LDS
   // round trip instead of before it; the scale is applied to the transposed values
   float* tG = tile;
   float* tA = tile + 16 * ROWT;
   store_ecl(tG + e * ROWT, G, g);
   store_ecl(tA + e * ROWT, A, g);
-  wgrad_rescale(acc, sc, cm);
+  wgrad_rescale(acc, sc, cm, AG ? nullptr : bsum);
   __builtin_amdgcn_wave_barrier();
-  int ce[4];   // this lane's channel of image column 16 t + e
+  int ce[4];   // this lane's channel of column 16 t + e
 #pragma unroll
-  for (int t = 0; t < 4; ++t) ce[t] = chan_img(t, e);
+  for (int t = 0; t < 4; ++t) ce[t] = AG ? chan_img(t, e) : 16 * t + e;
   if (__builtin_expect(exact, 0)) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int row = (4 * g + ks) * ROWT;
       float gv[4], av[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) { gv[t] = tG[row + ce[t]] * sc; av[t] = tA[row + ce[t]]; }
+      for (int t = 0; t < 4; ++t) {
+        gv[t] = tG[row + ce[t]] * sc;
+        av[t] = tA[row + ce[t]];
+        if constexpr (!AG) bsum[t] += gv[t];
+      }
       if constexpr (AG) {
         amfma4_block(acc, gv, av);
       } else {
@@ -627,6 +782,7 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float& sc, const f4 (
     f4 v;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) v[ks] = tG[(4 * g + ks) * ROWT + ce[ot]] * sc;
+    if constexpr (!AG) bsum[ot] += (v[0] + v[1]) + (v[2] + v[3]);
     h4 gh, gl;
     h4_split(v, gh, gl);
     if constexpr (AG) {
@@ -840,8 +996,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
 #pragma unroll
   for (int f = 0; f < NF; ++f) zero4(accFe[f]);
   zero4(sWC2);
-  f4 bsE[4];   // PASS 0: dbc1, PASS 1: db2, per lane in ECL (summed over the lane group's edges at the end)
+  // bias gradient (PASS 0: dbc1, PASS 1: db2): with the pair path per lane in ECL (bsE, summed over the
+  // lane group's edges at the end), else per lane at channel 16 t + e in units of 1/scW (sB, wgrad_h16)
+  f4 bsE[4];
   zero4(bsE);
+  float sB[4] = {0.f, 0.f, 0.f, 0.f};
   float sGC = 0.f;
   const int G = gridDim.x;
   const int nb = (int)(((long long)blockIdx.x * p.n_graphs) / G) * N;
@@ -1093,9 +1252,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           f4 m[4];
 #pragma unroll
           for (int mt = 0; mt < 4; ++mt) m[mt] = z2[mt] * sg2[mt];
-          wgrad_h16<PAIRS>(accW, scW, gz3, m, tile, g, e, bigM, cm3);
+          wgrad_h16<PAIRS>(accW, scW, gz3, m, tile, g, e, bigM, cm3, sB);
+          if constexpr (PAIRS) {
 #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) bsE[mt] += gz3[mt];
+            for (int mt = 0; mt < 4; ++mt) bsE[mt] += gz3[mt];
+          }
         }
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) sWC2[mt] += gc * (z3[mt] * sg3[mt]);
@@ -1141,9 +1302,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         f4 a[4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) a[mt] = z1[mt] * sg1[mt];
-        wgrad_h16<PAIRS>(accW, scW, gz2, a, tile, g, e, bigA, cm2);
+        wgrad_h16<PAIRS>(accW, scW, gz2, a, tile, g, e, bigA, cm2, sB);
+        if constexpr (PAIRS) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) bsE[mt] += gz2[mt];
+          for (int mt = 0; mt < 4; ++mt) bsE[mt] += gz2[mt];
+        }
       }
       STAMP(5);
       f4 gz1[4];
@@ -1603,26 +1766,40 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   // ---- D: weight-gradient partials: each wave's to LDS, then one per block (waves added in order) ----
   __syncthreads();   // the last chunk's tables are dead: reuse the LDS
   float* wp = smem + wave * EW_STRIDE;
-  auto put = [&](const f4 (&acc)[4][4], const f4 (&bs)[4], float sc, int wo) {
+  auto put = [&](const f4 (&acc)[4][4], float sc, int wo) {
     const float inv_sc = 1.f / sc;   // exact (power of two)
-    // acc is in image-column order on both axes (wgrad_h16 / wgrad_pair): un-permuted here
+    if constexpr (PAIRS) {
+      // acc in image-column order on both axes (wgrad_pair / wgrad_h16<true>): un-permuted here; bias:
+      // lane (e, g) holds channel 16 mt + 4 g + q summed over its edges; add the 16 edges
 #pragma unroll
-    for (int ot = 0; ot < 4; ++ot)
+      for (int ot = 0; ot < 4; ++ot)
 #pragma unroll
-      for (int it = 0; it < 4; ++it)
+        for (int it = 0; it < 4; ++it)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          wp[wo + chan_img(ot, 4 * g + q) * 65 + chan_img(it, e)] = acc[ot][it][q] * inv_sc;
-    // bias: lane (e, g) holds channel 16 mt + 4 g + q summed over its edges; add the 16 edges
+          for (int q = 0; q < 4; ++q)
+            wp[wo + chan_img(ot, 4 * g + q) * 65 + chan_img(it, e)] = acc[ot][it][q] * inv_sc;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float b = edge_sum16(bs[mt][q]);
-        if (e == 0) wp[wo + (16 * mt + 4 * g + q) * 65 + 64] = b;
+        for (int q = 0; q < 4; ++q) {
+          const float b = edge_sum16(bsE[mt][q]);
+          if (e == 0) wp[wo + (16 * mt + 4 * g + q) * 65 + 64] = b;
+        }
+    } else {
+#pragma unroll
+      for (int ot = 0; ot < 4; ++ot)
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) wp[wo + (16 * ot + 4 * g + q) * 65 + 16 * it + e] = acc[ot][it][q] * inv_sc;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float bs = group_sum(sB[t]) * inv_sc;
+        if (g == 0) wp[wo + (16 * t + e) * 65 + 64] = bs;
       }
+    }
   };
-  put(accW, bsE, scW, PASS == 0 ? EW_WC1 : EW_W2);
+  put(accW, scW, PASS == 0 ? EW_WC1 : EW_W2);
   if (PASS == 1) {
 #pragma unroll
     for (int f = 0; f < NF; ++f)
@@ -2016,9 +2193,11 @@ int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
     case 4: go(std::integral_constant<int, 4>{}); break;
     case 5: go(std::integral_constant<int, 5>{}); break;   // num_modes = 5 (model_confs.yaml:12)
     case 6: go(std::integral_constant<int, 6>{}); break;
+#if NONODE_MMAX_T >= 9
     case 7: go(std::integral_constant<int, 7>{}); break;
     case 8: go(std::integral_constant<int, 8>{}); break;
     case 9: go(std::integral_constant<int, 9>{}); break;
+#endif
     default: return fail(NONODE_EUNSUPPORTED, "tconv_bwd: modes=%d", M);
   }
   return check_launch("tconv_bwd_kernel");
@@ -2465,7 +2644,7 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   a.ne = n_edge_feat;
   a.flags = flags;
   a.blob = bblob;
-  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 22), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 29), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_bwd_kernel");
 }
 
