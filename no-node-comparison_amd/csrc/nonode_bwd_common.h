@@ -1,0 +1,203 @@
+// nonode_bwd_common.h — shared by the training translation units (nonode_train.hip, included by
+// nonode.hip, and nonode_node.hip): the backward weight-blob layout, true-scale SiLU helpers, the
+// power-of-two column scaling of the fp16x3 gradient products, and the node-backward interface.
+#pragma once
+#include "nonode_common.h"
+
+namespace {
+
+// ---- backward weight blob (unscaled f32 fragments, forward and transposed) --------------------
+enum : int {
+  BOFF_WA = 0,          // edge W1 h_i columns                 (frag layout, KT=4)
+  BOFF_WB = 4096,       // edge W1 h_j columns
+  BOFF_W2 = 8192,       // edge W2
+  BOFF_WC1 = 12288,     // coord W1
+  BOFF_WV1 = 16384,     // node_v W1
+  BOFF_WN1 = 20480,     // node W1 [64][128]                   (KT=8)
+  BOFF_WN2 = 28672,     // node W2
+  BOFF_W2T = 32768,     // W2^T
+  BOFF_WC1T = 36864,    // Wc1^T
+  BOFF_WV1T = 40960,    // WV1^T
+  BOFF_WN2T = 45056,    // WN2^T
+  BOFF_WN1TH = 49152,   // (WN1[:, 0:64])^T    (h columns)
+  BOFF_WN1TM = 53248,   // (WN1[:, 64:128])^T  (message-sum columns)
+  BOFF_WAT = 57344,     // W_A^T
+  BOFF_WBT = 61440,     // W_B^T
+  BOFF_FEAT = 65536,    // scalar-input columns [s, e...] as k-steps (as OFF_FEAT, unscaled)
+  BOFF_VEC = 66048,     // vectors (vp order), BV_* below
+};
+enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
+constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2, [SC_*] option flags
+// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the 64x64 matrices: the edge backward's
+// forward recompute (W2, Wc1), its transposed products (W2^T, Wc1^T) and its chunk tables
+// P = W_A h + b1, Q = W_B h; the node backward's WV1, WN1 (h and message columns), their transposes
+// and WN2^T (contiguous, in the order node_bwd_kernel stages them)
+constexpr int BOFF_H16 = BOFF_SCAL + 64;
+enum : int {
+  BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_WA, BH_WB,
+  BH_WV1, BH_WN1A, BH_WN1B, BH_WV1T, BH_WN2T, BH_WN1TH, BH_WN1TM, BH_WAT, BH_WBT, BH_COUNT
+};
+constexpr int BH_NODE0 = BH_WV1, BH_NODE_COUNT = BH_WN1TM + 1 - BH_WV1;   // node_bwd_kernel's seven
+constexpr int BBLOB_FLOATS = BOFF_H16 + BH_COUNT * 4096;
+
+// ---- true-scale SiLU and its derivative ---------------------------------------------------------
+__device__ __forceinline__ float sigm(float z) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z * NEG_LOG2E)); }
+__device__ __forceinline__ void silu_true(f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[mt][q] *= sigm(a[mt][q]);
+}
+// g *= silu'(z) = s (1 + z (1 - s))
+__device__ __forceinline__ void mul_dsilu(f4 (&gz)[4], const f4 (&z)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float s = sigm(z[mt][q]);
+      gz[mt][q] *= s * fmaf(z[mt][q], 1.f - s, 1.f);
+    }
+}
+__device__ __forceinline__ void zero4(f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) a[mt] = f4{0.f, 0.f, 0.f, 0.f};
+}
+// a = SiLU(z) keeping the sigmoid s for the reverse pass (one exp + one rcp per value, not two)
+__device__ __forceinline__ void silu_keep(const f4 (&z)[4], f4 (&s)[4], f4 (&a)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      s[mt][q] = sigm(z[mt][q]);
+      a[mt][q] = z[mt][q] * s[mt][q];
+    }
+}
+// a = SiLU(z) and d = SiLU'(z) = s (1 + z (1 - s)) (one exp + one rcp per value)
+__device__ __forceinline__ void silu_dsilu(const f4 (&z)[4], f4 (&a)[4], f4 (&d)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float s = sigm(z[mt][q]);
+      a[mt][q] = z[mt][q] * s;
+      d[mt][q] = s * fmaf(z[mt][q], 1.f - s, 1.f);
+    }
+}
+// g *= silu'(z) from the kept sigmoid
+__device__ __forceinline__ void mul_dsilu_s(f4 (&gz)[4], const f4 (&z)[4], const f4 (&s)[4]) {
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gz[mt][q] *= s[mt][q] * fmaf(z[mt][q], 1.f - s[mt][q], 1.f);
+}
+
+// ---- fp16x3 products of the edge backward ----------------------------------------------------
+// Activations are O(1) and take the forward's fp16x3 split (guarded by H16_LIMIT). Gradients have
+// no fixed scale (they carry the loss normalisation, ~1e-7 here), so they are scaled by powers of
+// two before the split: exact, and it keeps hi and lo out of the fp16 subnormal range.
+// 2^(12 - e) for m = f 2^e (f in [0.5, 1)): m times it lies in [2^11, 2^12)
+__device__ __forceinline__ float p2scale(float m) {
+  int ex = __builtin_amdgcn_frexp_expf(m);
+  ex = ex < -100 ? -100 : (ex > 100 ? 100 : ex);
+  return __builtin_ldexpf(1.f, 12 - ex);
+}
+// max over the 4 lane groups (the 64 channels of column e)
+__device__ __forceinline__ float col_max(float v) {
+  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float amax16(const f4 (&x)[4]) {
+  float m[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+    m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
+  return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
+}
+}  // namespace
+
+namespace nonode_tu {
+// ---- node backward (basic.py:174-185 reversed): nonode_node.hip --------------------------------
+struct NodeBwdArgs {
+  int n, N;
+  const float* h; const float* v; const float* M; const float* F;   // layer inputs + saved sums
+  const float* gxo; const float* gvo; const float* gho;              // grads of the layer outputs
+  const float* bb;                                                   // backward blob
+  float* gv; float* gF; float* gM; float* ghp;                       // outputs
+  float* op_gt; float* op_t; float* op_gphi; float* op_z; float* op_gz;   // GEMM operands
+  float* GB; float* GX;                                              // zeroed for the edge backward
+};
+// launches node_bwd_kernel over ntile 16-node tiles on stream s (NONODE_OK or an error code)
+int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s);
+
+// ---- gh = ghp + W_A^T GA + W_B^T GB, gx = gxo + GX after the edge backward: nonode_node.hip --------
+struct NodePostArgs {
+  int n;
+  const float* ghp; const float* GA; const float* GB; const float* gxo; const float* GX;
+  const float* bb;                 // backward blob (BH_WAT, BH_WBT fp16 fragments)
+  float* gh; float* gx;
+};
+int launch_node_post(const NodePostArgs& a, hipStream_t s);
+
+// ---- node-level weight gradients: nonode_node.hip ----------------------------------------------
+// The layer's GEMMs over its n nodes, C_j = sum_k G_j[k] (x) A_j[k] (64x64, plus the bias column
+// sum_k G_j[k]) for j < 6, and the node_v output row (j = 6: sum_k gphi[k] t[k], bias sum_k gphi[k]):
+//   0 GA (x) h -> edge W1 h_i block (+ b1)    3 gz (x) h -> node W1 h block (+ b1)
+//   1 GB (x) h -> edge W1 h_j block           4 gz (x) M -> node W1 message block
+//   2 gt (x) h -> node_v W1 (+ b1)            5 gh (x) z -> node W2 (+ b2)       6 gphi (x) t -> node_v W2 (+ b2)
+// Each workgroup writes one [NW_JOBS][64][65] partial (row 0 only for job 6); the caller adds them
+// in block order (gemm_reduce_batch, deterministic). SEGNO (no node_v MLP) passes t = gt = gphi = null:
+// jobs 2 and 6 are then zero.
+constexpr int NW_JOBS = 7, NW_MAX_BLOCKS = 256, NW_PART = 64 * 65;
+struct NodeWgradArgs {
+  long long n, chunks_per_block;   // n nodes in 32-node chunks; block b takes chunks [b c, (b + 1) c)
+  const float* h; const float* M; const float* z; const float* t;                  // A-side rows (n x 64)
+  const float* GA; const float* GB; const float* gt; const float* gz; const float* gh;   // G-side rows
+  const float* gphi;                                                                   // n
+  float* partial;                                                                      // [blocks][NW_JOBS][NW_PART]
+};
+// launches node_wgrad_kernel (returns the number of blocks, i.e. partials, in *nblk)
+int launch_node_wgrad(const NodeWgradArgs& a, int* nblk, hipStream_t s);
+
+constexpr int MMAX_T = 9;   // training path: every rfft bin of T <= 16 (as the forward, MMAX): tconv_bwd_kernel<1..9>
+
+// ---- TimeConv reverse (layer_no.py:80-126; oracle/egno_grad.py spectral_bwd) -------------------
+// Persistent: each 4-wave workgroup walks 16-column tiles (columns c = (b, n)). Per tile:
+//   1. DFT of the input h (wave w: input channels 16w..16w+15) -> sX (the forward's layout);
+//   2. (no forward recompute: the LeakyReLU decisions come from the forward, TrainState::mask);
+//   3. gy[t] = gout[t] * leaky'(y[t]);  gYr_m = (c_m/T) sum_t cos gy,  gYi_m = -(c_m/T) sum_t sin gy
+//      -> sG (zero for columns past BN);
+//   4. backward mixing on MFMA: gXr = Wr gYr + Wi gYi, gXi = -Wi gYr + Wr gYi (wave w: input
+//      channels 16w..) and gh[t] = gout[t] + sum_m (gXr_m cos - gXi_m sin)   (Xi = -sum_t h sin);
+//   5. weight gradient: gWr_m += Xr (x) gYr + Xi (x) gYi,  gWi_m += -Xi (x) gYr + Xr (x) gYi over the
+//      tile's columns (K = columns, read straight from sX / sG with channels along lane & 15),
+//      wave w owning rows i = 16w..16w+15.
+// One partial per workgroup [M][re|im][64][64]; tconv_wgrad_reduce adds them in a fixed order.
+// A workgroup runs TB_NG(MM) such 4-wave groups on TB_NG tiles at once (own sX / sG, shared twiddles,
+// the workgroup's barriers in lockstep): at C4 (640 tiles, 2 modes) every tile is in flight in one
+// round instead of each CU walking 2-3 tiles one after another, a latency chain of load -> DFT ->
+// barrier -> mixing -> store per tile. The groups' weight-gradient accumulators are added in group
+// order before the one partial is written.
+
+constexpr int TB_MAX_BLOCKS = 256;
+// 4-wave tile groups per workgroup: two at <= 2 modes (three spill at the
+// 170 registers of three waves per SIMD), else one
+#ifndef NONODE_TB_NG
+#define NONODE_TB_NG 2
+#endif
+constexpr int tb_groups(int MM) { return MM <= 2 ? NONODE_TB_NG : 1; }
+struct TconvBwdArgs {
+  int BN, T, M, ntiles;
+  const float* h;      // TimeConv input [T][BN][64]
+  const float* gout;   // gradient of its output
+  const float* wp;     // forward fragments (tconv_pack_kernel layout)
+  const float* wb;     // backward fragments (tconv_pack_bwd_kernel layout)
+  float* gh;           // gradient of the input
+  float* wpart;        // [grid][M][2][64][64]
+  const unsigned long long* mask;   // the forward's LeakyReLU decisions (TconvArgs::mask_out layout)
+};
+
+// launches tconv_bwd_kernel<M> (nonode_tconv.hip) on G workgroups
+int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s);
+}  // namespace nonode_tu

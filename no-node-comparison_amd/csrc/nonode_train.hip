@@ -5,7 +5,7 @@
 // pinned to the reference's own autograd gradients (tests/golden/egno_grad.npz).
 //
 // Included at the end of nonode.hip (same translation unit: shares the ECL helpers, the MFMA
-// fragment layout and the launch utilities).
+// fragment layout and the launch utilities); node_bwd_kernel is in nonode_node.hip.
 //
 // Per layer l (reverse order), given the gradients of that layer's outputs (gx, gv, gh):
 //   node_bwd_kernel   x/v update + node MLP reverse (basic.py:174-185): gF, gM, gv, part of gh
@@ -19,7 +19,17 @@
 //
 // Stage 1 of the training path: exact f32 MFMAs (16x16x4) for every matrix product.
 
+#include "nonode_bwd_common.h"
+
 namespace {
+
+using nonode_tu::NodeBwdArgs;
+using nonode_tu::launch_node_bwd;
+using nonode_tu::MMAX_T;
+using nonode_tu::TB_MAX_BLOCKS;
+using nonode_tu::TconvBwdArgs;
+using nonode_tu::launch_tconv_bwd;
+using nonode_tu::tb_groups;
 
 #ifndef NONODE_PAIR_A
 #define NONODE_PAIR_A 1
@@ -35,44 +45,6 @@ namespace {
 #else
 #define PAIR_FENCE() do {} while (0)
 #endif
-#ifndef NONODE_MMAX_T
-#define NONODE_MMAX_T 9
-#endif
-constexpr int MMAX_T = NONODE_MMAX_T;   // training path: every rfft bin of T <= 16 (as the forward, MMAX): tconv_bwd_kernel<1..9>
-
-// ---- backward weight blob (unscaled f32 fragments, forward and transposed) --------------------
-enum : int {
-  BOFF_WA = 0,          // edge W1 h_i columns                 (frag layout, KT=4)
-  BOFF_WB = 4096,       // edge W1 h_j columns
-  BOFF_W2 = 8192,       // edge W2
-  BOFF_WC1 = 12288,     // coord W1
-  BOFF_WV1 = 16384,     // node_v W1
-  BOFF_WN1 = 20480,     // node W1 [64][128]                   (KT=8)
-  BOFF_WN2 = 28672,     // node W2
-  BOFF_W2T = 32768,     // W2^T
-  BOFF_WC1T = 36864,    // Wc1^T
-  BOFF_WV1T = 40960,    // WV1^T
-  BOFF_WN2T = 45056,    // WN2^T
-  BOFF_WN1TH = 49152,   // (WN1[:, 0:64])^T    (h columns)
-  BOFF_WN1TM = 53248,   // (WN1[:, 64:128])^T  (message-sum columns)
-  BOFF_WAT = 57344,     // W_A^T
-  BOFF_WBT = 61440,     // W_B^T
-  BOFF_FEAT = 65536,    // scalar-input columns [s, e...] as k-steps (as OFF_FEAT, unscaled)
-  BOFF_VEC = 66048,     // vectors (vp order), BV_* below
-};
-enum : int { BV_B1 = 0, BV_B2, BV_BC1, BV_WC2, BV_BV1, BV_WV2, BV_BN1, BV_BN2, BV_WS, BV_COUNT };
-constexpr int BOFF_SCAL = BOFF_VEC + BV_COUNT * 64;   // [0] coord b2, [1] node_v b2, [SC_*] option flags
-// fp16 hi/lo fragments (pack_h16 layout, unscaled) of the 64x64 matrices: the edge backward's
-// forward recompute (W2, Wc1), its transposed products (W2^T, Wc1^T) and its chunk tables
-// P = W_A h + b1, Q = W_B h; the node backward's WV1, WN1 (h and message columns), their transposes
-// and WN2^T (contiguous, in the order node_bwd_kernel stages them)
-constexpr int BOFF_H16 = BOFF_SCAL + 64;
-enum : int {
-  BH_W2 = 0, BH_WC1, BH_W2T, BH_WC1T, BH_WA, BH_WB,
-  BH_WV1, BH_WN1A, BH_WN1B, BH_WV1T, BH_WN2T, BH_WN1TH, BH_WN1TM, BH_COUNT
-};
-constexpr int BH_NODE0 = BH_WV1, BH_NODE_COUNT = BH_COUNT - BH_WV1;
-constexpr int BBLOB_FLOATS = BOFF_H16 + BH_COUNT * 4096;
 
 // frag of W^T: value W^T[row][col] = W[col][row0 + row] (W row stride ld)
 __device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, int row0, int d) {
@@ -117,6 +89,8 @@ __global__ void pack_bwd_kernel(PackArgs a) {
     case 26: pack_h16_t_shifted(H + BH_WN2T * 8192, B + BOFF_SCAL, BH_WN2T, a.nw2, d); break;
     case 27: pack_h16_t_shifted(H + BH_WN1TH * 8192, B + BOFF_SCAL, BH_WN1TH, a.nw1, d, 128, 0); break;
     case 28: pack_h16_t_shifted(H + BH_WN1TM * 8192, B + BOFF_SCAL, BH_WN1TM, a.nw1, d, 128, HID); break;
+    case 29: pack_h16_t_shifted(H + BH_WAT * 8192, B + BOFF_SCAL, BH_WAT, a.w1, d, a.ld1, a.colA); break;
+    case 30: pack_h16_t_shifted(H + BH_WBT * 8192, B + BOFF_SCAL, BH_WBT, a.w1, d, a.ld1, a.colB); break;
     case 0: if (d < 4096) pack_frag(B + BOFF_WA, a.w1, a.ld1, a.colA, 4, d, 1.f); break;
     case 1: if (d < 4096) pack_frag(B + BOFF_WB, a.w1, a.ld1, a.colB, 4, d, 1.f); break;
     case 2: if (d < 4096) pack_frag(B + BOFF_W2, a.w2, 64, 0, 4, d, 1.f); break;
@@ -162,87 +136,12 @@ __global__ void pack_bwd_kernel(PackArgs a) {
         else if (i == 1 && a.vb2) val = a.vb2[0];
         else if (i == SC_NORM) val = (a.flags & NONODE_LAYER_NORM_RADIAL) ? 1.f : 0.f;
         else if (i == SC_TANH) val = (a.flags & NONODE_LAYER_TANH_COORD) ? 1.f : 0.f;
-        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-28
+        if (i < SC_H16S || i >= SC_H16S + BH_COUNT) B[BOFF_SCAL + i] = val;   // shifts: sections 16-30
       }
       break;
   }
 }
 
-// ---- true-scale SiLU and its derivative ---------------------------------------------------------
-__device__ __forceinline__ float sigm(float z) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z * NEG_LOG2E)); }
-__device__ __forceinline__ void silu_true(f4 (&a)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) a[mt][q] *= sigm(a[mt][q]);
-}
-// g *= silu'(z) = s (1 + z (1 - s))
-__device__ __forceinline__ void mul_dsilu(f4 (&gz)[4], const f4 (&z)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float s = sigm(z[mt][q]);
-      gz[mt][q] *= s * fmaf(z[mt][q], 1.f - s, 1.f);
-    }
-}
-__device__ __forceinline__ void zero4(f4 (&a)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) a[mt] = f4{0.f, 0.f, 0.f, 0.f};
-}
-// a = SiLU(z) keeping the sigmoid s for the reverse pass (one exp + one rcp per value, not two)
-__device__ __forceinline__ void silu_keep(const f4 (&z)[4], f4 (&s)[4], f4 (&a)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      s[mt][q] = sigm(z[mt][q]);
-      a[mt][q] = z[mt][q] * s[mt][q];
-    }
-}
-// a = SiLU(z) and d = SiLU'(z) = s (1 + z (1 - s)) (one exp + one rcp per value)
-__device__ __forceinline__ void silu_dsilu(const f4 (&z)[4], f4 (&a)[4], f4 (&d)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float s = sigm(z[mt][q]);
-      a[mt][q] = z[mt][q] * s;
-      d[mt][q] = s * fmaf(z[mt][q], 1.f - s, 1.f);
-    }
-}
-// g *= silu'(z) from the kept sigmoid
-__device__ __forceinline__ void mul_dsilu_s(f4 (&gz)[4], const f4 (&z)[4], const f4 (&s)[4]) {
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) gz[mt][q] *= s[mt][q] * fmaf(z[mt][q], 1.f - s[mt][q], 1.f);
-}
-
-// ---- fp16x3 products of the edge backward ----------------------------------------------------
-// Activations are O(1) and take the forward's fp16x3 split (guarded by H16_LIMIT). Gradients have
-// no fixed scale (they carry the loss normalisation, ~1e-7 here), so they are scaled by powers of
-// two before the split: exact, and it keeps hi and lo out of the fp16 subnormal range.
-// 2^(12 - e) for m = f 2^e (f in [0.5, 1)): m times it lies in [2^11, 2^12)
-__device__ __forceinline__ float p2scale(float m) {
-  int ex = __builtin_amdgcn_frexp_expf(m);
-  ex = ex < -100 ? -100 : (ex > 100 ? 100 : ex);
-  return __builtin_ldexpf(1.f, 12 - ex);
-}
-// max over the 4 lane groups (the 64 channels of column e)
-__device__ __forceinline__ float col_max(float v) {
-  const auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
-  const auto b = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
-}
-__device__ __forceinline__ float amax16(const f4 (&x)[4]) {
-  float m[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-    m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
-  return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
-}
 // max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors; no LDS round trip)
 template <int C>
 __device__ __forceinline__ float dppf(float v) {
@@ -367,271 +266,6 @@ __global__ void emb_in_kernel(int BN, int T, int din, int dim, int Bt, const flo
     val = kk < half ? sinf(arg) : cosf(arg);
   }
   emb_in[idx] = val;
-}
-
-// ---- node backward (basic.py:174-185 reversed) ---------------------------------------------------
-struct NodeBwdArgs {
-  int n, N;
-  const float* h; const float* v; const float* M; const float* F;   // layer inputs + saved sums
-  const float* gxo; const float* gvo; const float* gho;              // grads of the layer outputs
-  const float* bb;                                                   // backward blob
-  float* gv; float* gF; float* gM; float* ghp;                       // outputs
-  float* op_gt; float* op_t; float* op_gphi; float* op_z; float* op_gz;   // GEMM operands
-  float* GB; float* GX;                                              // zeroed for the edge backward
-};
-
-// fp16x3 node backward: 82 vs 100 us per C4 layer (default scheduler, same box), but the
-// iterative-ILP machine scheduler that the rest of the library is built with leaves invalid live
-// intervals in it (machine verifier: 'No live segment at use'; the greedy allocator then crashes)
-#ifndef NONODE_NODE_H16
-#define NONODE_NODE_H16 0
-#endif
-// Persistent: one workgroup (8 waves, two per SIMD) per CU stages the node-side matrices in LDS once
-// (112 KB) and its waves walk 16-node tiles. (One tile per wave with the fragments read from L2 moved
-// ~128 KB of fragments per 16 nodes: 92 us per C4 layer, L2-bound.) Also zeroes the edge backward's
-// GB / GX rows.
-constexpr int NB_WAVES = 8;
-#if NONODE_NODE_H16
-// The seven products (WV1 h, WN1 [h, M], WV1^T gt, WN2^T gho, WN1^T gz) run fp16x3 on
-// v_mfma_f32_16x16x32_f16 (24 MFMAs each, against 64 or 128 f32 16x16x4 MFMAs of 4x the cycles):
-// every operand column is scaled by a power of two to [2^11, 2^12) before the split and the product
-// scaled back (cs_split, exact), so activations and gradients of any magnitude take the same path.
-constexpr int NB_LDS_FLOATS = BH_NODE_COUNT * 4096;   // 28672: the seven fp16 hi/lo fragment sets
-// column-scaled fp16x3 split of a 16-column operand (as mm64_cs); returns the inverse scale
-__device__ __forceinline__ float cs_split(const f4 (&x)[4], h8 (&xh)[2], h8 (&xl)[2]) {
-  const float sc = p2scale(col_max(amax16(x)));
-  f4 xs[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) xs[mt] = x[mt] * sc;
-  h16_split(xs, xh, xl);
-  return 1.f / sc;   // exact (power of two)
-}
-// out (+)= inv * W x (W: one staged fragment set)
-template <bool ADD>
-__device__ __forceinline__ void mm_node(f4 (&out)[4], const h8* wh, const h8 (&xh)[2], const h8 (&xl)[2],
-                                        float inv, int lane, unsigned us) {
-  f4 acc[4];
-  zero4(acc);
-  mfma_h16(acc, wh, xh, xl, lane, us);
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) out[mt] = ADD ? out[mt] + acc[mt] * inv : acc[mt] * inv;
-}
-__global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
-  {
-    const f4* src = reinterpret_cast<const f4*>(p.bb + BOFF_H16 + BH_NODE0 * 4096);
-    for (int i = threadIdx.x; i < NB_LDS_FLOATS / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem)[i] = src[i];
-  }
-  __syncthreads();
-  const h8* sH_ = reinterpret_cast<const h8*>(smem);
-  const int ntile = (p.n + 15) >> 4;
-#pragma unroll 1
-  for (int tile = blockIdx.x * NB_WAVES + wave; tile < ntile; tile += gridDim.x * NB_WAVES) {
-  // loop-invariant reads stay in the loop (hoisted, the 7 x 64 fragment registers per lane would
-  // not fit): opaque zero offset
-  int off = 0;
-  asm volatile("" : "+v"(off));
-  const float* bb = p.bb + off;
-  const h8* sH = sH_ + off;
-  const auto W = [&](int k) { return sH + (k - BH_NODE0) * 1024; };
-  const auto us = [&](int k) { return h16_us(bb + BOFF_SCAL, k); };
-  const int r0 = tile * 16;
-  const int r = min(r0 + e, p.n - 1);
-  const bool valid = r0 + e < p.n;
-  f4 hr[4], Mr[4];
-  load_ecl(hr, p.h + (size_t)r * HID, g);
-  load_ecl(Mr, p.M + (size_t)r * HID, g);
-  h8 xh[2], xl[2];
-  float inv = cs_split(hr, xh, xl);
-  // phi_v(h) = wv2 . SiLU(WV1 h + bv1) + bv2;  node MLP pre-activation zp = WN1 [h, M] + bn1
-  f4 tp[4], zp[4];
-  load_vp(tp, bb + BOFF_VEC + BV_BV1 * 64, g);
-  mm_node<true>(tp, W(BH_WV1), xh, xl, inv, lane, us(BH_WV1));
-  load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
-  mm_node<true>(zp, W(BH_WN1A), xh, xl, inv, lane, us(BH_WN1A));
-  inv = cs_split(Mr, xh, xl);
-  mm_node<true>(zp, W(BH_WN1B), xh, xl, inv, lane, us(BH_WN1B));
-  f4 t[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) t[mt] = tp[mt];
-  silu_true(t);
-  const float phi = dot_vp(t, bb + BOFF_VEC + BV_WV2 * 64, g) + bb[BOFF_SCAL + 1];
-  const float gx0 = p.gxo[(size_t)r * 3 + 0], gx1 = p.gxo[(size_t)r * 3 + 1], gx2 = p.gxo[(size_t)r * 3 + 2];
-  const float v0 = p.v[(size_t)r * 3 + 0], v1 = p.v[(size_t)r * 3 + 1], v2 = p.v[(size_t)r * 3 + 2];
-  const float gphi = gx0 * v0 + gx1 * v1 + gx2 * v2;
-  // clamp(F / (N-1), +-100) passes the gradient inside [-100, 100]
-  const float finv = 1.f / (float)(p.N - 1);
-  const float F0 = p.F[(size_t)r * 4 + 0] * finv, F1 = p.F[(size_t)r * 4 + 1] * finv, F2 = p.F[(size_t)r * 4 + 2] * finv;
-  const float gF0 = (F0 >= -100.f && F0 <= 100.f) ? gx0 * finv : 0.f;
-  const float gF1 = (F1 >= -100.f && F1 <= 100.f) ? gx1 * finv : 0.f;
-  const float gF2 = (F2 >= -100.f && F2 <= 100.f) ? gx2 * finv : 0.f;
-  // gt_pre = gphi * wv2 (.) silu'(tp);  gh = WV1^T gt_pre
-  f4 gt[4];
-  load_vp(gt, bb + BOFF_VEC + BV_WV2 * 64, g);
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) gt[mt] *= gphi;
-  mul_dsilu(gt, tp);
-  f4 gh[4];
-  inv = cs_split(gt, xh, xl);
-  mm_node<false>(gh, W(BH_WV1T), xh, xl, inv, lane, us(BH_WV1T));
-  // node MLP reverse: gz = WN2^T gho (.) silu'(zp), gh += WN1h^T gz, gM = WN1m^T gz
-  f4 z[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
-  silu_true(z);
-  f4 gho[4], gz[4];
-  load_ecl(gho, p.gho + (size_t)r * HID, g);
-  inv = cs_split(gho, xh, xl);
-  mm_node<false>(gz, W(BH_WN2T), xh, xl, inv, lane, us(BH_WN2T));
-  mul_dsilu(gz, zp);
-  inv = cs_split(gz, xh, xl);
-  mm_node<true>(gh, W(BH_WN1TH), xh, xl, inv, lane, us(BH_WN1TH));
-  f4 gM[4];
-  mm_node<false>(gM, W(BH_WN1TM), xh, xl, inv, lane, us(BH_WN1TM));
-  if (valid) {
-    const size_t o = (size_t)r * HID;
-    store_ecl(p.ghp + o, gh, g);
-    store_ecl(p.gM + o, gM, g);
-    store_ecl(p.op_gt + o, gt, g);
-    store_ecl(p.op_t + o, t, g);
-    store_ecl(p.op_z + o, z, g);
-    store_ecl(p.op_gz + o, gz, g);
-    const f4 z4[4] = {};
-    store_ecl(p.GB + o, z4, g);                          // the edge backward's sender sums start at 0
-    if (g == 0) {
-      p.gv[(size_t)r * 3 + 0] = p.gvo[(size_t)r * 3 + 0] + phi * gx0;
-      p.gv[(size_t)r * 3 + 1] = p.gvo[(size_t)r * 3 + 1] + phi * gx1;
-      p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
-      *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
-      *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = f4{0.f, 0.f, 0.f, 0.f};
-      p.op_gphi[r] = gphi;
-    }
-  }
-  }
-}
-#else
-// exact f32 MFMAs: the six node-side f32 fragment matrices (WV1, WN1, WV1^T, WN2^T, WN1^T h / m)
-constexpr int NB_LDS_FLOATS = (BOFF_WN1 + 8192 - BOFF_WV1) + (BOFF_WN1TM + 4096 - BOFF_WV1T);   // 28672
-__global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
-  {
-    const float* bb = p.bb;
-    constexpr int n1 = BOFF_WN1 + 8192 - BOFF_WV1, n2 = BOFF_WN1TM + 4096 - BOFF_WV1T;
-    const f4* s1 = reinterpret_cast<const f4*>(bb + BOFF_WV1);
-    const f4* s2 = reinterpret_cast<const f4*>(bb + BOFF_WV1T);
-    for (int i = threadIdx.x; i < n1 / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem)[i] = s1[i];
-    for (int i = threadIdx.x; i < n2 / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem + n1)[i] = s2[i];
-  }
-  __syncthreads();
-  const float* sWV1_ = smem;                                  // [BOFF_WV1, BOFF_WN1 + 8192) staged
-  const float* sWN1_ = smem + (BOFF_WN1 - BOFF_WV1);
-  const float* sT = smem + (BOFF_WN1 + 8192 - BOFF_WV1);    // [BOFF_WV1T, BOFF_WN1TM + 4096) staged
-  const float* sWV1T_ = sT;
-  const float* sWN2T_ = sT + (BOFF_WN2T - BOFF_WV1T);
-  const float* sWN1TH_ = sT + (BOFF_WN1TH - BOFF_WV1T);
-  const float* sWN1TM_ = sT + (BOFF_WN1TM - BOFF_WV1T);
-  const int ntile = (p.n + 15) >> 4;
-#pragma unroll 1
-  for (int tile = blockIdx.x * NB_WAVES + wave; tile < ntile; tile += gridDim.x * NB_WAVES) {
-  // loop-invariant weight reads stay in the loop (hoisted, the bias vectors and fragments would
-  // pin registers across the tiles and spill): opaque zero offset
-  int off = 0;
-  asm volatile("" : "+v"(off));
-  const float* bb = p.bb + off;
-  const float* sWV1 = sWV1_ + off;
-  const float* sWN1 = sWN1_ + off;
-  const float* sWV1T = sWV1T_ + off;
-  const float* sWN2T = sWN2T_ + off;
-  const float* sWN1TH = sWN1TH_ + off;
-  const float* sWN1TM = sWN1TM_ + off;
-  const int r0 = tile * 16;
-  const int r = min(r0 + e, p.n - 1);
-  const bool valid = r0 + e < p.n;
-  f4 hr[4], Mr[4];
-  load_ecl(hr, p.h + (size_t)r * HID, g);
-  load_ecl(Mr, p.M + (size_t)r * HID, g);
-  // phi_v(h) = wv2 . SiLU(WV1 h + bv1) + bv2
-  f4 tp[4];
-  load_vp(tp, bb + BOFF_VEC + BV_BV1 * 64, g);
-  mfma_dense<4>(tp, sWV1, hr, lane);
-  f4 t[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) t[mt] = tp[mt];
-  silu_true(t);
-  const float phi = dot_vp(t, bb + BOFF_VEC + BV_WV2 * 64, g) + bb[BOFF_SCAL + 1];
-  const float gx0 = p.gxo[(size_t)r * 3 + 0], gx1 = p.gxo[(size_t)r * 3 + 1], gx2 = p.gxo[(size_t)r * 3 + 2];
-  const float v0 = p.v[(size_t)r * 3 + 0], v1 = p.v[(size_t)r * 3 + 1], v2 = p.v[(size_t)r * 3 + 2];
-  const float gphi = gx0 * v0 + gx1 * v1 + gx2 * v2;
-  // clamp(F / (N-1), +-100) passes the gradient inside [-100, 100]
-  const float inv = 1.f / (float)(p.N - 1);
-  const float F0 = p.F[(size_t)r * 4 + 0] * inv, F1 = p.F[(size_t)r * 4 + 1] * inv, F2 = p.F[(size_t)r * 4 + 2] * inv;
-  const float gF0 = (F0 >= -100.f && F0 <= 100.f) ? gx0 * inv : 0.f;
-  const float gF1 = (F1 >= -100.f && F1 <= 100.f) ? gx1 * inv : 0.f;
-  const float gF2 = (F2 >= -100.f && F2 <= 100.f) ? gx2 * inv : 0.f;
-  // gt_pre = gphi * wv2 (.) silu'(tp);  gh = WV1^T gt_pre
-  f4 gt[4];
-  load_vp(gt, bb + BOFF_VEC + BV_WV2 * 64, g);
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) gt[mt] *= gphi;
-  mul_dsilu(gt, tp);
-  f4 gh[4];
-  zero4(gh);
-  mfma_dense<4>(gh, sWV1T, gt, lane);
-  // node MLP: z = SiLU(WN1 [h, M] + bn1), h' = WN2 z + bn2
-  f4 in8[8];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
-  f4 zp[4];
-  load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
-  mfma_dense<8>(zp, sWN1, in8, lane);
-  f4 z[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
-  silu_true(z);
-  f4 gho[4], gz[4];
-  load_ecl(gho, p.gho + (size_t)r * HID, g);
-  zero4(gz);
-  mfma_dense<4>(gz, sWN2T, gho, lane);
-  mul_dsilu(gz, zp);
-  mfma_dense<4>(gh, sWN1TH, gz, lane);
-  f4 gM[4];
-  zero4(gM);
-  mfma_dense<4>(gM, sWN1TM, gz, lane);
-  if (valid) {
-    const size_t o = (size_t)r * HID;
-    store_ecl(p.ghp + o, gh, g);
-    store_ecl(p.gM + o, gM, g);
-    store_ecl(p.op_gt + o, gt, g);
-    store_ecl(p.op_t + o, t, g);
-    store_ecl(p.op_z + o, z, g);
-    store_ecl(p.op_gz + o, gz, g);
-    const f4 z4[4] = {};
-    store_ecl(p.GB + o, z4, g);                          // the edge backward's sender sums start at 0
-    if (g == 0) {
-      p.gv[(size_t)r * 3 + 0] = p.gvo[(size_t)r * 3 + 0] + phi * gx0;
-      p.gv[(size_t)r * 3 + 1] = p.gvo[(size_t)r * 3 + 1] + phi * gx1;
-      p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
-      *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
-      *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = f4{0.f, 0.f, 0.f, 0.f};
-      p.op_gphi[r] = gphi;
-    }
-  }
-  }
-}
-
-#endif
-
-int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s) {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    hipFuncSetAttribute((const void*)node_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, NB_LDS_FLOATS * 4);
-  });
-  const int want = (ntile + NB_WAVES - 1) / NB_WAVES;
-  const int G = want < num_cus() ? want : num_cus();
-  hipLaunchKernelGGL(node_bwd_kernel, dim3(G), dim3(NB_WAVES * 64), NB_LDS_FLOATS * 4, s, a);
-  return check_launch("node_bwd_kernel");
 }
 
 // ---- edge backward (basic.py:107-144, 167-173 reversed) ----------------------------------------
@@ -1904,40 +1538,6 @@ int launch_edge_bwd(int ne, EdgeBwdArgs a, int G, hipStream_t s) {
   return fail(NONODE_EUNSUPPORTED, "edge_bwd: n_edge_feat=%d", ne);
 }
 
-// gh = ghp + W_A^T GA + W_B^T GB ;  gx = gxo + GX
-__global__ __launch_bounds__(256) void node_post_kernel(int n, const float* ghp, const float* GA, const float* GB,
-                                                        const float* gxo, const float* GX, const float* bb,
-                                                        float* gh, float* gx) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
-  const int r0 = (blockIdx.x * 4 + wave) * 16;
-  if (r0 >= n) return;
-  const int r = min(r0 + e, n - 1);
-  f4 acc[4], ga[4], gb[4];
-  load_ecl(acc, ghp + (size_t)r * HID, g);
-  load_ecl(ga, GA + (size_t)r * HID, g);
-  load_ecl(gb, GB + (size_t)r * HID, g);
-  mfma_dense<4>(acc, bb + BOFF_WAT, ga, lane);
-  mfma_dense<4>(acc, bb + BOFF_WBT, gb, lane);
-  if (r0 + e < n) {
-    store_ecl(gh + (size_t)r * HID, acc, g);
-    if (g < 3) gx[(size_t)r * 3 + g] = gxo[(size_t)r * 3 + g] + GX[(size_t)r * 4 + g];
-  }
-}
-
-// ---- TimeConv reverse (layer_no.py:80-126; oracle/egno_grad.py spectral_bwd) -------------------
-// Persistent: each 4-wave workgroup walks 16-column tiles (columns c = (b, n)). Per tile:
-//   1. DFT of the input h (wave w: input channels 16w..16w+15) -> sX (the forward's layout);
-//   2. (no forward recompute: the LeakyReLU decisions come from the forward, TrainState::mask);
-//   3. gy[t] = gout[t] * leaky'(y[t]);  gYr_m = (c_m/T) sum_t cos gy,  gYi_m = -(c_m/T) sum_t sin gy
-//      -> sG (zero for columns past BN);
-//   4. backward mixing on MFMA: gXr = Wr gYr + Wi gYi, gXi = -Wi gYr + Wr gYi (wave w: input
-//      channels 16w..) and gh[t] = gout[t] + sum_m (gXr_m cos - gXi_m sin)   (Xi = -sum_t h sin);
-//   5. weight gradient: gWr_m += Xr (x) gYr + Xi (x) gYi,  gWi_m += -Xi (x) gYr + Xr (x) gYi over the
-//      tile's columns (K = columns, read straight from sX / sG with channels along lane & 15),
-//      wave w owning rows i = 16w..16w+15.
-// One partial per workgroup [M][re|im][64][64]; tconv_wgrad_reduce adds them in a fixed order.
-constexpr int TB_MAX_BLOCKS = 256;
-
 // backward mixing fragments: mode m < M, c = re|im: frag(mo, mt)[lane][q] = W[i][o][m][c] with
 // i = 16 mo + (l & 15), o = 16 mt + 4 (l >> 4) + q  (A operand over o, unscaled)
 __global__ void tconv_pack_bwd_kernel(const float* w, int Mfull, int M, float* out) {
@@ -1948,180 +1548,6 @@ __global__ void tconv_pack_bwd_kernel(const float* w, int Mfull, int M, float* o
   const int q = r & 3, l = (r >> 2) & 63, rest = r >> 8, mt = rest & 3, mo = rest >> 2;
   const int i = 16 * mo + (l & 15), o = 16 * mt + 4 * (l >> 4) + q;
   out[d] = w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
-}
-
-struct TconvBwdArgs {
-  int BN, T, M, ntiles;
-  const float* h;      // TimeConv input [T][BN][64]
-  const float* gout;   // gradient of its output
-  const float* wp;     // forward fragments (tconv_pack_kernel layout)
-  const float* wb;     // backward fragments (tconv_pack_bwd_kernel layout)
-  float* gh;           // gradient of the input
-  float* wpart;        // [grid][M][2][64][64]
-  const unsigned long long* mask;   // the forward's LeakyReLU decisions (TconvArgs::mask_out layout)
-};
-
-// LDS: sX [2 MM - 1][16][ROWP] (Xr_0, (Xr_m, Xs_m)), sG [2 MM][16][ROWP] ((gYr_m, gYi_m)), sCos / sSin
-// [MM * TMAX]: dynamic (83 KB at 5 modes, 152 KB at 9: beyond the 64 KB of static LDS)
-constexpr size_t tconv_bwd_lds_bytes(int MM) {
-  return ((size_t)(4 * MM - 1) * 16 * ROWP + 2 * (size_t)MM * TMAX) * sizeof(float);
-}
-template <int MM>
-__global__ __launch_bounds__(256) void tconv_bwd_kernel(TconvBwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float tb_smem[];
-  typedef float Row[16][ROWP];
-  Row* sX = reinterpret_cast<Row*>(tb_smem);
-  Row* sG = sX + (2 * MM - 1);
-  float* sCos = reinterpret_cast<float*>(sG + 2 * MM);
-  float* sSin = sCos + MM * TMAX;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
-  const int T = p.T, BN = p.BN;
-  if (tid < MM * T) {
-    const int m = tid / T, t = tid - (tid / T) * T;
-    const double ang = 2.0 * (double)m * (double)t / (double)T;
-    sCos[m * TMAX + t] = (float)cospi(ang);
-    sSin[m * TMAX + t] = (float)sinpi(ang);
-  }
-  const int ch = 16 * wave + 4 * g;   // this lane's 4 channels (input side and output side)
-  f4 aR[MM][4], aI[MM][4];            // gWr_m / gWi_m rows 16 wave.., column tiles it
-#pragma unroll
-  for (int m = 0; m < MM; ++m)
-#pragma unroll
-    for (int it = 0; it < 4; ++it) aR[m][it] = aI[m][it] = f4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();
-  for (int tile = blockIdx.x; tile < p.ntiles; tile += gridDim.x) {
-    const int col = tile * 16 + e;
-    const bool cvalid = col < BN;
-    const int c = cvalid ? col : BN - 1;
-    auto hval = [&](const float* base, int t) -> f4 {
-      return *reinterpret_cast<const f4*>(base + ((size_t)t * BN + c) * 64 + ch);
-    };
-    // ---- 1: DFT ----
-    {
-      f4 Xr[MM], Xs[MM];
-#pragma unroll
-      for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          const f4 hv = hval(p.h, t);
-#pragma unroll
-          for (int m = 0; m < MM; ++m) {
-            Xr[m] += hv * sCos[m * TMAX + t];
-            if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
-          }
-        }
-      }
-      *reinterpret_cast<f4*>(&sX[0][e][ch]) = Xr[0];
-#pragma unroll
-      for (int m = 1; m < MM; ++m) {
-        *reinterpret_cast<f4*>(&sX[2 * m - 1][e][ch]) = Xr[m];
-        *reinterpret_cast<f4*>(&sX[2 * m][e][ch]) = Xs[m];
-      }
-    }
-    __syncthreads();
-    auto mix = [&](f4& acc, const float* frags, int mat, const float (*src)[ROWP]) {
-      f4 in[4];
-      load_ecl(in, &src[e][0], g);
-      const float* wf = frags + (size_t)mat * 4096;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const f4 a = *reinterpret_cast<const f4*>(wf + ((wave * 4 + mt) * 64 + lane) * 4);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
-      }
-    };
-    // the forward's LeakyReLU decisions for this lane's element (column e, channels ch..ch+3): word
-    // ((t * ntiles + tile) * 4 + e / 4) * 4 + q, bit ((e & 3) << 4) | (ch >> 2)
-    const unsigned long long* mrow = p.mask + ((size_t)tile * 4 + (e >> 2)) * 4;
-    const int mbit = ((e & 3) << 4) | (ch >> 2);
-    const size_t mstride = (size_t)p.ntiles * 16;
-    // ---- 3: gy and its spectral coefficients ----
-    {
-      f4 gR[MM], gI[MM];
-#pragma unroll
-      for (int m = 0; m < MM; ++m) { gR[m] = f4{0.f, 0.f, 0.f, 0.f}; gI[m] = gR[m]; }
-#pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          f4 gy = hval(p.gout, t);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) gy[q] *= ((mrow[t * mstride + q] >> mbit) & 1) ? 1.f : 0.01f;
-#pragma unroll
-          for (int m = 0; m < MM; ++m) {
-            gR[m] += gy * sCos[m * TMAX + t];
-            gI[m] -= gy * sSin[m * TMAX + t];
-          }
-        }
-      }
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
-        const f4 z = {0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f4*>(&sG[2 * m][e][ch]) = cvalid ? gR[m] * cm : z;
-        *reinterpret_cast<f4*>(&sG[2 * m + 1][e][ch]) = cvalid ? gI[m] * cm : z;
-      }
-    }
-    __syncthreads();
-    // ---- 4: backward mixing (input tile mo = wave) and gh ----
-    {
-      f4 gXr[MM], gXi[MM];
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        gXr[m] = f4{0.f, 0.f, 0.f, 0.f};
-        gXi[m] = f4{0.f, 0.f, 0.f, 0.f};
-        mix(gXr[m], p.wb, 2 * m + 0, sG[2 * m]);       //  Wr gYr
-        mix(gXr[m], p.wb, 2 * m + 1, sG[2 * m + 1]);   //  Wi gYi
-        mix(gXi[m], p.wb, 2 * m + 0, sG[2 * m + 1]);   //  Wr gYi
-        f4 t = {0.f, 0.f, 0.f, 0.f};
-        mix(t, p.wb, 2 * m + 1, sG[2 * m]);            //  Wi gYr
-        gXi[m] -= t;
-      }
-      if (cvalid) {
-#pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-          if (t < T) {
-            f4 o = hval(p.gout, t);
-#pragma unroll
-            for (int m = 0; m < MM; ++m) o += gXr[m] * sCos[m * TMAX + t] - gXi[m] * sSin[m * TMAX + t];
-            *reinterpret_cast<f4*>(p.gh + ((size_t)t * BN + c) * 64 + ch) = o;
-          }
-        }
-      }
-    }
-    // ---- 5: weight gradient over this tile's 16 columns ----
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int row = 4 * g + ks;
-#pragma unroll
-      for (int m = 0; m < MM; ++m) {
-        const float xr = sX[m == 0 ? 0 : 2 * m - 1][row][16 * wave + e];
-        const float xs = m == 0 ? 0.f : sX[2 * m][row][16 * wave + e];
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
-          const float gyr = sG[2 * m][row][16 * it + e], gyi = sG[2 * m + 1][row][16 * it + e];
-          aR[m][it] = mfma(xr, gyr, aR[m][it]);          // Xr gYr
-          aI[m][it] = mfma(xr, gyi, aI[m][it]);          // Xr gYi
-          if (m > 0) {
-            aR[m][it] = mfma(-xs, gyi, aR[m][it]);       // + Xi gYi  (Xi = -Xs)
-            aI[m][it] = mfma(xs, gyr, aI[m][it]);        // - Xi gYr
-          }
-        }
-      }
-    }
-    __syncthreads();
-  }
-  float* wp = p.wpart + (size_t)blockIdx.x * p.M * 2 * 4096;
-#pragma unroll
-  for (int m = 0; m < MM; ++m)
-#pragma unroll
-    for (int it = 0; it < 4; ++it)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int i = 16 * wave + 4 * g + q, o = 16 * it + e;
-        wp[((m * 2 + 0) * 64 + i) * 64 + o] = aR[m][it][q];
-        wp[((m * 2 + 1) * 64 + i) * 64 + o] = aI[m][it][q];
-      }
 }
 
 // the TimeConv_x weight gradient from tconvx_bwd_kernel's per-block sums [nb][io][MMAX_T][2]: one block adds
@@ -2174,33 +1600,6 @@ __global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int
   for (int q = 0; q < 16; ++q) tot += red[q][oq][c4];
   const int mc = d >> 12, r = d & 4095, m = mc >> 1, c = mc & 1, i = r >> 6, o = r & 63;
   dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = tot;
-}
-
-int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
-  auto go = [&](auto mm) {
-    constexpr int MM = decltype(mm)::value;
-    static std::once_flag once;
-    std::call_once(once, [] {
-      hipFuncSetAttribute((const void*)tconv_bwd_kernel<MM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)tconv_bwd_lds_bytes(MM));
-    });
-    hipLaunchKernelGGL(tconv_bwd_kernel<MM>, dim3(G), dim3(256), tconv_bwd_lds_bytes(MM), s, a);
-  };
-  switch (M) {
-    case 1: go(std::integral_constant<int, 1>{}); break;
-    case 2: go(std::integral_constant<int, 2>{}); break;
-    case 3: go(std::integral_constant<int, 3>{}); break;
-    case 4: go(std::integral_constant<int, 4>{}); break;
-    case 5: go(std::integral_constant<int, 5>{}); break;   // num_modes = 5 (model_confs.yaml:12)
-    case 6: go(std::integral_constant<int, 6>{}); break;
-#if NONODE_MMAX_T >= 9
-    case 7: go(std::integral_constant<int, 7>{}); break;
-    case 8: go(std::integral_constant<int, 8>{}); break;
-    case 9: go(std::integral_constant<int, 9>{}); break;
-#endif
-    default: return fail(NONODE_EUNSUPPORTED, "tconv_bwd: modes=%d", M);
-  }
-  return check_launch("tconv_bwd_kernel");
 }
 
 // TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. Writes gx, gv.
@@ -2404,21 +1803,6 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
   gemm_tn_body<V4>(G, ldg, M, A, lda, N, K, kslice, partial);
 }
 
-// Several 64x64 weight-gradient GEMMs over the same K rows in one launch (blockIdx.y = GEMM): their
-// waves are in flight together, which hides the row-load latency a single small GEMM exposes, and
-// one launch replaces several. GEMM j writes its block partials at partial + j * pstride.
-constexpr int GEMM_BATCH_MAX = 6;
-struct GemmBatchArgs {
-  const float* G[GEMM_BATCH_MAX]; const float* A[GEMM_BATCH_MAX];
-  int ldg[GEMM_BATCH_MAX], lda[GEMM_BATCH_MAX];
-  long long K, kslice, pstride;
-  float* partial;
-};
-__global__ __launch_bounds__(256) void gemm_tn_batch(GemmBatchArgs a) {
-  const int j = blockIdx.y;
-  gemm_tn_body<true>(a.G[j], a.ldg[j], 64, a.A[j], a.lda[j], 64, a.K, a.kslice, a.partial + (size_t)j * a.pstride);
-}
-
 // dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
 // partial[b][i][N]. 256 threads = 16 outputs x 16 strided partial sums, combined in a fixed order
 // (deterministic).
@@ -2519,36 +1903,6 @@ struct Gemm {
                        cs, bias, accumulate, scale, split, col1, (long long)NO);
     return check_launch("gemm_reduce");
   }
-  // count 64x64 GEMMs C_j = sum_k G_j[k] (x) A_j[k] over the same K rows in one launch (gemm_tn_batch);
-  // their reductions are appended to red[] (*nred) for one launch_reduce_batch by the caller
-  struct Job { const float* G; int ldg; const float* A; int lda; float* dst; int ld, col0; float* bias; int accumulate; };
-  int batch(const Job* jobs, int count, long long K, ReduceJob* red, int* nred) const {
-    if (count > GEMM_BATCH_MAX) return fail(NONODE_EINVAL, "gemm batch of %d", count);
-    if (K <= 0) return NONODE_OK;
-    GemmBatchArgs a{};
-    for (int j = 0; j < count; ++j) {
-      const Job& b = jobs[j];
-      if (b.ldg % 4 || b.lda % 4 || ((uintptr_t)b.G & 15) || ((uintptr_t)b.A & 15))
-        return fail(NONODE_EINVAL, "gemm batch: unaligned operand");
-      a.G[j] = b.G; a.A[j] = b.A; a.ldg[j] = b.ldg; a.lda[j] = b.lda;
-    }
-    long long waves = (K + 31) / 32;
-    if (waves > max_waves) waves = max_waves;
-    long long kslice = (K + waves - 1) / waves;
-    kslice = (kslice + 4 * GEMM_UNR - 1) / (4 * GEMM_UNR) * (4 * GEMM_UNR);
-    waves = (K + kslice - 1) / kslice;
-    const int nblk = (int)((waves + 3) / 4);
-    constexpr int NO = 64 * 65;
-    a.K = K; a.kslice = kslice; a.pstride = (long long)nblk * NO; a.partial = partial;
-    hipLaunchKernelGGL(gemm_tn_batch, dim3(nblk, count), dim3(256), 0, s, a);
-    if (int rc = check_launch("gemm_tn_batch")) return rc;
-    for (int j = 0; j < count; ++j) {
-      const Job& b = jobs[j];
-      red[(*nred)++] = ReduceJob{partial + (size_t)j * a.pstride, nblk, 64, 64, b.dst, b.ld, b.col0, 1, b.bias,
-                                 b.accumulate, 1.f, 1 << 30, 0, (long long)NO};
-    }
-    return NONODE_OK;
-  }
 };
 
 // ---- state layout of the training forward ---------------------------------------------------------
@@ -2605,7 +1959,10 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take((BN * 3 + TX_THREADS - 1) / TX_THREADS * (2 * 2 * MMAX_T * 2));   // one row per tconvx block
-  w.partial = take((size_t)GEMM_BATCH_MAX * (GEMM_MAX_WAVES / 4 + 1) * 64 * 65);   // gemm_tn_batch partials
+  // gemm_tn_partial partials (one per block), or node_wgrad_kernel's (one [NW_JOBS][64][65] per block)
+  const size_t gparts = (size_t)(GEMM_MAX_WAVES / 4 + 1) * 64 * 65;
+  const size_t nparts = (size_t)nonode_tu::NW_MAX_BLOCKS * nonode_tu::NW_JOBS * nonode_tu::NW_PART;
+  w.partial = take(gparts > nparts ? gparts : nparts);
   w.floats = tot;
   return w;
 }
@@ -2644,7 +2001,7 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   a.ne = n_edge_feat;
   a.flags = flags;
   a.blob = bblob;
-  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 29), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 31), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("pack_bwd_kernel");
 }
 
@@ -2770,7 +2127,7 @@ struct LayerRev {
   const nonode_layer_grads* lg;
   float *g_xin, *g_vin, *g_hin;
 };
-int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, const Gemm& gemm, hipStream_t s) {
+int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
   const size_t n = (size_t)r.n;
   const int N = r.N, ne = r.ne, ld1 = 2 * HID + 1 + ne;
   const nonode_layer_grads& lg = *r.lg;
@@ -2807,24 +2164,31 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, const Gemm& gemm, hipS
     // edge Linear 1 scalar columns [s | e] (EGNO order [s, h_i, h_j, e], basic.py:152-154, 170)
     red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1);
   }
-  hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, r.n, w.ghp, w.GA, w.GB, r.gx,
-                     w.GX, r.bb, r.g_hin, r.g_xin);
-  if (int rc = check_launch("node_post_kernel")) return rc;
-  // ---- node-level weight gradients of this layer: six 64x64 GEMMs in one launch, their and the
-  // edge-level reductions in another ----
+  {
+    nonode_tu::NodePostArgs pa{r.n, w.ghp, w.GA, w.GB, r.gx, w.GX, r.bb, r.g_hin, r.g_xin};
+    if (int rc = nonode_tu::launch_node_post(pa, s)) return rc;
+  }
+  // ---- node-level weight gradients of this layer: one node_wgrad_kernel launch (NodeWgradArgs),
+  // its and the edge-level reductions in another ----
   // edge Linear 1 h_i / h_j blocks; its bias gradient sum_e gz1 = sum_i GA_i comes with the h_i block
   {
-    const Gemm::Job jobs[6] = {
-        {w.GA, 64, r.he, 64, lg.edge_w1, ld1, 1, lg.edge_b1, 0},
-        {w.GB, 64, r.he, 64, lg.edge_w1, ld1, 1 + HID, nullptr, 0},
-        {w.op_gt, 64, r.he, 64, lg.vel_w1, 64, 0, lg.vel_b1, 0},
-        {w.op_gz, 64, r.he, 64, lg.node_w1, 128, 0, lg.node_b1, 0},
-        {w.op_gz, 64, r.Ms, 64, lg.node_w1, 128, HID, nullptr, 0},
-        {r.gh, 64, w.op_z, 64, lg.node_w2, 64, 0, lg.node_b2, 0}};
-    if (int rc = gemm.batch(jobs, 6, (long long)n, rjobs, &nred)) return rc;
-    if (int rc = launch_reduce_batch(rjobs, nred, s)) return rc;
+    nonode_tu::NodeWgradArgs wa{};
+    wa.n = (long long)n;
+    wa.h = r.he; wa.M = r.Ms; wa.z = w.op_z; wa.t = w.op_t;
+    wa.GA = w.GA; wa.GB = w.GB; wa.gt = w.op_gt; wa.gz = w.op_gz; wa.gh = r.gh; wa.gphi = w.op_gphi;
+    wa.partial = w.partial;
+    int nblk = 0;
+    if (int rc = nonode_tu::launch_node_wgrad(wa, &nblk, s)) return rc;
+    struct { float* dst; int ld, col0; float* bias; } d[nonode_tu::NW_JOBS] = {
+        {lg.edge_w1, ld1, 1, lg.edge_b1}, {lg.edge_w1, ld1, 1 + HID, nullptr}, {lg.vel_w1, 64, 0, lg.vel_b1},
+        {lg.node_w1, 128, 0, lg.node_b1}, {lg.node_w1, 128, HID, nullptr},   {lg.node_w2, 64, 0, lg.node_b2},
+        {lg.vel_w2, 64, 0, lg.vel_b2}};
+    constexpr long long pstride = (long long)nonode_tu::NW_JOBS * nonode_tu::NW_PART;
+    for (int j = 0; j < nonode_tu::NW_JOBS; ++j)
+      rjobs[nred++] = ReduceJob{w.partial + (size_t)j * nonode_tu::NW_PART, nblk, j < 6 ? 64 : 1, 64, d[j].dst,
+                                d[j].ld, d[j].col0, 1, d[j].bias, 0, 1.f, 1 << 30, 0, pstride};
+    return launch_reduce_batch(rjobs, nred, s);
   }
-  return gemm(w.op_gphi, 1, 1, w.op_t, 64, 64, (long long)n, lg.vel_w2, 64, 0, lg.vel_b2);
 }
 
 // Reverse of TimeConv + TimeConv_x of one EGNO layer (layer_no.py:80-178, egno.py:99-108): given the
@@ -2857,7 +2221,8 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   ta.mask = r.mask;
   int TG = num_cus();
   TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;
-  TG = ta.ntiles < TG ? ta.ntiles : TG;
+  const int tgw = (ta.ntiles + tb_groups(M) - 1) / tb_groups(M);   // workgroups: tb_groups(M) tiles each per trip
+  TG = tgw < TG ? tgw : TG;
   if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
   if (modes > M) hipMemsetAsync(r.g_tw, 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
   hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 / 4 + 15) / 16), dim3(256), 0, s, w.tpart, TG, M, modes,
@@ -2909,7 +2274,7 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     lr.edge_fea = edge_fea; lr.bb = bblobs[l];
     lr.gx = gx; lr.gv = gv; lr.gh = gh; lr.lg = &layer_grads[l];
     lr.g_xin = w.gxe; lr.g_vin = w.gve; lr.g_hin = w.ghe;
-    if (int rc = egnn_layer_reverse(lr, w, gemm, s)) return rc;
+    if (int rc = egnn_layer_reverse(lr, w, s)) return rc;
     const int nxt = cur ^ 1;
     if (!tc) {   // no TimeConv: the layer-input gradients are the next (earlier) layer's output gradients
       hipMemcpyAsync(w.gx[nxt], w.gxe, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -3124,7 +2489,6 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
   const size_t n = (size_t)B * N;
   const SegnoState st = segno_state(const_cast<void*>(state), B, N, T);
   BwdWs w = bwd_ws(workspace, B, N, 1, 1);
-  Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
   float *gx = w.gx[0], *gv = w.gv[0], *gh = w.gh[0];
   if (g_x) hipMemcpyAsync(gx, g_x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   else hipMemsetAsync(gx, 0, n * 3 * sizeof(float), s);
@@ -3155,6 +2519,8 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
     if (int rc = check_launch("segno_node_bwd_kernel")) return rc;
     hipMemsetAsync(w.GB, 0, n * 64 * sizeof(float), s);
     hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
+    ReduceJob rj[REDUCE_BATCH_MAX];   // the substep's edge- and node-level reductions: one launch
+    int nrj = 0;
     {
       const int G = edge_bwd_grid(B);
       EdgeBwdArgs ea;
@@ -3165,26 +2531,38 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       ea.stash = w.stash; ea.stash_c = w.stash_c; ea.Pn = w.Pn; ea.Qn = w.Qn;
       if (int rc = launch_edge_bwd(ne, ea, G, s)) return rc;
       auto red = [&](int off, int M_, int N_, float* dst, int ld, float* bias, int col0) {
-        const int NO = M_ * (N_ + 1);
-        hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, w.wpart + off, G, M_, N_, dst, ld,
-                           col0, 1, bias, acc, 1.f, 1 << 30, 0, (long long)EW_STRIDE);
-        return check_launch("gemm_reduce(segno edge)");
+        rj[nrj++] = ReduceJob{w.wpart + off, G, M_, N_, dst, ld, col0, 1, bias, acc, 1.f, 1 << 30, 0,
+                              (long long)EW_STRIDE};
       };
-      if (int rc = red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 0)) return rc;
-      if (int rc = red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 0)) return rc;
-      if (int rc = red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 0)) return rc;
+      red(EW_W2, 64, 64, lg.edge_w2, 64, lg.edge_b2, 0);
+      red(EW_WC1, 64, 64, lg.coord_w1, 64, lg.coord_b1, 0);
+      red(EW_WC2, 1, 64, lg.coord_w2, 64, lg.coord_b2, 0);
       // edge Linear 1 scalar columns [s | e] (SEGNO order [h_i, h_j, s, e], gcl.py:78)
-      if (int rc = red(EW_FEAT, 64, 1 + ne, lg.edge_w1, ld1, nullptr, 2 * HID)) return rc;
+      red(EW_FEAT, 64, 1 + ne, lg.edge_w1, ld1, nullptr, 2 * HID);
     }
-    hipLaunchKernelGGL(node_post_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, (int)n, w.ghp, w.GA, w.GB, gx, w.GX,
-                       bblob, w.gh[nxt], w.gx[nxt]);
-    if (int rc = check_launch("node_post_kernel")) return rc;
-    // node-level weight gradients of this substep (edge Linear 1 h_i / h_j blocks, node MLP)
-    if (int rc = gemm(w.GA, 64, 64, hs, 64, 64, (long long)n, lg.edge_w1, ld1, 0, lg.edge_b1, acc)) return rc;
-    if (int rc = gemm(w.GB, 64, 64, hs, 64, 64, (long long)n, lg.edge_w1, ld1, HID, nullptr, acc)) return rc;
-    if (int rc = gemm(w.op_gz, 64, 64, hs, 64, 64, (long long)n, lg.node_w1, 128, 0, lg.node_b1, acc)) return rc;
-    if (int rc = gemm(w.op_gz, 64, 64, Ms, 64, 64, (long long)n, lg.node_w1, 128, HID, nullptr, acc)) return rc;
-    if (int rc = gemm(gh, 64, 64, w.op_z, 64, 64, (long long)n, lg.node_w2, 64, 0, lg.node_b2, acc)) return rc;
+    {
+      nonode_tu::NodePostArgs pa{(int)n, w.ghp, w.GA, w.GB, gx, w.GX, bblob, w.gh[nxt], w.gx[nxt]};
+      if (int rc = nonode_tu::launch_node_post(pa, s)) return rc;
+    }
+    // node-level weight gradients of this substep (edge Linear 1 h_i / h_j blocks, node MLP): one
+    // node_wgrad_kernel launch (jobs 0, 1, 3, 4, 5; no node_v MLP) and one reduction launch
+    {
+      nonode_tu::NodeWgradArgs wa{};
+      wa.n = (long long)n;
+      wa.h = hs; wa.M = Ms; wa.z = w.op_z; wa.t = nullptr;
+      wa.GA = w.GA; wa.GB = w.GB; wa.gt = nullptr; wa.gz = w.op_gz; wa.gh = gh; wa.gphi = nullptr;
+      wa.partial = w.partial;
+      int nblk = 0;
+      if (int rc = nonode_tu::launch_node_wgrad(wa, &nblk, s)) return rc;
+      struct { int job; float* dst; int ld, col0; float* bias; } d[5] = {
+          {0, lg.edge_w1, ld1, 0, lg.edge_b1}, {1, lg.edge_w1, ld1, HID, nullptr}, {3, lg.node_w1, 128, 0, lg.node_b1},
+          {4, lg.node_w1, 128, HID, nullptr}, {5, lg.node_w2, 64, 0, lg.node_b2}};
+      for (int j = 0; j < 5; ++j)
+        rj[nrj++] = ReduceJob{w.partial + (size_t)d[j].job * nonode_tu::NW_PART, nblk, 64, 64, d[j].dst, d[j].ld,
+                              d[j].col0, 1, d[j].bias, acc, 1.f, 1 << 30, 0,
+                              (long long)nonode_tu::NW_JOBS * nonode_tu::NW_PART};
+      if (int rc = launch_reduce_batch(rj, nrj, s)) return rc;
+    }
     cur = nxt;
     gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
   }
@@ -3234,13 +2612,12 @@ int nonode_egnn_layer_bwd(int variant, int n_graphs, int N, int n_edge_feat, int
   const float *gv = g_v, *gh = g_h;
   if (!g_v) { hipMemsetAsync(w.gv[0], 0, n * 3 * sizeof(float), s); gv = w.gv[0]; }
   if (!g_h) { hipMemsetAsync(w.gh[0], 0, n * 64 * sizeof(float), s); gh = w.gh[0]; }
-  Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
   LayerRev lr;
   lr.n = (int)n; lr.N = N; lr.n_graphs = n_graphs; lr.ef_mod = ef_mod; lr.ne = n_edge_feat;
   lr.he = h; lr.xe = x; lr.ve = v; lr.Ms = Ms; lr.Fs = Fs; lr.edge_fea = edge_fea; lr.bb = bblob;
   lr.gx = g_x; lr.gv = gv; lr.gh = gh; lr.lg = grads;
   lr.g_xin = g_x_in; lr.g_vin = g_v_in; lr.g_hin = g_h_in;
-  return egnn_layer_reverse(lr, w, gemm, s);
+  return egnn_layer_reverse(lr, w, s);
 }
 
 size_t nonode_egno_tconv_bwd_workspace_bytes(int BN, int T, int modes) {

@@ -40,8 +40,7 @@ def test_library_is_gfx950_code_object():
 
 def test_size_queries_need_no_gpu():
     L = pkg.lib()
-    # f32 / fp16 sections + the 32-column form's W2 | Wc1 fragments, feature columns and vectors
-    assert L.nonode_layer_blob_floats() == 33856 + 8192 + 6 * 4096 + 8192 + 512 + 256
+    assert L.nonode_layer_blob_floats() == 33856 + 8192 + 6 * 4096
     B, N, T = 512, 20, 10
     ws = L.nonode_egno_workspace_bytes(B, N, T, B)
     assert ws == (B * N * T * 67 + B * T * 64 + 64) * 4

@@ -1,5 +1,7 @@
 #!/bin/bash
-# build an A/B variant: bash tools/build_ab.sh <name> -DFLAG=VAL ...
+# build an A/B variant of the library (same units and flags as build()): bash tools/build_ab.sh <name> -DFLAG=VAL ...
+# (NONODE_SCHED="" builds nonode.hip with the default machine scheduler as well)
 cd "$(dirname "$0")/.."
 n=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-slp-vectorize -Wno-unused-value -mllvm -amdgpu-mfma-vgpr-form=1 ${SCHED--mllvm -amdgpu-sched-strategy=iterative-ilp} -I include "$@" -o ab/lib_$n.so no-node-comparison_amd/csrc/nonode.hip
+mkdir -p ab
+python3 -c "import sys; import __graft_entry__ as g; g.compile_lib(sys.argv[1], defines=sys.argv[2:])" "ab/lib_$n.so" "$@"

@@ -1,5 +1,4 @@
 #!/bin/bash
 # Diagnostic build with in-kernel s_memtime section stamps -> no-node-comparison_amd/libnonode_stamp.so
 cd "$(dirname "$0")/.."
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-slp-vectorize -Wno-unused-value -mllvm -amdgpu-mfma-vgpr-form=1 -mllvm -amdgpu-sched-strategy=iterative-ilp -I include -DNONODE_STAMP=1 \
-  -o no-node-comparison_amd/libnonode_stamp.so no-node-comparison_amd/csrc/nonode.hip
+python3 -c "import __graft_entry__ as g; g.compile_lib('no-node-comparison_amd/libnonode_stamp.so', defines=['-DNONODE_STAMP=1'])"
