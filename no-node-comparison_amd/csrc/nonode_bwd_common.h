@@ -115,6 +115,48 @@ __device__ __forceinline__ float amax16(const f4 (&x)[4]) {
     m[mt] = fmaxf(fmaxf(fabsf(x[mt][0]), fabsf(x[mt][1])), fmaxf(fabsf(x[mt][2]), fabsf(x[mt][3])));
   return fmaxf(fmaxf(m[0], m[1]), fmaxf(m[2], m[3]));
 }
+// max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors; no LDS round trip)
+template <int C>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_max16(float m) {
+  m = fmaxf(m, dppf<0xB1>(m));    // quad_perm [1, 0, 3, 2]
+  m = fmaxf(m, dppf<0x4E>(m));    // quad_perm [2, 3, 0, 1]
+  m = fmaxf(m, dppf<0x141>(m));   // row_half_mirror
+  return fmaxf(m, dppf<0x140>(m));  // row_mirror
+}
+// fp16x3 split of 4 values (as h16_split)
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void h4_split(f4 v, h4& hi, h4& lo) {
+  hi = __builtin_convertvector(v, h4);
+  const auto hw = __builtin_bit_cast(u2, hi);
+  const f4 r = {resid_lo(hw[0], v[0]), resid_hi(hw[0], v[1]), resid_lo(hw[1], v[2]), resid_hi(hw[1], v[3])};
+  lo = __builtin_convertvector(r, h4);
+}
+__device__ __forceinline__ float amax4(f4 v) {
+  return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
+// fp16 images [32 rows][64 halves] read back transposed (ds_read_b64_tr_b16) as K = 32 MFMA operands:
+// chunks of 8 halves XOR-swizzled per row (the edge backward's pair path and node_wgrad_kernel)
+constexpr int IMG_HALVES = 32 * 64;   // one image (hi or lo): 32 rows x 64 halves
+__device__ __forceinline__ int img_swz(int r) { return (((r >> 1) & 1) << 1) ^ ((r >> 2) & 1) ^ (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int img_off(int r, int chunk) { return r * 64 + 8 * (chunk ^ img_swz(r)); }   // halves
+typedef short s4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ h8 tr_read8(const _Float16* img, int t, int lane) {
+  // lane 4q + p of group gq reads row 8 gq + q (+ 4), image columns 16 t + 4p .. + 3
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = 16 * t + 4 * p;                     // image column of the 4 halves
+  const int r0 = 8 * gq + q, r1 = r0 + 4;
+  const _Float16* a0 = img + img_off(r0, c >> 3) + (c & 7);
+  const _Float16* a1 = img + img_off(r1, c >> 3) + (c & 7);
+  const s4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
+  const s4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a1));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  const s8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(h8, v);
+}
 }  // namespace
 
 namespace nonode_tu {

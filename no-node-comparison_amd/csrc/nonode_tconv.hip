@@ -12,8 +12,12 @@ using nonode_tu::tb_groups;
 
 // LDS per group: sX [2 MM - 1][16][ROWP] (Xr_0, (Xr_m, Xs_m)), sG [2 MM][16][ROWP] ((gYr_m, gYi_m));
 // shared sCos / sSin [MM * TMAX]: dynamic (93 KB at 2 modes x 3 groups, 152 KB at 9 modes x 1)
+// At <= 2 modes the backward mixing fragments (2 MM x 4096 floats) are staged in LDS once per
+// workgroup too: read from L2 they were 32 KB per wave and tile.
+constexpr bool tb_wlds(int MM) { return MM <= 2; }
 constexpr size_t tconv_bwd_lds_bytes(int MM) {
-  return ((size_t)tb_groups(MM) * (4 * MM - 1) * 16 * ROWP + 2 * (size_t)MM * TMAX) * sizeof(float);
+  return ((size_t)tb_groups(MM) * (4 * MM - 1) * 16 * ROWP + 2 * (size_t)MM * TMAX +
+          (tb_wlds(MM) ? (size_t)2 * MM * 4096 : 0)) * sizeof(float);
 }
 template <int MM>
 __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwdArgs p) {
@@ -26,7 +30,13 @@ __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwd
   Row* sG = sX + (2 * MM - 1);
   float* sCos = reinterpret_cast<float*>(reinterpret_cast<Row*>(tb_smem) + NG * (4 * MM - 1));
   float* sSin = sCos + MM * TMAX;
+  float* sWb = sSin + MM * TMAX;   // tb_wlds(MM): the backward mixing fragments
   const int T = p.T, BN = p.BN;
+  if constexpr (tb_wlds(MM)) {
+    for (int i = tid; i < 2 * MM * 1024; i += 256 * NG)
+      reinterpret_cast<f4*>(sWb)[i] = reinterpret_cast<const f4*>(p.wb)[i];
+  }
+  const float* wb = tb_wlds(MM) ? sWb : p.wb;
   if (tid < MM * T) {
     const int m = tid / T, t = tid - (tid / T) * T;
     const double ang = 2.0 * (double)m * (double)t / (double)T;
@@ -126,11 +136,11 @@ __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwd
       for (int m = 0; m < MM; ++m) {
         gXr[m] = f4{0.f, 0.f, 0.f, 0.f};
         gXi[m] = f4{0.f, 0.f, 0.f, 0.f};
-        mix(gXr[m], p.wb, 2 * m + 0, sG[2 * m]);       //  Wr gYr
-        mix(gXr[m], p.wb, 2 * m + 1, sG[2 * m + 1]);   //  Wi gYi
-        mix(gXi[m], p.wb, 2 * m + 0, sG[2 * m + 1]);   //  Wr gYi
+        mix(gXr[m], wb, 2 * m + 0, sG[2 * m]);       //  Wr gYr
+        mix(gXr[m], wb, 2 * m + 1, sG[2 * m + 1]);   //  Wi gYi
+        mix(gXi[m], wb, 2 * m + 0, sG[2 * m + 1]);   //  Wr gYi
         f4 t = {0.f, 0.f, 0.f, 0.f};
-        mix(t, p.wb, 2 * m + 1, sG[2 * m]);            //  Wi gYr
+        mix(t, wb, 2 * m + 1, sG[2 * m]);            //  Wi gYr
         gXi[m] -= t;
       }
       if (cvalid) {

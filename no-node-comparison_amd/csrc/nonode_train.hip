@@ -142,17 +142,6 @@ __global__ void pack_bwd_kernel(PackArgs a) {
   }
 }
 
-// max over the 16 lanes of a row (DPP: quad swaps, half-row and row mirrors; no LDS round trip)
-template <int C>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row_max16(float m) {
-  m = fmaxf(m, dppf<0xB1>(m));    // quad_perm [1, 0, 3, 2]
-  m = fmaxf(m, dppf<0x4E>(m));    // quad_perm [2, 3, 0, 1]
-  m = fmaxf(m, dppf<0x141>(m));   // row_half_mirror
-  return fmaxf(m, dppf<0x140>(m));  // row_mirror
-}
 // out += W x for a gradient column set x: each column scaled to [2^11, 2^12) before the split, the
 // product scaled back (per lane: lane (e, g) holds column e)
 __device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x)[4], int lane, unsigned us,
@@ -167,14 +156,6 @@ __device__ __forceinline__ void mm64_cs(f4 (&out)[4], const h8* wh, const f4 (&x
   mfma_h16(acc, wh, xh, xl, lane, us);
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) out[mt] += acc[mt] * inv;
-}
-typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-typedef unsigned u2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void h4_split(f4 v, h4& hi, h4& lo) {
-  hi = __builtin_convertvector(v, h4);
-  const auto hw = __builtin_bit_cast(u2, hi);
-  const f4 r = {resid_lo(hw[0], v[0]), resid_hi(hw[0], v[1]), resid_lo(hw[1], v[2]), resid_hi(hw[1], v[3])};
-  lo = __builtin_convertvector(r, h4);
 }
 __device__ __forceinline__ f4 mfma16k16(h4 a, h4 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
@@ -444,23 +425,6 @@ __device__ __forceinline__ void wgrad_h16(f4 (&acc)[4][4], float& sc, const f4 (
 // image-column order on both axes and un-permuted when it is written out (put_pair).
 // Chunks are XOR-swizzled per row (chunk ^ img_swz(row)): conflict-free transposed reads and 2-way
 // b128 writes (the minimum for 16 lanes x 16 bytes on 32 banks).
-constexpr int IMG_HALVES = 32 * 64;   // one image (hi or lo): 32 rows x 64 halves
-__device__ __forceinline__ int img_swz(int r) { return (((r >> 1) & 1) << 1) ^ ((r >> 2) & 1) ^ (((r >> 3) & 1) << 2); }
-__device__ __forceinline__ int img_off(int r, int chunk) { return r * 64 + 8 * (chunk ^ img_swz(r)); }   // halves
-typedef short s4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ h8 tr_read8(const _Float16* img, int t, int lane) {
-  // lane 4q + p of group gq reads row 8 gq + q (+ 4), image columns 16 t + 4p .. + 3
-  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int c = 16 * t + 4 * p;                     // image column of the 4 halves
-  const int r0 = 8 * gq + q, r1 = r0 + 4;
-  const _Float16* a0 = img + img_off(r0, c >> 3) + (c & 7);
-  const _Float16* a1 = img + img_off(r1, c >> 3) + (c & 7);
-  const s4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a0));
-  const s4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(a1));
-  typedef short s8 __attribute__((ext_vector_type(8)));
-  const s8 v = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-  return __builtin_bit_cast(h8, v);
-}
 // lane (e, g) writes its split of unit `u` (rows 16 u + e)
 __device__ __forceinline__ void img_put(_Float16* hi_img, _Float16* lo_img, const h8 (&hi)[2], const h8 (&lo)[2],
                                         int u, int e, int g) {
@@ -1550,32 +1514,26 @@ __global__ void tconv_pack_bwd_kernel(const float* w, int Mfull, int M, float* o
   out[d] = w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
 }
 
-// the TimeConv_x weight gradient from tconvx_bwd_kernel's per-block sums [nb][io][MMAX_T][2]: one block adds
-// the slices in order and writes g_tconvx [2][2][Mfull][2] whole (modes >= M zero), replacing a
-// memset and four copies
+// the TimeConv_x weight gradient from tconvx_bwd_kernel's per-block sums [nb][io][MMAX_T][2]: block d
+// (one per output of g_tconvx [2][2][Mfull][2], modes >= M zero) adds the nb partial rows' entry with
+// 256 threads (strided sums, then a fixed-order tree in LDS: deterministic). (One 256-thread block for
+// every output, three lanes per output, had made this a 21 us serial chain per C4 layer.)
 __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int nb, int M, int Mfull, float* dst) {
   constexpr int cnt = 2 * 2 * MMAX_T * 2;   // partial row length (72)
-  constexpr int NL = 256 / cnt;             // partial lanes per output (3)
-  __shared__ float red[NL][cnt];
-  const int o = threadIdx.x % cnt, lanei = threadIdx.x / cnt;
-  if (lanei < NL) {
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};   // independent sums: several partial rows in flight
-    for (int r = lanei; r < nb; r += 4 * NL)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (r + NL * j < nb) s4[j] += part[(size_t)(r + NL * j) * cnt + o];
-    red[lanei][o] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  __shared__ float red[256];
+  const int d = blockIdx.x, io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
+  float v = 0.f;
+  if (m < M) {
+    const int k = (io * MMAX_T + m) * 2 + c;
+    for (int r = threadIdx.x; r < nb; r += 256) v += part[(size_t)r * cnt + k];
   }
+  red[threadIdx.x] = v;
   __syncthreads();
-  for (int d = threadIdx.x; d < 4 * Mfull * 2; d += 256) {
-    const int io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
-    float v = 0.f;
-    if (m < M) {
-      const int k = (io * MMAX_T + m) * 2 + c;
-      for (int q = 0; q < NL; ++q) v += red[q][k];
-    }
-    dst[d] = v;
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) dst[d] = red[0];
 }
 
 // dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
@@ -2211,7 +2169,7 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   hipLaunchKernelGGL(txk, dim3(nbx), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
                      r.lm, r.gx, r.gv, r.txw, r.g_xin, r.g_vin, w.xpart, r.frames);
   if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
-  hipLaunchKernelGGL(tconvx_grad_finish, dim3(1), dim3(256), 0, s, w.xpart, nbx, M, modes, r.g_txw);
+  hipLaunchKernelGGL(tconvx_grad_finish, dim3(4 * modes * 2), dim3(256), 0, s, w.xpart, nbx, M, modes, r.g_txw);
   if (int rc = check_launch("tconvx_grad_finish")) return rc;
   hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, r.tw, modes, M, w.twb);
   if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
