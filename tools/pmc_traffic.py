@@ -26,7 +26,9 @@ def kernel_key(name):
     if "edge_bwd_kernel" in name:   # edge_bwd_kernel<NE, PASS>
         m = re.search(r"edge_bwd_kernel<\d+,\s*(\d+)>", name) or re.search(r"edge_bwd_kernelILi\d+ELi(\d+)E", name)
         return f"edge_bwd_kernel<pass {m.group(1)}>" if m else "edge_bwd_kernel"
-    for k in ("temb_kernel", "embed_kernel", "node_bwd_kernel", "node_post_kernel"):
+    if "tconv_bwd_kernel" in name:
+        return "tconv_bwd_kernel"
+    for k in ("temb_kernel", "embed_kernel", "node_bwd_kernel", "node_post_kernel", "node_wgrad_kernel"):
         if k in name:
             return k
     return None
