@@ -225,10 +225,7 @@ constexpr int MMAX_T = 9;   // training path: every rfft bin of T <= 16 (as the 
 constexpr int TB_MAX_BLOCKS = 256;
 // 4-wave tile groups per workgroup: two at <= 2 modes (three spill at the
 // 170 registers of three waves per SIMD), else one
-#ifndef NONODE_TB_NG
-#define NONODE_TB_NG 2
-#endif
-constexpr int tb_groups(int MM) { return MM <= 2 ? NONODE_TB_NG : 1; }
+constexpr int tb_groups(int MM) { return MM <= 2 ? 2 : 1; }
 struct TconvBwdArgs {
   int BN, T, M, ntiles;
   const float* h;      // TimeConv input [T][BN][64]

@@ -8,10 +8,6 @@ namespace {
 
 using nonode_tu::NodeBwdArgs;
 
-// fp16x3 node products (default; 0: the exact f32 MFMA form, kept for the A/B of DESIGN.md section 3.4)
-#ifndef NONODE_NODE_H16
-#define NONODE_NODE_H16 1
-#endif
 // column-scaled fp16x3 split of a 16-column operand (as mm64_cs); returns the inverse scale
 __device__ __forceinline__ float cs_split(const f4 (&x)[4], h8 (&xh)[2], h8 (&xl)[2]) {
   const float sc = p2scale(col_max(amax16(x)));
@@ -37,7 +33,6 @@ __device__ __forceinline__ void mm_node(f4 (&out)[4], const h8* wh, const h8 (&x
 // ~128 KB of fragments per 16 nodes: 92 us per C4 layer, L2-bound.) Also zeroes the edge backward's
 // GB / GX rows.
 constexpr int NB_WAVES = 8;
-#if NONODE_NODE_H16
 // The seven products (WV1 h, WN1 [h, M], WV1^T gt, WN2^T gho, WN1^T gz) run fp16x3 on
 // v_mfma_f32_16x16x32_f16 (24 MFMAs each, against 64 or 128 f32 16x16x4 MFMAs of 4x the cycles):
 // every operand column is scaled by a power of two to [2^11, 2^12) before the split and the product
@@ -137,118 +132,6 @@ __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) 
   }
   }
 }
-#else
-// exact f32 MFMAs: the six node-side f32 fragment matrices (WV1, WN1, WV1^T, WN2^T, WN1^T h / m)
-constexpr int NB_LDS_FLOATS = (BOFF_WN1 + 8192 - BOFF_WV1) + (BOFF_WN1TM + 4096 - BOFF_WV1T);   // 28672
-__global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
-  {
-    const float* bb = p.bb;
-    constexpr int n1 = BOFF_WN1 + 8192 - BOFF_WV1, n2 = BOFF_WN1TM + 4096 - BOFF_WV1T;
-    const f4* s1 = reinterpret_cast<const f4*>(bb + BOFF_WV1);
-    const f4* s2 = reinterpret_cast<const f4*>(bb + BOFF_WV1T);
-    for (int i = threadIdx.x; i < n1 / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem)[i] = s1[i];
-    for (int i = threadIdx.x; i < n2 / 4; i += NB_WAVES * 64) reinterpret_cast<f4*>(smem + n1)[i] = s2[i];
-  }
-  __syncthreads();
-  const float* sWV1_ = smem;                                  // [BOFF_WV1, BOFF_WN1 + 8192) staged
-  const float* sWN1_ = smem + (BOFF_WN1 - BOFF_WV1);
-  const float* sT = smem + (BOFF_WN1 + 8192 - BOFF_WV1);    // [BOFF_WV1T, BOFF_WN1TM + 4096) staged
-  const float* sWV1T_ = sT;
-  const float* sWN2T_ = sT + (BOFF_WN2T - BOFF_WV1T);
-  const float* sWN1TH_ = sT + (BOFF_WN1TH - BOFF_WV1T);
-  const float* sWN1TM_ = sT + (BOFF_WN1TM - BOFF_WV1T);
-  const int ntile = (p.n + 15) >> 4;
-#pragma unroll 1
-  for (int tile = blockIdx.x * NB_WAVES + wave; tile < ntile; tile += gridDim.x * NB_WAVES) {
-  // loop-invariant weight reads stay in the loop (hoisted, the bias vectors and fragments would
-  // pin registers across the tiles and spill): opaque zero offset
-  int off = 0;
-  asm volatile("" : "+v"(off));
-  const float* bb = p.bb + off;
-  const float* sWV1 = sWV1_ + off;
-  const float* sWN1 = sWN1_ + off;
-  const float* sWV1T = sWV1T_ + off;
-  const float* sWN2T = sWN2T_ + off;
-  const float* sWN1TH = sWN1TH_ + off;
-  const float* sWN1TM = sWN1TM_ + off;
-  const int r0 = tile * 16;
-  const int r = min(r0 + e, p.n - 1);
-  const bool valid = r0 + e < p.n;
-  f4 hr[4], Mr[4];
-  load_ecl(hr, p.h + (size_t)r * HID, g);
-  load_ecl(Mr, p.M + (size_t)r * HID, g);
-  // phi_v(h) = wv2 . SiLU(WV1 h + bv1) + bv2
-  f4 tp[4];
-  load_vp(tp, bb + BOFF_VEC + BV_BV1 * 64, g);
-  mfma_dense<4>(tp, sWV1, hr, lane);
-  f4 t[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) t[mt] = tp[mt];
-  silu_true(t);
-  const float phi = dot_vp(t, bb + BOFF_VEC + BV_WV2 * 64, g) + bb[BOFF_SCAL + 1];
-  const float gx0 = p.gxo[(size_t)r * 3 + 0], gx1 = p.gxo[(size_t)r * 3 + 1], gx2 = p.gxo[(size_t)r * 3 + 2];
-  const float v0 = p.v[(size_t)r * 3 + 0], v1 = p.v[(size_t)r * 3 + 1], v2 = p.v[(size_t)r * 3 + 2];
-  const float gphi = gx0 * v0 + gx1 * v1 + gx2 * v2;
-  // clamp(F / (N-1), +-100) passes the gradient inside [-100, 100]
-  const float inv = 1.f / (float)(p.N - 1);
-  const float F0 = p.F[(size_t)r * 4 + 0] * inv, F1 = p.F[(size_t)r * 4 + 1] * inv, F2 = p.F[(size_t)r * 4 + 2] * inv;
-  const float gF0 = (F0 >= -100.f && F0 <= 100.f) ? gx0 * inv : 0.f;
-  const float gF1 = (F1 >= -100.f && F1 <= 100.f) ? gx1 * inv : 0.f;
-  const float gF2 = (F2 >= -100.f && F2 <= 100.f) ? gx2 * inv : 0.f;
-  // gt_pre = gphi * wv2 (.) silu'(tp);  gh = WV1^T gt_pre
-  f4 gt[4];
-  load_vp(gt, bb + BOFF_VEC + BV_WV2 * 64, g);
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) gt[mt] *= gphi;
-  mul_dsilu(gt, tp);
-  f4 gh[4];
-  zero4(gh);
-  mfma_dense<4>(gh, sWV1T, gt, lane);
-  // node MLP: z = SiLU(WN1 [h, M] + bn1), h' = WN2 z + bn2
-  f4 in8[8];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
-  f4 zp[4];
-  load_vp(zp, bb + BOFF_VEC + BV_BN1 * 64, g);
-  mfma_dense<8>(zp, sWN1, in8, lane);
-  f4 z[4];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) z[mt] = zp[mt];
-  silu_true(z);
-  f4 gho[4], gz[4];
-  load_ecl(gho, p.gho + (size_t)r * HID, g);
-  zero4(gz);
-  mfma_dense<4>(gz, sWN2T, gho, lane);
-  mul_dsilu(gz, zp);
-  mfma_dense<4>(gh, sWN1TH, gz, lane);
-  f4 gM[4];
-  zero4(gM);
-  mfma_dense<4>(gM, sWN1TM, gz, lane);
-  if (valid) {
-    const size_t o = (size_t)r * HID;
-    store_ecl(p.ghp + o, gh, g);
-    store_ecl(p.gM + o, gM, g);
-    store_ecl(p.op_gt + o, gt, g);
-    store_ecl(p.op_t + o, t, g);
-    store_ecl(p.op_z + o, z, g);
-    store_ecl(p.op_gz + o, gz, g);
-    const f4 z4[4] = {};
-    store_ecl(p.GB + o, z4, g);                          // the edge backward's sender sums start at 0
-    if (g == 0) {
-      p.gv[(size_t)r * 3 + 0] = p.gvo[(size_t)r * 3 + 0] + phi * gx0;
-      p.gv[(size_t)r * 3 + 1] = p.gvo[(size_t)r * 3 + 1] + phi * gx1;
-      p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
-      *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
-      *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = f4{0.f, 0.f, 0.f, 0.f};
-      p.op_gphi[r] = gphi;
-    }
-  }
-  }
-}
-
-#endif
 
 
 // ---- node_post (NodePostArgs): gh = ghp + W_A^T GA + W_B^T GB, gx = gxo + GX --------------------

@@ -31,20 +31,8 @@ using nonode_tu::TconvBwdArgs;
 using nonode_tu::launch_tconv_bwd;
 using nonode_tu::tb_groups;
 
-#ifndef NONODE_PAIR_A
-#define NONODE_PAIR_A 1
-#endif
-#ifndef NONODE_PAIR_B
-#define NONODE_PAIR_B 0   // pass B in the pair form measured slower (664 vs 524 us per C4 layer: spills)
-#endif
-#ifndef NONODE_PAIR_FENCE
-#define NONODE_PAIR_FENCE 1
-#endif
-#if NONODE_PAIR_FENCE
+// scheduling fence between the pair loop's stages (each stage's two chains interleave, the stages do not)
 #define PAIR_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define PAIR_FENCE() do {} while (0)
-#endif
 
 // frag of W^T: value W^T[row][col] = W[col][row0 + row] (W row stride ld)
 __device__ __forceinline__ void pack_frag_t(float* dst, const float* W, int ld, int row0, int d) {
@@ -543,7 +531,10 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   constexpr int NW = 4;
   constexpr int NF = 1 + NE;   // scalar inputs of edge W1: |r|^2, e_0 .. e_{NE-1}
   // two units per iteration (the pair loops below; else one unit at a time throughout)
-  constexpr bool PAIRS = PASS == 0 ? NONODE_PAIR_A != 0 : NONODE_PAIR_B != 0;
+  // pass A runs two units per iteration; pass B's pair form measured slower
+  // (round 4: 524 -> 664 us per C4 layer with the handoff prefetched, 581 without; both spill) and was
+  // removed
+  constexpr bool PAIRS = PASS == 0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int N = p.N, Nm1 = N - 1;
   const int rows = p.ct * 16;
@@ -1159,132 +1150,6 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         }
         STAMP(4);
         STAMP(15);
-      }
-    }
-    if constexpr (PASS == 1 && PAIRS) {
-      // ---- pass B, two units per iteration (as pass A): dW2 in the K = 32 form with a's split as its
-      // operand, W2^T gz2 for both units through shared fragment reads; the per-unit sums (scalar
-      // columns, GA / GB / GX tables) in unit order afterwards
-      const int npair = U >> 1;
-      u_first = ((U & 1) && wave == npair % NW) ? U - 1 : U;
-      _Float16* img = reinterpret_cast<_Float16*>(tile);
-      const unsigned us_w2t = h16_us(bb + BOFF_SCAL, BH_W2T);
-      const float* vWS = sV + (BOFF_VEC - BOFF_FEAT) + BV_WS * 64;
-      auto load_h = [&](int uu, f4 (&gz)[4], float& c) __attribute__((always_inline)) {
-        const float* ep;
-        size_t su;
-        unit_src(uu, ep, su);
-        const float* sb16 = p.stash + su * HID;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) gz[mt] = *reinterpret_cast<const f4*>(sb16 + mt * 256 + e * 16 + 4 * g);
-        c = p.stash_c[su + e];
-      };
-      float fa[NEP], fb[NEP];
-      f4 gna[4], gnb[4];
-      float cna = 0.f, cnb = 0.f;
-      if (wave < npair) {
-        load_ef(2 * wave, fa);
-        load_ef(2 * wave + 1, fb);
-        load_h(2 * wave, gna, cna);
-        load_h(2 * wave + 1, gnb, cnb);
-      }
-      // per unit, in unit order: W1 scalar-column and |r|^2 gradients, r gradient, GA / GB / GX
-      auto finish = [&](const UnitGeo& o, const f4 (&gz1)[4], float c) __attribute__((always_inline)) {
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) accFe[f][mt] += o.fe[f] * gz1[mt];
-        float gs = dot_vp(gz1, vWS, g);
-        if constexpr (rnorm) gs = o.s2 < 1e-12f ? gs * 1e12f : 0.f;
-        float f0, f1, f2;
-        grad_f(o, c, f0, f1, f2);
-        const float gr0 = fmaf(2.f * gs, o.q0, c * f0);
-        const float gr1 = fmaf(2.f * gs, o.q1, c * f1);
-        const float gr2 = fmaf(2.f * gs, o.q2, c * f2);
-        if (o.tau != cur_tau) {   // wave-uniform
-          if (cur_tau >= 0) flush_ga(cur_tau);
-          cur_tau = o.tau;
-        }
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) gaR[mt] += gz1[mt];
-        gxR0 += gr0;
-        gxR1 += gr1;
-        gxR2 += gr2;
-        if (o.rv) {
-          f4 t[4];
-          load_ecl(t, myGB + o.sl * ROWP, g);
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) t[mt] += gz1[mt];
-          store_ecl(myGB + o.sl * ROWP, t, g);
-          if (g == 0) {
-            f4* xs = reinterpret_cast<f4*>(myGX + o.sl * 4);
-            *xs -= f4{gr0, gr1, gr2, 0.f};
-          }
-        }
-      };
-      for (int ip = wave; ip < npair; ip += NW) {
-        asm volatile("" ::: "memory");   // keep the fragment reads in the loop
-        float ea[NEP], eb[NEP];
-        f4 gz2a[4], gz2b[4];
-        const float ca = cna, cb = cnb;
-#pragma unroll
-        for (int kk = 0; kk < NEP; ++kk) { ea[kk] = fa[kk]; eb[kk] = fb[kk]; }
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) { gz2a[mt] = gna[mt]; gz2b[mt] = gnb[mt]; }
-        {
-          const int ipn = ip + NW < npair ? ip + NW : ip;
-          load_ef(2 * ipn, fa);
-          load_ef(2 * ipn + 1, fb);
-          load_h(2 * ipn, gna, cna);
-          load_h(2 * ipn + 1, gnb, cnb);
-        }
-        f4 z1a[4], z1b[4];
-        UnitGeo ga, gb;
-        head_u(2 * ip, ea, z1a, ga);
-        head_u(2 * ip + 1, eb, z1b, gb);
-        STAMP(0);
-        // a = SiLU(z1) (split: dW2's operand), d1 = SiLU'(z1)
-        f4 d1a[4], d1b[4];
-        h8 aah[2], aal[2], abh[2], abl[2];
-        float amx;
-        {
-          f4 aa[4], ab[4];
-          silu_dsilu(z1a, aa, d1a);
-          silu_dsilu(z1b, ab, d1b);
-          amx = fmaxf(amax16(aa), amax16(ab));
-          h16_split(aa, aah, aal);
-          h16_split(ab, abh, abl);
-        }
-        if (__builtin_expect(__any(amx > H16_LIMIT), 0)) {
-          // an activation beyond the fp16 range: redone after the loop by the single-unit form (exact f32)
-          bigmask |= 1ull << ((ip - wave) / NW);
-          continue;
-        }
-        if (!ga.rv) zero4(gz2a);   // zero gradient for receivers past the range
-        if (!gb.rv) zero4(gz2b);
-        STAMP(1);
-        const float cma = col_max(amax16(gz2a)), cmb = col_max(amax16(gz2b));
-        // dW2 += gz2 (x) a over the pair's 32 edges (K = 32); db2 += gz2
-        wgrad_pair(accW, scW, gz2a, gz2b, aah, aal, abh, abl, img, e, g, lane, fmaxf(cma, cmb));
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          bsE[mt] += gz2a[mt];
-          bsE[mt] += gz2b[mt];
-        }
-        STAMP(5);
-        PAIR_FENCE();
-        // gz1 = (W2^T gz2) SiLU'(z1)
-        f4 gz1a[4], gz1b[4];
-        zero4(gz1a);
-        zero4(gz1b);
-        mm64_cs2(gz1a, gz1b, hW2T, gz2a, gz2b, lane, us_w2t, cma, cmb);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) { gz1a[mt] *= d1a[mt]; gz1b[mt] *= d1b[mt]; }
-        STAMP(6);
-        PAIR_FENCE();
-        finish(ga, gz1a, ca);
-        finish(gb, gz1b, cb);
-        STAMP(7);
       }
     }
     if constexpr (PAIRS) {
