@@ -79,6 +79,10 @@ size_t nonode_layer_blob_floats(void);
  * call it again after every optimizer step. hidden must be 64, n_edge_feat <= 4. */
 int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
                       float* blob, void* stream);
+/* nonode_pack_layer of n_layers layers in one launch (w, blobs: host arrays; same rules per layer).
+ * A training step re-packs every layer after each optimizer step (egno.py _packed). */
+int nonode_pack_layers(const nonode_layer_weights* const* w, int n_layers, int variant, int hidden,
+                       int n_edge_feat, float* const* blobs, void* stream);
 
 /* Workspace bytes nonode_egno_forward needs. */
 size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt);
@@ -155,6 +159,10 @@ size_t nonode_tconv_blob_floats(int modes);
 /* Pack time_conv_modules.l.t_conv.weights1 [64][64][modes][2] (layer_no.py:203-205) for trajectory
  * length T: the irfft scale (c_m / T) is folded in. Call again after every optimizer step. */
 int nonode_pack_tconv(const float* tconv_w, int modes, int T, float* blob, void* stream);
+/* nonode_pack_tconv of n_layers weight arrays in one launch (tconv_w, blobs: host arrays of device
+ * pointers; same rules). */
+int nonode_pack_tconvs(const float* const* tconv_w, int n_layers, int modes, int T, float* const* blobs,
+                       void* stream);
 
 /* TimeConv + TimeConv_x of one EGNO layer (layer_no.py:96-126,152-178, egno.py:100-108) on
  * time-major [T][BN] arrays; x_out/v_out may alias x/v (in place per column), h_out may not
@@ -202,6 +210,9 @@ size_t nonode_bwd_blob_floats(void);
 /* Pack one EGNO (or SEGNO) layer for the backward pass. */
 int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
                           float* bblob, void* stream);
+/* nonode_pack_layer_bwd of n_layers layers in one launch (w, bblobs: host arrays; same rules). */
+int nonode_pack_layers_bwd(const nonode_layer_weights* const* w, int n_layers, int variant, int hidden,
+                           int n_edge_feat, float* const* bblobs, void* stream);
 
 /* Bytes of the saved forward state (every layer's inputs, message / force sums, embedding rows). */
 size_t nonode_egno_train_state_bytes(int B, int N, int T, int n_layers, int in_node, int time_emb_dim);

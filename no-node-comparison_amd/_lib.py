@@ -28,6 +28,7 @@ SYMBOLS = (
     "nonode_gather_batch", "nonode_rollout_metrics",
     "nonode_egnn_layer_bwd_workspace_bytes", "nonode_egnn_layer_bwd",
     "nonode_egno_tconv_bwd_workspace_bytes", "nonode_egno_tconv_bwd",
+    "nonode_pack_layers", "nonode_pack_layers_bwd", "nonode_pack_tconvs",
 )
 
 VARIANT_EGNO = 0
@@ -76,6 +77,10 @@ def lib():
     L.nonode_last_error.restype = ctypes.c_char_p
     L.nonode_layer_blob_floats.restype = _sz
     L.nonode_pack_layer.argtypes = [ctypes.POINTER(LayerWeights), _i, _i, _i, _vp, _vp]
+    L.nonode_pack_layers.argtypes = [ctypes.POINTER(ctypes.POINTER(LayerWeights)), _i, _i, _i, _i,
+                                     ctypes.POINTER(_vp), _vp]
+    L.nonode_pack_layers_bwd.argtypes = L.nonode_pack_layers.argtypes
+    L.nonode_pack_tconvs.argtypes = [ctypes.POINTER(_vp), _i, _i, _i, ctypes.POINTER(_vp), _vp]
     L.nonode_egno_workspace_bytes.argtypes = [_i, _i, _i, _i]
     L.nonode_egno_workspace_bytes.restype = _sz
     L.nonode_egno_forward.argtypes = ([_i] * 9 + [_vp] * 8 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4

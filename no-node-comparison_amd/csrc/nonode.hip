@@ -60,6 +60,10 @@ struct PackArgs {
   int flags;   // NONODE_LAYER_* option bits (stored at OFF_SCAL + 2 / + 3)
   float* blob;
 };
+// several layers' PackArgs in one launch (blockIdx.z = layer): a training step re-packs every layer
+// after each optimizer step, and one launch per layer and blob kind cost ~5 us each
+constexpr int PACK_MAX = 8;
+struct PackBatch { PackArgs a[PACK_MAX]; };
 
 // scale(col): multiplier of input column col (the SiLU-domain factors, see silu()).
 __device__ __forceinline__ void pack_frag(float* dst, const float* src, int ld, int col0, int KT, int d,
@@ -120,7 +124,8 @@ __device__ __forceinline__ void pack_h16_shifted(_Float16* dst, float* scal, int
   if (blockIdx.x == 0 && threadIdx.x == 0) scal[SC_H16S + idx] = h16_us_bits(k);
 }
 
-__global__ void pack_kernel(PackArgs a) {
+__global__ void pack_kernel(PackBatch pb) {
+  const PackArgs& a = pb.a[blockIdx.z];
   const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
   const int sec = blockIdx.y;
   float* B = a.blob;
@@ -1349,7 +1354,10 @@ struct TconvArgs {
 //   y[t] = sum_m (Yr_m cos(2 pi m t/T) - Yi_m sin(2 pi m t/T))   (= irfft(pad(Y), n=T)).
 size_t tconv_blob_floats(int modes) { return (size_t)(1 + 3 * (modes - 1)) * 4096; }
 
-__global__ void tconv_pack_kernel(const float* w, int Mfull, int M, int T, float* out) {
+struct TconvPackBatch { const float* w[PACK_MAX]; float* out[PACK_MAX]; };
+__global__ void tconv_pack_kernel(TconvPackBatch tb, int Mfull, int M, int T) {
+  const float* w = tb.w[blockIdx.y];
+  float* out = tb.out[blockIdx.y];
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   const int nmat = 1 + 3 * (M - 1);
   if (d >= nmat * 4096) return;
@@ -1820,14 +1828,9 @@ int effective_modes(int T, int modes) {
 }  // namespace
 
 // ================================ C ABI ========================================================
-extern "C" {
-
-const char* nonode_version(void) { return "nonode-mi355x 0.1 (gfx950)"; }
-const char* nonode_last_error(void) { return g_err.c_str(); }
-size_t nonode_layer_blob_floats(void) { return BLOB_FLOATS; }
-
-int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
-                      float* blob, void* stream) {
+namespace {
+// the validated PackArgs of one layer (nonode_pack_layer's rules)
+int pack_args(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat, float* blob, PackArgs* out) {
   if (!w || !blob) return fail(NONODE_EINVAL, "pack_layer: null pointer");
   const int flags = variant & ~0xff;
   variant &= 0xff;
@@ -1844,7 +1847,7 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
     return fail(NONODE_EINVAL, "pack_layer: TANH_COORD is a SEGNO option");
   if (variant == NONODE_VARIANT_EGNO && (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2))
     return fail(NONODE_EINVAL, "pack_layer: EGNO needs node_v_net weights");
-  PackArgs a;
+  PackArgs& a = *out;
   a.ld1 = 2 * HID + 1 + n_edge_feat;
   if (variant == NONODE_VARIANT_EGNO) { a.colS = 0; a.colA = 1; a.colB = 1 + HID; }       // [s,h_i,h_j,e]
   else if (variant == NONODE_VARIANT_SEGNO) { a.colA = 0; a.colB = HID; a.colS = 2 * HID; }  // [h_i,h_j,s,e]
@@ -1858,21 +1861,58 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
   a.ne = n_edge_feat;
   a.flags = flags;
   a.blob = blob;
-  hipLaunchKernelGGL(pack_kernel, dim3(32, 16), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("pack_kernel");
+  return NONODE_OK;
 }
+}  // namespace
+
+extern "C" {
 
 size_t nonode_tconv_blob_floats(int modes) { return (modes >= 1 && modes <= MMAX) ? tconv_blob_floats(modes) : 0; }
 
+const char* nonode_version(void) { return "nonode-mi355x 0.1 (gfx950)"; }
+const char* nonode_last_error(void) { return g_err.c_str(); }
+size_t nonode_layer_blob_floats(void) { return BLOB_FLOATS; }
+
+int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
+                      float* blob, void* stream) {
+  return nonode_pack_layers(&w, 1, variant, hidden, n_edge_feat, &blob, stream);
+}
+int nonode_pack_layers(const nonode_layer_weights* const* w, int n_layers, int variant, int hidden,
+                       int n_edge_feat, float* const* blobs, void* stream) {
+  if (!w || !blobs || n_layers < 0) return fail(NONODE_EINVAL, "pack_layers: null pointer");
+  for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
+    const int cnt = n_layers - l0 < PACK_MAX ? n_layers - l0 : PACK_MAX;
+    PackBatch pb{};
+    for (int k = 0; k < cnt; ++k)
+      if (int rc = pack_args(w[l0 + k], variant, hidden, n_edge_feat, blobs[l0 + k], &pb.a[k])) return rc;
+    hipLaunchKernelGGL(pack_kernel, dim3(32, 16, cnt), dim3(256), 0, (hipStream_t)stream, pb);
+    if (int rc = check_launch("pack_kernel")) return rc;
+  }
+  return NONODE_OK;
+}
 int nonode_pack_tconv(const float* tconv_w, int modes, int T, float* blob, void* stream) {
-  if (!tconv_w || !blob) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
+  return nonode_pack_tconvs(&tconv_w, 1, modes, T, &blob, stream);
+}
+int nonode_pack_tconvs(const float* const* tconv_w, int n_layers, int modes, int T, float* const* blobs,
+                       void* stream) {
+  if (!tconv_w || !blobs || n_layers < 0) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
   if (modes < 1 || modes > MMAX || T < 1 || T > TMAX)
     return fail(NONODE_EUNSUPPORTED, "pack_tconv: modes=%d T=%d", modes, T);
   const int M = effective_modes(T, modes);
   const int n = (int)tconv_blob_floats(M);
-  hipLaunchKernelGGL(tconv_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, tconv_w, modes,
-                     M, T, blob);
-  return check_launch("tconv_pack_kernel");
+  for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
+    const int cnt = n_layers - l0 < PACK_MAX ? n_layers - l0 : PACK_MAX;
+    TconvPackBatch tb{};
+    for (int k = 0; k < cnt; ++k) {
+      if (!tconv_w[l0 + k] || !blobs[l0 + k]) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
+      tb.w[k] = tconv_w[l0 + k];
+      tb.out[k] = blobs[l0 + k];
+    }
+    hipLaunchKernelGGL(tconv_pack_kernel, dim3((n + 255) / 256, cnt), dim3(256), 0, (hipStream_t)stream, tb, modes,
+                       M, T);
+    if (int rc = check_launch("tconv_pack_kernel")) return rc;
+  }
+  return NONODE_OK;
 }
 
 int nonode_egno_tconv(int BN, int T, int modes, const float* h, const float* x, const float* v,

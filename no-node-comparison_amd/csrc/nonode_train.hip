@@ -59,7 +59,8 @@ __device__ __forceinline__ void pack_h16_t_shifted(_Float16* dst, float* scal, i
   if (blockIdx.x == 0 && threadIdx.x == 0) scal[SC_H16S + idx] = h16_us_bits(k);
 }
 
-__global__ void pack_bwd_kernel(PackArgs a) {
+__global__ void pack_bwd_kernel(PackBatch pb) {
+  const PackArgs& a = pb.a[blockIdx.z];
   const int d = blockIdx.x * blockDim.x + threadIdx.x;   // 0 .. 8191
   float* B = a.blob;
   _Float16* H = reinterpret_cast<_Float16*>(B + BOFF_H16);
@@ -1792,12 +1793,10 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
 
 }  // namespace
 
-extern "C" {
-
-size_t nonode_bwd_blob_floats(void) { return BBLOB_FLOATS; }
-
-int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat, float* bblob,
-                          void* stream) {
+namespace {
+// the validated PackArgs of one layer's backward blob (nonode_pack_layer_bwd's rules)
+int pack_bwd_args(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat, float* bblob,
+                  PackArgs* out) {
   if (!w || !bblob) return fail(NONODE_EINVAL, "pack_layer_bwd: null pointer");
   const int flags = variant & ~0xff;
   variant &= 0xff;
@@ -1812,7 +1811,7 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   if (!egno && variant != NONODE_VARIANT_SEGNO) return fail(NONODE_EINVAL, "pack_layer_bwd: variant %d", variant);
   if (egno && (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2))
     return fail(NONODE_EINVAL, "pack_layer_bwd: EGNO needs node_v_net weights");
-  PackArgs a;
+  PackArgs& a = *out;
   a.ld1 = 2 * HID + 1 + n_edge_feat;
   if (egno) { a.colS = 0; a.colA = 1; a.colB = 1 + HID; }       // [s, h_i, h_j, e]  basic.py:152-154
   else { a.colA = 0; a.colB = HID; a.colS = 2 * HID; }          // [h_i, h_j, s, e]  gcl.py:78
@@ -1824,8 +1823,30 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
   a.ne = n_edge_feat;
   a.flags = flags;
   a.blob = bblob;
-  hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 31), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("pack_bwd_kernel");
+  return NONODE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+size_t nonode_bwd_blob_floats(void) { return BBLOB_FLOATS; }
+
+int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat, float* bblob,
+                          void* stream) {
+  return nonode_pack_layers_bwd(&w, 1, variant, hidden, n_edge_feat, &bblob, stream);
+}
+int nonode_pack_layers_bwd(const nonode_layer_weights* const* w, int n_layers, int variant, int hidden,
+                           int n_edge_feat, float* const* bblobs, void* stream) {
+  if (!w || !bblobs || n_layers < 0) return fail(NONODE_EINVAL, "pack_layer_bwd: null pointer");
+  for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
+    const int cnt = n_layers - l0 < PACK_MAX ? n_layers - l0 : PACK_MAX;
+    PackBatch pb{};
+    for (int k = 0; k < cnt; ++k)
+      if (int rc = pack_bwd_args(w[l0 + k], variant, hidden, n_edge_feat, bblobs[l0 + k], &pb.a[k])) return rc;
+    hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 31, cnt), dim3(256), 0, (hipStream_t)stream, pb);
+    if (int rc = check_launch("pack_bwd_kernel")) return rc;
+  }
+  return NONODE_OK;
 }
 
 size_t nonode_egno_train_state_bytes(int B, int N, int T, int n_layers, int in_node, int time_emb_dim) {

@@ -152,15 +152,18 @@ class EGNO(nn.Module):
         tblobs = torch.empty(self.n_layers, L.nonode_tconv_blob_floats(self.num_modes), dtype=torch.float32,
                              device=dev) if self.use_time_conv else None
         stream = _lib.stream_of(blobs)
-        for i, layer in enumerate(self.layers):
-            w = layer.weight_struct()
-            _lib.check(L.nonode_pack_layer(ctypes.byref(w), self._pack_variant(), self.hidden_nf,
-                                           self.in_edge_nf, _lib.ptr(blobs[i]), stream))
-            if not self.use_time_conv:
-                continue
-            tw = self.time_conv_modules[i].t_conv.weights1.detach().float().contiguous()
-            _lib.check(L.nonode_pack_tconv(_lib.ptr(tw), self.num_modes, self.num_timesteps, _lib.ptr(tblobs[i]),
-                                           stream))
+        # every layer in one launch per blob kind (nonode_pack_layers / nonode_pack_tconvs)
+        ws = [layer.weight_struct() for layer in self.layers]
+        WP = ctypes.POINTER(_lib.LayerWeights)
+        P = ctypes.c_void_p * self.n_layers
+        _lib.check(L.nonode_pack_layers((WP * self.n_layers)(*[ctypes.pointer(w) for w in ws]), self.n_layers,
+                                        self._pack_variant(), self.hidden_nf, self.in_edge_nf,
+                                        P(*[blobs[i].data_ptr() for i in range(self.n_layers)]), stream))
+        if self.use_time_conv:
+            tws = [m.t_conv.weights1.detach().float().contiguous() for m in self.time_conv_modules]
+            _lib.check(L.nonode_pack_tconvs(P(*[t.data_ptr() for t in tws]), self.n_layers, self.num_modes,
+                                            self.num_timesteps, P(*[tblobs[i].data_ptr() for i in range(self.n_layers)]),
+                                            stream))
         self._blobs, self._blob_key = (blobs, tblobs), key
         return self._blobs
 
@@ -189,10 +192,12 @@ class EGNO(nn.Module):
         dev = self.embedding.weight.device
         bb = torch.empty(self.n_layers, L.nonode_bwd_blob_floats(), dtype=torch.float32, device=dev)
         stream = _lib.stream_of(bb)
-        for i, layer in enumerate(self.layers):
-            w = layer.weight_struct()
-            _lib.check(L.nonode_pack_layer_bwd(ctypes.byref(w), self._pack_variant(), self.hidden_nf, self.in_edge_nf,
-                                               _lib.ptr(bb[i]), stream))
+        ws = [layer.weight_struct() for layer in self.layers]   # one launch for every layer
+        WP = ctypes.POINTER(_lib.LayerWeights)
+        P = ctypes.c_void_p * self.n_layers
+        _lib.check(L.nonode_pack_layers_bwd((WP * self.n_layers)(*[ctypes.pointer(w) for w in ws]), self.n_layers,
+                                            self._pack_variant(), self.hidden_nf, self.in_edge_nf,
+                                            P(*[bb[i].data_ptr() for i in range(self.n_layers)]), stream))
         self._bblobs, self._bblob_key = bb, key
         return bb
 
