@@ -1498,9 +1498,22 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
 #pragma unroll
   for (int k = 0; k < CNT; ++k) red[threadIdx.x][k] = pp[k];
   __syncthreads();
+  // the block's 128 rows added in a fixed tree: every thread sums 16 rows of one column (one serial
+  // 128-row sum per column had been a ~4 us chain per block), then 8 partials per column
+  constexpr int RG = TX_THREADS / 16;   // row groups
+  __shared__ float red2[RG][CNT];
+  for (int q = threadIdx.x; q < RG * CNT; q += TX_THREADS) {
+    const int k = q % CNT, rg = q / CNT;
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc += red[rg * 16 + r][k];
+    red2[rg][k] = acc;
+  }
+  __syncthreads();
   if (threadIdx.x < CNT) {
     float acc = 0.f;
-    for (int r = 0; r < TX_THREADS; ++r) acc += red[r][threadIdx.x];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) acc += red2[rg][threadIdx.x];
     const int io = threadIdx.x / (MM * 2), rest = threadIdx.x - io * (MM * 2);   // rest = 2 m + c
     part[(size_t)blockIdx.x * (2 * 2 * MMAX_T * 2) + io * (MMAX_T * 2) + rest] = acc;
   }
