@@ -126,6 +126,14 @@ __device__ __forceinline__ float row_max16(float m) {
   m = fmaxf(m, dppf<0x141>(m));   // row_half_mirror
   return fmaxf(m, dppf<0x140>(m));  // row_mirror
 }
+// sum over the 16 lanes of a row (the same DPP steps: each adds a disjoint half, so every lane ends
+// with the row's sum, in the same order on every lane)
+__device__ __forceinline__ float row_sum16(float m) {
+  m += dppf<0xB1>(m);
+  m += dppf<0x4E>(m);
+  m += dppf<0x141>(m);
+  return m + dppf<0x140>(m);
+}
 // fp16x3 split of 4 values (as h16_split)
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
@@ -167,11 +175,14 @@ struct NodeBwdArgs {
   const float* gxo; const float* gvo; const float* gho;              // grads of the layer outputs
   const float* bb;                                                   // backward blob
   float* gv; float* gF; float* gM; float* ghp;                       // outputs
-  float* op_gt; float* op_t; float* op_gphi; float* op_z; float* op_gz;   // GEMM operands
+  float* op_gt; float* op_z; float* op_gz;                           // GEMM operands (node_wgrad)
+  float* p6;   // per-workgroup partials [blocks][65] of the node_v output row: sum gphi t | sum gphi
   float* GB; float* GX;                                              // zeroed for the edge backward
 };
-// launches node_bwd_kernel over ntile 16-node tiles on stream s (NONODE_OK or an error code)
-int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s);
+// launches node_bwd_kernel over ntile 16-node tiles on stream s (NONODE_OK or an error code); *nparts =
+// the number of p6 partial rows it writes (at most NB_MAX_PARTS)
+constexpr int NB_MAX_PARTS = 1024;
+int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s, int* nparts);
 
 // ---- gh = ghp + W_A^T GA + W_B^T GB, gx = gxo + GX after the edge backward: nonode_node.hip --------
 struct NodePostArgs {

@@ -48,6 +48,11 @@ __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) 
   __syncthreads();
   const h8* sH_ = reinterpret_cast<const h8*>(smem);
   const int ntile = (p.n + 15) >> 4;
+  // the node_v output row's gradient sum_n gphi_n t_n (and sum_n gphi_n), per lane: column e's terms
+  // for channels 16 mt + 4 g + q; the wave's 16 columns are added at the end (no t / gphi to HBM)
+  f4 s6[4];
+  zero4(s6);
+  float b6 = 0.f;
 #pragma unroll 1
   for (int tile = blockIdx.x * NB_WAVES + wave; tile < ntile; tile += gridDim.x * NB_WAVES) {
   // loop-invariant reads stay in the loop (hoisted, the 7 x 64 fragment registers per lane would
@@ -116,8 +121,10 @@ __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) 
     store_ecl(p.ghp + o, gh, g);
     store_ecl(p.gM + o, gM, g);
     store_ecl(p.op_gt + o, gt, g);
-    store_ecl(p.op_t + o, t, g);
     store_ecl(p.op_z + o, z, g);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) s6[mt] += t[mt] * gphi;
+    b6 += gphi;
     store_ecl(p.op_gz + o, gz, g);
     const f4 z4[4] = {};
     store_ecl(p.GB + o, z4, g);                          // the edge backward's sender sums start at 0
@@ -127,9 +134,28 @@ __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) 
       p.gv[(size_t)r * 3 + 2] = p.gvo[(size_t)r * 3 + 2] + phi * gx2;
       *reinterpret_cast<f4*>(p.gF + (size_t)r * 4) = f4{gF0, gF1, gF2, 0.f};
       *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = f4{0.f, 0.f, 0.f, 0.f};
-      p.op_gphi[r] = gphi;
     }
   }
+  }
+  // the wave's 16 columns added (DPP row sums: lanes 16 g + e, e = 0..15), then the block's 8 waves in
+  // wave order through LDS (the fragments' space): one partial row per workgroup
+  __syncthreads();
+  float* srow = smem + wave * 68;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float v = row_sum16(s6[mt][q]);
+      if (e == 0) srow[16 * mt + 4 * g + q] = v;
+    }
+  const float bt = row_sum16(b6);
+  if (lane == 0) srow[64] = bt;
+  __syncthreads();
+  if (threadIdx.x < 65) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NB_WAVES; ++w) v += smem[w * 68 + threadIdx.x];
+    p.p6[(size_t)blockIdx.x * 65 + threadIdx.x] = v;
   }
 }
 
@@ -291,13 +317,16 @@ __global__ __launch_bounds__(NW_WAVES * 64) void node_wgrad_kernel(nonode_tu::No
 }  // namespace
 
 namespace nonode_tu {
-int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s) {
+int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s, int* nparts) {
   static std::once_flag once;
   std::call_once(once, [] {
     hipFuncSetAttribute((const void*)node_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, NB_LDS_FLOATS * 4);
   });
   const int want = (ntile + NB_WAVES - 1) / NB_WAVES;
-  const int G = want < num_cus() ? want : num_cus();
+  int G = want < num_cus() ? want : num_cus();
+  G = G < NB_MAX_PARTS ? G : NB_MAX_PARTS;
+  if (G < 1) G = 1;
+  *nparts = G;
   hipLaunchKernelGGL(node_bwd_kernel, dim3(G), dim3(NB_WAVES * 64), NB_LDS_FLOATS * 4, s, a);
   return check_launch("node_bwd_kernel");
 }

@@ -1770,7 +1770,7 @@ TrainState train_state(void* base, int B, int N, int T, int L, int in_node, int 
 struct BwdWs {
   float *gx[2], *gv[2], *gh[2];          // ping-pong grads of the current layer outputs (n rows)
   float *gF, *gM, *ghp, *GA, *GB, *GX, *gxe, *gve, *ghe;
-  float *op_gt, *op_t, *op_gphi, *op_z, *op_gz;
+  float *op_gt, *op_z, *op_gz, *p6;
   float *wpart;
   float *stash, *stash_c;                // edge backward pass A -> pass B ((N - 1) n rows)
   float *Pn, *Qn;                        // edge backward pass A -> pass B: node projections (n rows)
@@ -1788,7 +1788,8 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   for (int i = 0; i < 2; ++i) { w.gx[i] = take(n * 3); w.gv[i] = take(n * 3); w.gh[i] = take(n * 64); }
   w.gF = take(n * 4); w.gM = take(n * 64); w.ghp = take(n * 64); w.GA = take(n * 64); w.GB = take(n * 64);
   w.GX = take(n * 4); w.gxe = take(n * 3); w.gve = take(n * 3); w.ghe = take(n * 64);
-  w.op_gt = take(n * 64); w.op_t = take(n * 64); w.op_gphi = take(n); w.op_z = take(n * 64); w.op_gz = take(n * 64);
+  w.op_gt = take(n * 64); w.op_z = take(n * 64); w.op_gz = take(n * 64);
+  w.p6 = take((size_t)nonode_tu::NB_MAX_PARTS * 65);   // node_bwd's node_v output-row partials
   w.wpart = take((size_t)EB_MAX_BLOCKS * EW_STRIDE);
   const size_t npad = n + 16 * EB_MAX_BLOCKS;   // (N - 1) x (n + 16 G) handoff rows, G <= EB_MAX_BLOCKS
   w.stash = take(npad * (N - 1) * 64); w.stash_c = take(npad * (N - 1));
@@ -1992,10 +1993,11 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
   na.n = r.n; na.N = N; na.h = r.he; na.v = r.ve; na.M = r.Ms; na.F = r.Fs;
   na.gxo = r.gx; na.gvo = r.gv; na.gho = r.gh; na.bb = r.bb;
   na.gv = r.g_vin; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp;
-  na.op_gt = w.op_gt; na.op_t = w.op_t; na.op_gphi = w.op_gphi; na.op_z = w.op_z; na.op_gz = w.op_gz;
+  na.op_gt = w.op_gt; na.op_z = w.op_z; na.op_gz = w.op_gz; na.p6 = w.p6;
   const int ntile = (int)((n + 15) / 16);
   na.GB = w.GB; na.GX = w.GX;
-  if (int rc = launch_node_bwd(na, ntile, s)) return rc;
+  int n6 = 0;   // node_bwd's node_v output-row partial rows
+  if (int rc = launch_node_bwd(na, ntile, s, &n6)) return rc;
   ReduceJob rjobs[REDUCE_BATCH_MAX];
   int nred = 0;
   {
@@ -2031,8 +2033,8 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
   {
     nonode_tu::NodeWgradArgs wa{};
     wa.n = (long long)n;
-    wa.h = r.he; wa.M = r.Ms; wa.z = w.op_z; wa.t = w.op_t;
-    wa.GA = w.GA; wa.GB = w.GB; wa.gt = w.op_gt; wa.gz = w.op_gz; wa.gh = r.gh; wa.gphi = w.op_gphi;
+    wa.h = r.he; wa.M = r.Ms; wa.z = w.op_z; wa.t = nullptr;   // job 6 (node_v output row): node_bwd's p6
+    wa.GA = w.GA; wa.GB = w.GB; wa.gt = w.op_gt; wa.gz = w.op_gz; wa.gh = r.gh; wa.gphi = nullptr;
     wa.partial = w.partial;
     int nblk = 0;
     if (int rc = nonode_tu::launch_node_wgrad(wa, &nblk, s)) return rc;
@@ -2041,9 +2043,11 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
         {lg.node_w1, 128, 0, lg.node_b1}, {lg.node_w1, 128, HID, nullptr},   {lg.node_w2, 64, 0, lg.node_b2},
         {lg.vel_w2, 64, 0, lg.vel_b2}};
     constexpr long long pstride = (long long)nonode_tu::NW_JOBS * nonode_tu::NW_PART;
-    for (int j = 0; j < nonode_tu::NW_JOBS; ++j)
-      rjobs[nred++] = ReduceJob{w.partial + (size_t)j * nonode_tu::NW_PART, nblk, j < 6 ? 64 : 1, 64, d[j].dst,
-                                d[j].ld, d[j].col0, 1, d[j].bias, 0, 1.f, 1 << 30, 0, pstride};
+    for (int j = 0; j < 6; ++j)
+      rjobs[nred++] = ReduceJob{w.partial + (size_t)j * nonode_tu::NW_PART, nblk, 64, 64, d[j].dst, d[j].ld,
+                                d[j].col0, 1, d[j].bias, 0, 1.f, 1 << 30, 0, pstride};
+    // the node_v output row (job 6) from node_bwd's per-wave partials
+    rjobs[nred++] = ReduceJob{w.p6, n6, 1, 64, d[6].dst, d[6].ld, d[6].col0, 1, d[6].bias, 0, 1.f, 1 << 30, 0, 65};
     return launch_reduce_batch(rjobs, nred, s);
   }
 }
