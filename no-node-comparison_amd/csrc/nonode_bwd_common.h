@@ -184,31 +184,30 @@ struct NodeBwdArgs {
 constexpr int NB_MAX_PARTS = 1024;
 int launch_node_bwd(const NodeBwdArgs& a, int ntile, hipStream_t s, int* nparts);
 
-// ---- gh = ghp + W_A^T GA + W_B^T GB, gx = gxo + GX after the edge backward: nonode_node.hip --------
+// ---- gh = ghp + W_A^T GA + W_B^T GB, gx = gxo + GX after the edge backward (in node_wgrad_kernel) ----
 struct NodePostArgs {
   int n;
   const float* ghp; const float* GA; const float* GB; const float* gxo; const float* GX;
   const float* bb;                 // backward blob (BH_WAT, BH_WBT fp16 fragments)
   float* gh; float* gx;
 };
-int launch_node_post(const NodePostArgs& a, hipStream_t s);
 
 // ---- node-level weight gradients: nonode_node.hip ----------------------------------------------
 // The layer's GEMMs over its n nodes, C_j = sum_k G_j[k] (x) A_j[k] (64x64, plus the bias column
-// sum_k G_j[k]) for j < 6, and the node_v output row (j = 6: sum_k gphi[k] t[k], bias sum_k gphi[k]):
+// sum_k G_j[k]):
 //   0 GA (x) h -> edge W1 h_i block (+ b1)    3 gz (x) h -> node W1 h block (+ b1)
 //   1 GB (x) h -> edge W1 h_j block           4 gz (x) M -> node W1 message block
-//   2 gt (x) h -> node_v W1 (+ b1)            5 gh (x) z -> node W2 (+ b2)       6 gphi (x) t -> node_v W2 (+ b2)
-// Each workgroup writes one [NW_JOBS][64][65] partial (row 0 only for job 6); the caller adds them
-// in block order (gemm_reduce_batch, deterministic). SEGNO (no node_v MLP) passes t = gt = gphi = null:
-// jobs 2 and 6 are then zero.
-constexpr int NW_JOBS = 7, NW_MAX_BLOCKS = 256, NW_PART = 64 * 65;
+//   2 gt (x) h -> node_v W1 (+ b1)            5 gh (x) z -> node W2 (+ b2)
+// (the node_v output row is node_bwd's, NodeBwdArgs::p6). Each workgroup writes one
+// [NW_JOBS][64][65] partial; the caller adds them in block order (gemm_reduce_batch, deterministic).
+// SEGNO (no node_v MLP) passes gt = null: job 2 is then zero.
+constexpr int NW_JOBS = 6, NW_MAX_BLOCKS = 256, NW_PART = 64 * 65;
 struct NodeWgradArgs {
   long long n, chunks_per_block;   // n nodes in 32-node chunks; block b takes chunks [b c, (b + 1) c)
-  const float* h; const float* M; const float* z; const float* t;                  // A-side rows (n x 64)
+  const float* h; const float* M; const float* z;                                      // A-side rows (n x 64)
   const float* GA; const float* GB; const float* gt; const float* gz; const float* gh;   // G-side rows
-  const float* gphi;                                                                   // n
   float* partial;                                                                      // [blocks][NW_JOBS][NW_PART]
+  NodePostArgs post;   // node_post fused (post.ghp non-null): gh = ghp + W_A^T GA + W_B^T GB from the staged GA / GB
 };
 // launches node_wgrad_kernel (returns the number of blocks, i.e. partials, in *nblk)
 int launch_node_wgrad(const NodeWgradArgs& a, int* nblk, hipStream_t s);

@@ -160,64 +160,52 @@ __global__ __launch_bounds__(NB_WAVES * 64) void node_bwd_kernel(NodeBwdArgs p) 
 }
 
 
-// ---- node_post (NodePostArgs): gh = ghp + W_A^T GA + W_B^T GB, gx = gxo + GX --------------------
-// Persistent 8-wave workgroups (two per CU) stage W_A^T, W_B^T (fp16 hi/lo, 32 KB) in LDS once and
-// walk 16-node tiles; both products fp16x3 with the column scaling of cs_split (GA, GB are
-// gradients). (The round-3 form read 32 KB of f32 fragments from L2 per tile: 32 us per C4 layer.)
-constexpr int NP_WAVES = 8;
-__global__ __launch_bounds__(NP_WAVES * 64) void node_post_kernel(nonode_tu::NodePostArgs p) {
-  __shared__ __attribute__((aligned(16))) float sW[2 * 4096];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
-  {
-    const f4* src = reinterpret_cast<const f4*>(p.bb + BOFF_H16 + BH_WAT * 4096);   // W_A^T | W_B^T
-    for (int i = threadIdx.x; i < 2048; i += NP_WAVES * 64) reinterpret_cast<f4*>(sW)[i] = src[i];
-  }
-  __syncthreads();
-  const h8* sA_ = reinterpret_cast<const h8*>(sW);
-  const int ntile = (p.n + 15) >> 4;
-#pragma unroll 1
-  for (int tile = blockIdx.x * NP_WAVES + wave; tile < ntile; tile += gridDim.x * NP_WAVES) {
-    int off = 0;   // (loop-invariant fragment reads stay in the loop, see node_bwd_kernel)
-    asm volatile("" : "+v"(off));
-    const h8* sA = sA_ + off;
-    const int r0 = tile * 16;
-    const int r = min(r0 + e, p.n - 1);
-    f4 acc[4], ga[4], gb[4];
-    load_ecl(acc, p.ghp + (size_t)r * HID, g);
-    load_ecl(ga, p.GA + (size_t)r * HID, g);
-    load_ecl(gb, p.GB + (size_t)r * HID, g);
-    h8 xh[2], xl[2];
-    float inv = cs_split(ga, xh, xl);
-    mm_node<true>(acc, sA, xh, xl, inv, lane, h16_us(p.bb + BOFF_SCAL, BH_WAT));
-    inv = cs_split(gb, xh, xl);
-    mm_node<true>(acc, sA + 1024, xh, xl, inv, lane, h16_us(p.bb + BOFF_SCAL, BH_WBT));
-    if (r0 + e < p.n) {
-      store_ecl(p.gh + (size_t)r * HID, acc, g);
-      if (g < 3) p.gx[(size_t)r * 3 + g] = p.gxo[(size_t)r * 3 + g] + p.GX[(size_t)r * 4 + g];
-    }
-  }
-}
-
 // ---- node-level weight gradients (NodeWgradArgs) ------------------------------------------------
 // One 12-wave workgroup per CU walks its range of 32-node chunks. Each chunk's nine operand slabs
-// (32 x 64 floats each) and gphi are staged in LDS once (row stride 80 floats: the 64 lanes of an MFMA
-// operand read hit 64 distinct banks), so HBM sees every operand row once (the unfused form read h four
-// times and gz twice, 12 row reads per node against 9). Wave w accumulates rows [32 (w & 1), +32) of
-// GEMM w >> 1 with exact f32 MFMAs (v_mfma_f32_16x16x4_f32: the products of the reference's fp32
-// autograd GEMMs, summed in a fixed order), three waves per SIMD; the next chunk's rows are loaded into
-// registers while the current one is multiplied. Job 6 (a 1 x 64 row) is per-thread FMAs.
+// (32 x 64 floats each) are staged in LDS once (row stride 80 floats: the 64 lanes of an MFMA operand
+// read hit 64 distinct banks), so HBM sees every operand row once (the unfused form read h four times
+// and gz twice). Wave w accumulates rows [32 (w & 1), +32) of GEMM w >> 1 with exact f32 MFMAs
+// (v_mfma_f32_16x16x4_f32: the products of the reference's fp32 autograd GEMMs, summed in a fixed
+// order), three waves per SIMD; the next chunk's rows are loaded into registers while the current one
+// is multiplied. node_post runs here too (NodeWgradArgs::post, waves 0..3), on the staged GA / GB: the
+// separate kernel read GA, GB again (26 us per C4 layer).
 constexpr int NW_WAVES = 12, NW_CH = 32, NW_ROW = 80, NW_SLABS = 9;
 constexpr int NW_SLAB = NW_CH * NW_ROW;                                   // floats per staged slab
-constexpr int NW_LDS_FLOATS = NW_SLABS * NW_SLAB + NW_CH + NW_WAVES * 64;   // + gphi + job-6 reduction
+constexpr int NW_LDS_FLOATS = NW_SLABS * NW_SLAB;
+constexpr int NW_LDS_POST = 2 * 4096;                                    // W_A^T | W_B^T fp16 hi/lo (fused node_post)
+// output rows [32 hf, +32) of W x (one fragment set), hf = 0 / 1: 12 of mfma_h16's 24 MFMAs, same chains
+__device__ __forceinline__ void mfma_h16_half(f4 (&acc)[2], const h8* wf, const h8 (&xh)[2], const h8 (&xl)[2],
+                                              int lane, unsigned us, int hf) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    h8 ah[2], al[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      ah[m] = wf[((s * 4 + 2 * hf + m) * 2 + 0) * 64 + lane];
+      al[m] = wf[((s * 4 + 2 * hf + m) * 2 + 1) * 64 + lane];
+    }
+    const h8 xs = h8_scale(xh[s], us);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc[m] = mfma16(ah[m], xh[s], acc[m]);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc[m] = mfma16(al[m], xs, acc[m]);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc[m] = mfma16(ah[m], xl[s], acc[m]);
+  }
+}
 constexpr int NW_SLAB_F4 = NW_CH * 16;                                   // f4 loads per slab (512)
 __global__ __launch_bounds__(NW_WAVES * 64) void node_wgrad_kernel(nonode_tu::NodeWgradArgs p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, il = lane & 15, kg = lane >> 4;
-  // slab order: h, M, z, t (A side), GA, GB, gt, gz, gh (G side)
-  const float* const src[NW_SLABS] = {p.h, p.M, p.z, p.t, p.GA, p.GB, p.gt, p.gz, p.gh};
+  // slab order: h, M, z (A side), ghp (node_post's addend), GA, GB, gt, gz, gh (G side)
+  const float* const src[NW_SLABS] = {p.h, p.M, p.z, p.post.ghp, p.GA, p.GB, p.gt, p.gz, p.gh};
   float* sG = smem;                                 // [slab][node][NW_ROW]
-  float* sPhi = smem + NW_SLABS * NW_SLAB;          // [node]
-  float* sRed = sPhi + NW_CH;                       // [wave][64] job-6 partial sums
+  const h8* sWp = reinterpret_cast<const h8*>(smem + NW_LDS_FLOATS);   // fused node_post fragments
+  const bool post = p.post.ghp != nullptr;
+  if (post) {
+    const f4* wsrc = reinterpret_cast<const f4*>(p.post.bb + BOFF_H16 + BH_WAT * 4096);   // W_A^T | W_B^T
+    for (int i = tid; i < NW_LDS_POST / 4; i += NW_WAVES * 64) reinterpret_cast<f4*>(smem + NW_LDS_FLOATS)[i] = wsrc[i];
+  }
   const int job = wave >> 1, a0 = 2 * (wave & 1);
   constexpr int GS[6] = {4, 5, 6, 7, 7, 8}, AS[6] = {0, 0, 0, 0, 1, 2};
   const int gslab = GS[job], aslab = AS[job];
@@ -232,21 +220,18 @@ __global__ __launch_bounds__(NW_WAVES * 64) void node_wgrad_kernel(nonode_tu::No
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
-  float s6 = 0.f, b6 = 0.f;   // job 6: column lane of t over this thread's nodes; bias (wave 0 only)
   // register prefetch of one chunk: threads tid < 512 load f4 (node tid >> 4, channels 4 (tid & 15) ..)
-  // of every slab (the slab loop is unrolled, so each source pointer is a kernel argument), the
-  // next 32 threads gphi
+  // of every slab (the slab loop is unrolled, so each source pointer is a kernel argument)
   f4 pre[NW_SLABS];
-  float prephi = 0.f;
   const int pnode = (tid >> 4) & 31, pc4 = tid & 15;
   auto fetch = [&](long long c) {
     const long long row = c * NW_CH + pnode;
     const bool ok = tid < NW_SLAB_F4 && row < p.n;
+    long long off = row * 64 + 4 * pc4;
+    asm volatile("" : "+v"(off));   // (one offset, not nine hoisted per-thread source pointers)
 #pragma unroll
-    for (int sl = 0; sl < NW_SLABS; ++sl)   // (a null source: SEGNO has no t / gt, zeros)
-      pre[sl] = (ok && src[sl]) ? *reinterpret_cast<const f4*>(src[sl] + row * 64 + 4 * pc4) : f4{0.f, 0.f, 0.f, 0.f};
-    const long long prow = c * NW_CH + (tid - NW_SLAB_F4);
-    prephi = (p.gphi && tid >= NW_SLAB_F4 && tid < NW_SLAB_F4 + NW_CH && prow < p.n) ? p.gphi[prow] : 0.f;
+    for (int sl = 0; sl < NW_SLABS; ++sl)   // (a null source: SEGNO has no gt, zeros)
+      pre[sl] = (ok && src[sl]) ? *reinterpret_cast<const f4*>(src[sl] + off) : f4{0.f, 0.f, 0.f, 0.f};
   };
   if (c0 < c1) fetch(c0);
 #pragma unroll 1
@@ -256,11 +241,40 @@ __global__ __launch_bounds__(NW_WAVES * 64) void node_wgrad_kernel(nonode_tu::No
 #pragma unroll
       for (int sl = 0; sl < NW_SLABS; ++sl)
         *reinterpret_cast<f4*>(sG + sl * NW_SLAB + pnode * NW_ROW + 4 * pc4) = pre[sl];
-    } else if (tid < NW_SLAB_F4 + NW_CH) {
-      sPhi[tid - NW_SLAB_F4] = prephi;
+    }
+    __syncthreads();
+    // node_post (before the next chunk's prefetch, whose registers it reuses): waves 0..3 (one per
+    // SIMD) take tile wave >> 1 of the chunk, output rows [32 (wave & 1), +32); gh = (ghp + A) + B
+    if (post && wave < 4) {
+      const int tl = wave >> 1, hf = wave & 1;
+      int off = 0;   // (keeps the loop-invariant fragment reads in the loop, see node_bwd_kernel)
+      asm volatile("" : "+v"(off));
+      const long long row = c * NW_CH + 16 * tl + il;
+      const bool ok = row < p.n;
+      f4 o[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+        o[m] = *reinterpret_cast<const f4*>(sG + 3 * NW_SLAB + (16 * tl + il) * NW_ROW + 16 * (2 * hf + m) + 4 * kg);
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {   // GA (slab 4) through W_A^T, GB (slab 5) through W_B^T
+        const float* xr = sG + (4 + pr) * NW_SLAB + (16 * tl + il) * NW_ROW;
+        f4 x[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) x[mt] = *reinterpret_cast<const f4*>(xr + 16 * mt + 4 * kg);
+        h8 xh[2], xl[2];
+        const float inv = cs_split(x, xh, xl);
+        f4 a[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+        mfma_h16_half(a, sWp + off + pr * 1024, xh, xl, lane, h16_us(p.post.bb + BOFF_SCAL, pr ? BH_WBT : BH_WAT), hf);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) o[m] = o[m] + a[m] * inv;
+      }
+      if (ok) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) *reinterpret_cast<f4*>(p.post.gh + row * 64 + 16 * (2 * hf + m) + 4 * kg) = o[m];
+        if (hf == 0 && kg < 3) p.post.gx[row * 3 + kg] = p.post.gxo[row * 3 + kg] + p.post.GX[row * 4 + kg];
+      }
     }
     if (c + 1 < c1) fetch(c + 1);
-    __syncthreads();
     const float* g = sG + gslab * NW_SLAB;
     const float* av = sG + aslab * NW_SLAB;
 #pragma unroll
@@ -278,12 +292,6 @@ __global__ __launch_bounds__(NW_WAVES * 64) void node_wgrad_kernel(nonode_tu::No
         for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[a], xv[b], acc[a][b]);
       }
     }
-    // job 6: thread (column lane, node group wave) over nodes wave, wave + 12, wave + 24
-    for (int node = wave; node < NW_CH; node += NW_WAVES) {
-      const float ph = sPhi[node];
-      s6 = fmaf(ph, sG[3 * NW_SLAB + node * NW_ROW + lane], s6);
-      if (lane == 0) b6 += ph;
-    }
   }
   // partials: this block's [job][64][65]
   float* out = p.partial + (size_t)blockIdx.x * nonode_tu::NW_JOBS * nonode_tu::NW_PART;
@@ -296,22 +304,6 @@ __global__ __launch_bounds__(NW_WAVES * 64) void node_wgrad_kernel(nonode_tu::No
       for (int q = 0; q < 4; ++q) oj[(16 * (a0 + a) + 4 * kg + q) * 65 + 16 * b + il] = acc[a][b][q];
     const float bs = group_sum(bsum[a]);
     if (kg == 0) oj[(16 * (a0 + a) + il) * 65 + 64] = bs;
-  }
-  // job 6: the 12 node groups added in wave order
-  sRed[wave * 64 + lane] = s6;
-  __shared__ float sB6[NW_WAVES];
-  if (lane == 0) sB6[wave] = b6;
-  __syncthreads();
-  if (wave == 0) {
-    float t6 = 0.f;
-    for (int w = 0; w < NW_WAVES; ++w) t6 += sRed[w * 64 + lane];
-    float* o6 = out + (size_t)6 * nonode_tu::NW_PART;
-    o6[lane] = t6;
-    if (lane == 0) {
-      float tb = 0.f;
-      for (int w = 0; w < NW_WAVES; ++w) tb += sB6[w];
-      o6[64] = tb;
-    }
   }
 }
 }  // namespace
@@ -335,7 +327,7 @@ int launch_node_wgrad(const NodeWgradArgs& a_in, int* nblk, hipStream_t s) {
   static std::once_flag once;
   std::call_once(once, [] {
     hipFuncSetAttribute((const void*)node_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        NW_LDS_FLOATS * 4);
+                        (NW_LDS_FLOATS + NW_LDS_POST) * 4);
   });
   NodeWgradArgs a = a_in;
   const long long nch = (a.n + NW_CH - 1) / NW_CH;
@@ -347,16 +339,9 @@ int launch_node_wgrad(const NodeWgradArgs& a_in, int* nblk, hipStream_t s) {
   G = (nch + a.chunks_per_block - 1) / a.chunks_per_block;
   if (G < 1) G = 1;
   *nblk = (int)G;
-  hipLaunchKernelGGL(node_wgrad_kernel, dim3((unsigned)G), dim3(NW_WAVES * 64), NW_LDS_FLOATS * 4, s, a);
+  const int lds = (NW_LDS_FLOATS + (a.post.ghp ? NW_LDS_POST : 0)) * 4;
+  hipLaunchKernelGGL(node_wgrad_kernel, dim3((unsigned)G), dim3(NW_WAVES * 64), lds, s, a);
   return check_launch("node_wgrad_kernel");
 }
 
-int launch_node_post(const NodePostArgs& a, hipStream_t s) {
-  const int ntile = (a.n + 15) / 16;
-  const int want = (ntile + NP_WAVES - 1) / NP_WAVES;
-  const int G = want < 2 * num_cus() ? want : 2 * num_cus();
-  if (G < 1) return NONODE_OK;
-  hipLaunchKernelGGL(node_post_kernel, dim3(G), dim3(NP_WAVES * 64), 0, s, a);
-  return check_launch("node_post_kernel");
-}
 }  // namespace nonode_tu

@@ -11,7 +11,7 @@
 //   node_bwd_kernel   x/v update + node MLP reverse (basic.py:174-185): gF, gM, gv, part of gh
 //   edge_bwd_kernel   per-edge recompute + reverse of the coordinate and edge MLPs (basic.py:
 //                     170-173, 107-144): per-receiver / per-sender sums GA, GB and gx terms
-//   node_post_kernel  gh = part + W_A^T GA + W_B^T GB,  gx = gx + edge terms
+//   node_wgrad_kernel gh = part + W_A^T GA + W_B^T GB,  gx = gx + edge terms (and the node-level GEMMs)
 //   tconvx_bwd / tconv_bwd  TimeConv_x / TimeConv reverse (layer_no.py:80-178)
 // Weight gradients are GEMMs over edges or nodes, C = sum_k G[k] (x) A[k]: the kernels above write
 // the per-row operands, gemm_tn_partial sums K-slices per workgroup and gemm_reduce adds the
@@ -2023,30 +2023,28 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
     // edge Linear 1 scalar columns [s | e] (EGNO order [s, h_i, h_j, e], basic.py:152-154, 170)
     red(EW_FEAT, 64, nf, lg.edge_w1, ld1, nullptr, 1, 2 * HID + 1);
   }
-  {
-    nonode_tu::NodePostArgs pa{r.n, w.ghp, w.GA, w.GB, r.gx, w.GX, r.bb, r.g_hin, r.g_xin};
-    if (int rc = nonode_tu::launch_node_post(pa, s)) return rc;
-  }
+  const nonode_tu::NodePostArgs pa{r.n, w.ghp, w.GA, w.GB, r.gx, w.GX, r.bb, r.g_hin, r.g_xin};
   // ---- node-level weight gradients of this layer: one node_wgrad_kernel launch (NodeWgradArgs),
   // its and the edge-level reductions in another ----
   // edge Linear 1 h_i / h_j blocks; its bias gradient sum_e gz1 = sum_i GA_i comes with the h_i block
   {
     nonode_tu::NodeWgradArgs wa{};
     wa.n = (long long)n;
-    wa.h = r.he; wa.M = r.Ms; wa.z = w.op_z; wa.t = nullptr;   // job 6 (node_v output row): node_bwd's p6
-    wa.GA = w.GA; wa.GB = w.GB; wa.gt = w.op_gt; wa.gz = w.op_gz; wa.gh = r.gh; wa.gphi = nullptr;
+    wa.h = r.he; wa.M = r.Ms; wa.z = w.op_z;
+    wa.GA = w.GA; wa.GB = w.GB; wa.gt = w.op_gt; wa.gz = w.op_gz; wa.gh = r.gh;
     wa.partial = w.partial;
+    wa.post = pa;
     int nblk = 0;
     if (int rc = nonode_tu::launch_node_wgrad(wa, &nblk, s)) return rc;
-    struct { float* dst; int ld, col0; float* bias; } d[nonode_tu::NW_JOBS] = {
+    struct { float* dst; int ld, col0; float* bias; } d[nonode_tu::NW_JOBS + 1] = {
         {lg.edge_w1, ld1, 1, lg.edge_b1}, {lg.edge_w1, ld1, 1 + HID, nullptr}, {lg.vel_w1, 64, 0, lg.vel_b1},
         {lg.node_w1, 128, 0, lg.node_b1}, {lg.node_w1, 128, HID, nullptr},   {lg.node_w2, 64, 0, lg.node_b2},
         {lg.vel_w2, 64, 0, lg.vel_b2}};
     constexpr long long pstride = (long long)nonode_tu::NW_JOBS * nonode_tu::NW_PART;
-    for (int j = 0; j < 6; ++j)
+    for (int j = 0; j < nonode_tu::NW_JOBS; ++j)
       rjobs[nred++] = ReduceJob{w.partial + (size_t)j * nonode_tu::NW_PART, nblk, 64, 64, d[j].dst, d[j].ld,
                                 d[j].col0, 1, d[j].bias, 0, 1.f, 1 << 30, 0, pstride};
-    // the node_v output row (job 6) from node_bwd's per-wave partials
+    // the node_v output row (d[6]) from node_bwd's per-workgroup partials
     rjobs[nred++] = ReduceJob{w.p6, n6, 1, 64, d[6].dst, d[6].ld, d[6].col0, 1, d[6].bias, 0, 1.f, 1 << 30, 0, 65};
     return launch_reduce_batch(rjobs, nred, s);
   }
@@ -2202,7 +2200,7 @@ int nonode_egno_backward_frames(int B, int N, int T, int n_layers, int in_node, 
 // SEGNO training: forward_step (model.py:95-102) = T applications of SEGNO_GCL (gcl.py:111-119) with
 // shared weights and dt = 1/T, run as T single-substep launches that save every substep's inputs and
 // message / force sums; the reverse pass walks the substeps backwards on the EGNO backward kernels
-// (edge_bwd_kernel with the per-edge clamp of gcl.py:99-100, node_post_kernel, the GEMMs) and adds
+// (edge_bwd_kernel with the per-edge clamp of gcl.py:99-100, node_wgrad_kernel) and adds
 // every substep's weight gradients into the same outputs. Replaces loss.backward() of
 // train_nbody.py:168-179 through forward_step.
 namespace {
@@ -2401,18 +2399,16 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       // edge Linear 1 scalar columns [s | e] (SEGNO order [h_i, h_j, s, e], gcl.py:78)
       red(EW_FEAT, 64, 1 + ne, lg.edge_w1, ld1, nullptr, 2 * HID);
     }
-    {
-      nonode_tu::NodePostArgs pa{(int)n, w.ghp, w.GA, w.GB, gx, w.GX, bblob, w.gh[nxt], w.gx[nxt]};
-      if (int rc = nonode_tu::launch_node_post(pa, s)) return rc;
-    }
+    const nonode_tu::NodePostArgs pa{(int)n, w.ghp, w.GA, w.GB, gx, w.GX, bblob, w.gh[nxt], w.gx[nxt]};
     // node-level weight gradients of this substep (edge Linear 1 h_i / h_j blocks, node MLP): one
     // node_wgrad_kernel launch (jobs 0, 1, 3, 4, 5; no node_v MLP) and one reduction launch
     {
       nonode_tu::NodeWgradArgs wa{};
       wa.n = (long long)n;
-      wa.h = hs; wa.M = Ms; wa.z = w.op_z; wa.t = nullptr;
-      wa.GA = w.GA; wa.GB = w.GB; wa.gt = nullptr; wa.gz = w.op_gz; wa.gh = gh; wa.gphi = nullptr;
+      wa.h = hs; wa.M = Ms; wa.z = w.op_z;
+      wa.GA = w.GA; wa.GB = w.GB; wa.gt = nullptr; wa.gz = w.op_gz; wa.gh = gh;
       wa.partial = w.partial;
+      wa.post = pa;
       int nblk = 0;
       if (int rc = nonode_tu::launch_node_wgrad(wa, &nblk, s)) return rc;
       struct { int job; float* dst; int ld, col0; float* bias; } d[5] = {

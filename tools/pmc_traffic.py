@@ -28,7 +28,7 @@ def kernel_key(name):
         return f"edge_bwd_kernel<pass {m.group(1)}>" if m else "edge_bwd_kernel"
     if "tconv_bwd_kernel" in name:
         return "tconv_bwd_kernel"
-    for k in ("temb_kernel", "embed_kernel", "node_bwd_kernel", "node_post_kernel", "node_wgrad_kernel"):
+    for k in ("temb_kernel", "embed_kernel", "node_bwd_kernel", "node_wgrad_kernel"):
         if k in name:
             return k
     return None
