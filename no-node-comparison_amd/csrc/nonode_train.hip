@@ -1370,8 +1370,8 @@ int launch_edge_bwd(int ne, EdgeBwdArgs a, int G, hipStream_t s) {
 
 // backward mixing fragments: mode m < M, c = re|im: frag(mo, mt)[lane][q] = W[i][o][m][c] with
 // i = 16 mo + (l & 15), o = 16 mt + 4 (l >> 4) + q  (A operand over o, unscaled)
-__global__ void tconv_pack_bwd_kernel(const float* w, int Mfull, int M, float* out) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+// (run by the extra workgroups of tconvx_bwd_kernel: one element per thread)
+__device__ __forceinline__ void tconv_pack_bwd(const float* w, int Mfull, int M, float* out, int d) {
   if (d >= M * 2 * 4096) return;
   const int mat = d >> 12, r = d & 4095;
   const int m = mat >> 1, c = mat & 1;
@@ -1380,14 +1380,15 @@ __global__ void tconv_pack_bwd_kernel(const float* w, int Mfull, int M, float* o
   out[d] = w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
 }
 
-// the TimeConv_x weight gradient from tconvx_bwd_kernel's per-block sums [nb][io][MMAX_T][2]: block d
-// (one per output of g_tconvx [2][2][Mfull][2], modes >= M zero) adds the nb partial rows' entry with
-// 256 threads (strided sums, then a fixed-order tree in LDS: deterministic). (One 256-thread block for
-// every output, three lanes per output, had made this a 21 us serial chain per C4 layer.)
-__global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int nb, int M, int Mfull, float* dst) {
+// the TimeConv_x weight gradient from tconvx_bwd_kernel's per-block sums [nb][io][MMAX_T][2]: workgroup d
+// (one per output of g_tconvx [2][2][Mfull][2], modes >= M zero; the extra workgroups of
+// tconv_wgrad_reduce) adds the nb partial rows' entry with 256 threads (strided sums, then a fixed-order
+// tree in LDS: deterministic). (One 256-thread block for every output, three lanes per output, had made
+// this a 21 us serial chain per C4 layer.)
+__device__ __forceinline__ void tconvx_grad_finish(const float* part, int nb, int M, int Mfull, float* dst, int d) {
   constexpr int cnt = 2 * 2 * MMAX_T * 2;   // partial row length (72)
   __shared__ float red[256];
-  const int d = blockIdx.x, io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
+  const int io = d / (Mfull * 2), m = (d / 2) % Mfull, c = d & 1;
   float v = 0.f;
   if (m < M) {
     const int k = (io * MMAX_T + m) * 2 + c;
@@ -1403,8 +1404,14 @@ __global__ __launch_bounds__(256) void tconvx_grad_finish(const float* part, int
 }
 
 // dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
-// strided partial lanes, combined in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst) {
+// strided partial lanes, combined in a fixed order (deterministic). Workgroups from nred on run
+// tconvx_grad_finish (the TimeConv_x weight gradient, xpart -> g_txw) in the same launch.
+__global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst,
+                                                          int nred, const float* xpart, int nbx, float* g_txw) {
+  if ((int)blockIdx.x >= nred) {
+    tconvx_grad_finish(xpart, nbx, M, Mfull, g_txw, blockIdx.x - nred);
+    return;
+  }
   // 16 outputs x 16 partial lanes per block, one float4 of 4 consecutive outputs per load (1 KB per
   // wave and partial row instead of 256 B; the scalar form ran at ~0.9 TB/s)
   __shared__ f4 red[16][17];
@@ -1434,7 +1441,12 @@ template <int MM>
 __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x,
                                                                 const float* v, const float* lm, const float* gxo,
                                                                 const float* gvo, const float* w, float* gx,
-                                                                float* gv, float* part, int frames) {
+                                                                float* gv, float* part, int frames, int nbx,
+                                                                const float* tw, float* twb) {
+  if ((int)blockIdx.x >= nbx) {   // extra workgroups: the TimeConv backward's mixing fragments
+    tconv_pack_bwd(tw, Mfull, M, twb, (blockIdx.x - nbx) * TX_THREADS + threadIdx.x);
+    return;
+  }
   constexpr int CNT = 2 * 2 * MM * 2;   // this build's partials; the row written is [io][MMAX_T][2]
   // twiddles cos / sin(pi 2 m t / T) once per block in LDS (the same float values a per-thread double
   // cospi / sinpi gave; that software double trig per thread had made this kernel ~38 us at C4)
@@ -2067,13 +2079,11 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   const int nbx = (BN * 3 + TX_THREADS - 1) / TX_THREADS;
   // mode-bound builds: 2 (C4), 4, 9 (registers of the per-thread partials)
   auto txk = M <= 2 ? tconvx_bwd_kernel<2> : (M <= 4 ? tconvx_bwd_kernel<4> : tconvx_bwd_kernel<MMAX_T>);
-  hipLaunchKernelGGL(txk, dim3(nbx), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
-                     r.lm, r.gx, r.gv, r.txw, r.g_xin, r.g_vin, w.xpart, r.frames);
+  // (+ the workgroups that pack the TimeConv backward's fragments, tconv_pack_bwd)
+  const int npack = (M * 2 * 4096 + TX_THREADS - 1) / TX_THREADS;
+  hipLaunchKernelGGL(txk, dim3(nbx + npack), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
+                     r.lm, r.gx, r.gv, r.txw, r.g_xin, r.g_vin, w.xpart, r.frames, nbx, r.tw, w.twb);
   if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
-  hipLaunchKernelGGL(tconvx_grad_finish, dim3(4 * modes * 2), dim3(256), 0, s, w.xpart, nbx, M, modes, r.g_txw);
-  if (int rc = check_launch("tconvx_grad_finish")) return rc;
-  hipLaunchKernelGGL(tconv_pack_bwd_kernel, dim3((M * 2 * 4096 + 255) / 256), dim3(256), 0, s, r.tw, modes, M, w.twb);
-  if (int rc = check_launch("tconv_pack_bwd_kernel")) return rc;
   TconvBwdArgs ta;
   ta.BN = BN; ta.T = T; ta.M = M; ta.ntiles = (BN + 15) / 16;
   ta.h = r.hs; ta.gout = r.gh; ta.wp = w.twf; ta.wb = w.twb; ta.gh = r.g_hin; ta.wpart = w.tpart;
@@ -2084,8 +2094,9 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   TG = tgw < TG ? tgw : TG;
   if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
   if (modes > M) hipMemsetAsync(r.g_tw, 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
-  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3((M * 2 * 4096 / 4 + 15) / 16), dim3(256), 0, s, w.tpart, TG, M, modes,
-                     r.g_tw);
+  const int nred = (M * 2 * 4096 / 4 + 15) / 16;   // (+ one tconvx_grad_finish workgroup per g_txw entry)
+  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3(nred + 4 * modes * 2), dim3(256), 0, s, w.tpart, TG, M, modes,
+                     r.g_tw, nred, w.xpart, nbx, r.g_txw);
   return check_launch("tconv_wgrad_reduce");
 }
 
