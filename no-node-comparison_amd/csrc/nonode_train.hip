@@ -1403,36 +1403,6 @@ __device__ __forceinline__ void tconvx_grad_finish(const float* part, int nb, in
   if (threadIdx.x == 0) dst[d] = red[0];
 }
 
-// dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
-// strided partial lanes, combined in a fixed order (deterministic). Workgroups from nred on run
-// tconvx_grad_finish (the TimeConv_x weight gradient, xpart -> g_txw) in the same launch.
-__global__ __launch_bounds__(256) void tconv_wgrad_reduce(const float* part, int nblk, int M, int Mfull, float* dst,
-                                                          int nred, const float* xpart, int nbx, float* g_txw) {
-  if ((int)blockIdx.x >= nred) {
-    tconvx_grad_finish(xpart, nbx, M, Mfull, g_txw, blockIdx.x - nred);
-    return;
-  }
-  // 16 outputs x 16 partial lanes per block, one float4 of 4 consecutive outputs per load (1 KB per
-  // wave and partial row instead of 256 B; the scalar form ran at ~0.9 TB/s)
-  __shared__ f4 red[16][17];
-  const int per = M * 2 * 4096;
-  const int ol = threadIdx.x & 15, pl = threadIdx.x >> 4;
-  const int d4 = blockIdx.x * 16 + ol;   // float4 index
-  f4 s = f4{0.f, 0.f, 0.f, 0.f};
-  if (4 * d4 < per)
-    for (int b = pl; b < nblk; b += 16) s += reinterpret_cast<const f4*>(part + (size_t)b * per)[d4];
-  red[pl][ol] = s;
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const int oq = threadIdx.x >> 2, c4 = threadIdx.x & 3;   // output float4 oq, component c4
-  const int d = 4 * (blockIdx.x * 16 + oq) + c4;
-  if (d >= per) return;
-  float tot = 0.f;
-  for (int q = 0; q < 16; ++q) tot += red[q][oq][c4];
-  const int mc = d >> 12, r = d & 4095, m = mc >> 1, c = mc & 1, i = r >> 6, o = r & 63;
-  dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = tot;
-}
-
 // TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. Writes gx, gv.
 // One thread per (column c, coordinate d); the block sums its threads' weight-gradient terms in a
 // fixed order and writes one row of 2*2*MMAX_T*2 partials (tconvx_grad_finish adds the blocks' rows).
@@ -1658,12 +1628,12 @@ __global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__
 // (columns j >= split go to col1 + (j - split) instead: the [s | ... | e] blocks of edge W1)
 __device__ __forceinline__ void gemm_reduce_body(const float* partial, int nblk, int M, int N, float* dst, int ld,
                                                  int col0, int cs, float* bias, int accumulate, float scale,
-                                                 int split, int col1, long long pstride) {
+                                                 int split, int col1, long long pstride, int bx) {
   __shared__ float red[16][17];
   const int NO = M * (N + 1);
-  if ((int)blockIdx.x * 16 >= NO) return;   // whole block (a batch's grid covers its largest job)
+  if (bx * 16 >= NO) return;   // whole block (a batch's grid covers its largest job)
   const int ol = threadIdx.x & 15, part = threadIdx.x >> 4;
-  const int o = blockIdx.x * 16 + ol;
+  const int o = bx * 16 + ol;
   // eight independent partial sums per thread (a fixed tree: deterministic), so the loads of a
   // thread are in flight together
   float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1692,7 +1662,7 @@ __device__ __forceinline__ void gemm_reduce_body(const float* partial, int nblk,
 __global__ __launch_bounds__(256) void gemm_reduce(const float* partial, int nblk, int M, int N, float* dst, int ld,
                                                    int col0, int cs, float* bias, int accumulate, float scale,
                                                    int split, int col1, long long pstride) {
-  gemm_reduce_body(partial, nblk, M, N, dst, ld, col0, cs, bias, accumulate, scale, split, col1, pstride);
+  gemm_reduce_body(partial, nblk, M, N, dst, ld, col0, cs, bias, accumulate, scale, split, col1, pstride, blockIdx.x);
 }
 // a batch of reductions in one launch (blockIdx.y = job)
 struct ReduceJob {
@@ -1704,21 +1674,76 @@ struct ReduceBatchArgs { ReduceJob j[REDUCE_BATCH_MAX]; };
 __global__ __launch_bounds__(256) void gemm_reduce_batch(ReduceBatchArgs a) {
   const ReduceJob& r = a.j[blockIdx.y];
   gemm_reduce_body(r.partial, r.nblk, r.M, r.N, r.dst, r.ld, r.col0, r.cs, r.bias, r.accumulate, r.scale, r.split,
-                   r.col1, r.pstride);
+                   r.col1, r.pstride, blockIdx.x);
+}
+// the batch's arguments and its grid width (blocks per job)
+int reduce_batch_args(const ReduceJob* jobs, int count, ReduceBatchArgs* a, int* gx) {
+  if (count > REDUCE_BATCH_MAX) return fail(NONODE_EINVAL, "reduce batch of %d", count);
+  *a = ReduceBatchArgs{};
+  *gx = 1;
+  for (int i = 0; i < count; ++i) {
+    a->j[i] = jobs[i];
+    const int NO = jobs[i].M * (jobs[i].N + 1);
+    *gx = (NO + 15) / 16 > *gx ? (NO + 15) / 16 : *gx;
+  }
+  return NONODE_OK;
 }
 int launch_reduce_batch(const ReduceJob* jobs, int count, hipStream_t s) {
   if (count <= 0) return NONODE_OK;
-  if (count > REDUCE_BATCH_MAX) return fail(NONODE_EINVAL, "reduce batch of %d", count);
-  ReduceBatchArgs a{};
+  ReduceBatchArgs a;
   int gx = 1;
-  for (int i = 0; i < count; ++i) {
-    a.j[i] = jobs[i];
-    const int NO = jobs[i].M * (jobs[i].N + 1);
-    gx = (NO + 15) / 16 > gx ? (NO + 15) / 16 : gx;
-  }
+  if (int rc = reduce_batch_args(jobs, count, &a, &gx)) return rc;
   hipLaunchKernelGGL(gemm_reduce_batch, dim3(gx, count), dim3(256), 0, s, a);
   return check_launch("gemm_reduce_batch");
 }
+
+// dst weights1 [i][o][Mfull][2] = sum over nblk partials, modes < M. 256 threads = 64 outputs x 4
+// strided partial lanes, combined in a fixed order (deterministic). The same launch runs
+// tconvx_grad_finish (the TimeConv_x weight gradient, xpart -> g_txw) and the EGNN layer's reductions
+// (gemm_reduce_batch jobs, deferred to here) in its further workgroups.
+struct TconvReduceArgs {
+  const float* part; int nblk, M, Mfull; float* dst;     // TimeConv weight gradient (tconv_bwd partials)
+  int nred;                                              // its workgroups
+  const float* xpart; int nbx; float* g_txw; int nfin;   // TimeConv_x weight gradient: nfin workgroups
+  ReduceBatchArgs rb; int rb_count, rb_gx;               // the EGNN layer's deferred reductions
+};
+__global__ __launch_bounds__(256) void tconv_wgrad_reduce(TconvReduceArgs a) {
+  const int blk = blockIdx.x;
+  if (blk >= a.nred + a.nfin) {   // a deferred gemm_reduce_batch job (rb_gx workgroups per job)
+    const int b = blk - a.nred - a.nfin, jj = b / a.rb_gx;
+    const ReduceJob& r = a.rb.j[jj];
+    gemm_reduce_body(r.partial, r.nblk, r.M, r.N, r.dst, r.ld, r.col0, r.cs, r.bias, r.accumulate, r.scale, r.split,
+                     r.col1, r.pstride, b - jj * a.rb_gx);
+    return;
+  }
+  if (blk >= a.nred) {
+    tconvx_grad_finish(a.xpart, a.nbx, a.M, a.Mfull, a.g_txw, blk - a.nred);
+    return;
+  }
+  const float* part = a.part;
+  const int nblk = a.nblk, M = a.M, Mfull = a.Mfull;
+  float* dst = a.dst;
+  // 16 outputs x 16 partial lanes per block, one float4 of 4 consecutive outputs per load (1 KB per
+  // wave and partial row instead of 256 B; the scalar form ran at ~0.9 TB/s)
+  __shared__ f4 red[16][17];
+  const int per = M * 2 * 4096;
+  const int ol = threadIdx.x & 15, pl = threadIdx.x >> 4;
+  const int d4 = blk * 16 + ol;   // float4 index
+  f4 s = f4{0.f, 0.f, 0.f, 0.f};
+  if (4 * d4 < per)
+    for (int b = pl; b < nblk; b += 16) s += reinterpret_cast<const f4*>(part + (size_t)b * per)[d4];
+  red[pl][ol] = s;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int oq = threadIdx.x >> 2, c4 = threadIdx.x & 3;   // output float4 oq, component c4
+  const int d = 4 * (blk * 16 + oq) + c4;
+  if (d >= per) return;
+  float tot = 0.f;
+  for (int q = 0; q < 16; ++q) tot += red[q][oq][c4];
+  const int mc = d >> 12, r = d & 4095, m = mc >> 1, c = mc & 1, i = r >> 6, o = r & 63;
+  dst[(((size_t)i * 64 + o) * Mfull + m) * 2 + c] = tot;
+}
+
 
 struct Gemm {
   float* partial;
@@ -1997,7 +2022,10 @@ struct LayerRev {
   const nonode_layer_grads* lg;
   float *g_xin, *g_vin, *g_hin;
 };
-int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
+// defer (non-null): the layer's reductions are returned in *defer (count in defer->n) for a later
+// launch (tconv_reverse runs them beside its own) instead of launched here
+struct DeferredReduce { ReduceJob j[REDUCE_BATCH_MAX]; int n = 0; };
+int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s, DeferredReduce* defer = nullptr) {
   const size_t n = (size_t)r.n;
   const int N = r.N, ne = r.ne, ld1 = 2 * HID + 1 + ne;
   const nonode_layer_grads& lg = *r.lg;
@@ -2058,6 +2086,11 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s) {
                                 d[j].col0, 1, d[j].bias, 0, 1.f, 1 << 30, 0, pstride};
     // the node_v output row (d[6]) from node_bwd's per-workgroup partials
     rjobs[nred++] = ReduceJob{w.p6, n6, 1, 64, d[6].dst, d[6].ld, d[6].col0, 1, d[6].bias, 0, 1.f, 1 << 30, 0, 65};
+    if (defer) {
+      for (int i = 0; i < nred; ++i) defer->j[i] = rjobs[i];
+      defer->n = nred;
+      return NONODE_OK;
+    }
     return launch_reduce_batch(rjobs, nred, s);
   }
 }
@@ -2073,7 +2106,7 @@ struct TconvRev {
   const float *gh, *gx, *gv;
   float *g_hin, *g_xin, *g_vin, *g_tw, *g_txw;
 };
-int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
+int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s, const DeferredReduce* defer = nullptr) {
   const int BN = r.BN, T = r.T, M = r.M, modes = r.modes;
   // g_txw [2][2][Mfull][2]: one partial row per tconvx block, added in block order (modes >= M zero)
   const int nbx = (BN * 3 + TX_THREADS - 1) / TX_THREADS;
@@ -2095,8 +2128,17 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s) {
   if (int rc = launch_tconv_bwd(M, ta, TG, s)) return rc;
   if (modes > M) hipMemsetAsync(r.g_tw, 0, (size_t)64 * 64 * modes * 2 * sizeof(float), s);   // bins >= M
   const int nred = (M * 2 * 4096 / 4 + 15) / 16;   // (+ one tconvx_grad_finish workgroup per g_txw entry)
-  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3(nred + 4 * modes * 2), dim3(256), 0, s, w.tpart, TG, M, modes,
-                     r.g_tw, nred, w.xpart, nbx, r.g_txw);
+  TconvReduceArgs ra;
+  ra.part = w.tpart; ra.nblk = TG; ra.M = M; ra.Mfull = modes; ra.dst = r.g_tw; ra.nred = nred;
+  ra.xpart = w.xpart; ra.nbx = nbx; ra.g_txw = r.g_txw; ra.nfin = 4 * modes * 2;
+  ra.rb_count = defer ? defer->n : 0;
+  ra.rb_gx = 1;
+  if (ra.rb_count > 0) {
+    if (int rc = reduce_batch_args(defer->j, defer->n, &ra.rb, &ra.rb_gx)) return rc;
+  } else {
+    ra.rb = ReduceBatchArgs{};
+  }
+  hipLaunchKernelGGL(tconv_wgrad_reduce, dim3(nred + ra.nfin + ra.rb_count * ra.rb_gx), dim3(256), 0, s, ra);
   return check_launch("tconv_wgrad_reduce");
 }
 
@@ -2144,7 +2186,8 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     lr.edge_fea = edge_fea; lr.bb = bblobs[l];
     lr.gx = gx; lr.gv = gv; lr.gh = gh; lr.lg = &layer_grads[l];
     lr.g_xin = w.gxe; lr.g_vin = w.gve; lr.g_hin = w.ghe;
-    if (int rc = egnn_layer_reverse(lr, w, s)) return rc;
+    DeferredReduce dr;   // with TimeConv, the layer's reductions run in tconv_reverse's last launch
+    if (int rc = egnn_layer_reverse(lr, w, s, tc ? &dr : nullptr)) return rc;
     const int nxt = cur ^ 1;
     if (!tc) {   // no TimeConv: the layer-input gradients are the next (earlier) layer's output gradients
       hipMemcpyAsync(w.gx[nxt], w.gxe, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
@@ -2163,7 +2206,7 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     tr.mask = st.mask + (size_t)l * T * ((BN + 15) / 16) * 16;
     tr.gh = w.ghe; tr.gx = w.gxe; tr.gv = w.gve;
     tr.g_hin = w.gh[nxt]; tr.g_xin = w.gx[nxt]; tr.g_vin = w.gv[nxt]; tr.g_tw = g_tconv[l]; tr.g_txw = g_tconvx[l];
-    if (int rc = tconv_reverse(tr, w, s)) return rc;
+    if (int rc = tconv_reverse(tr, w, s, &dr)) return rc;
     cur = nxt;
     gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
   }
