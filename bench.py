@@ -594,9 +594,10 @@ def run_egno_train(args, world, rank, dev, backend):
         records = _lib.profile_end()
     value = plan["B_global"] * args.steps / el
     res = _result(args, world, plan, el / args.steps * 1e3, value,
-                  f"C4: EGNO training step (fwd + bwd + 1 all-reduce + Adam), charged N={N}, T={T}, B={B} per GPU",
+                  f"C4: EGNO training step (fwd + bwd{' + 1 all-reduce' if world > 1 else ''} + Adam), charged N={N}, T={T}, B={B} per GPU",
                   {"n_balls": N, "num_timesteps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
-                   "parallelism": f"data-parallel x{world}, one {backend or 'no'} all-reduce per step"},
+                   "parallelism": (f"data-parallel x{world}, one {backend} all-reduce per step" if backend else
+                                   "single GPU, no all-reduce")},
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0, loss=float(loss.detach()))
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
@@ -738,10 +739,11 @@ def run_segno_train(args, world, rank, dev, backend):
         records = _lib.profile_end()
     value = plan["B_global"] * args.steps / el
     res = _result(args, world, plan, el / args.steps * 1e3, value,
-                  f"SEGNO training step (forward_step of {T} substeps + MSE + HIP reverse pass + 1 all-reduce + "
-                  f"Adam), charged N={N}, B={B} per GPU",
+                  f"SEGNO training step (forward_step of {T} substeps + MSE + HIP reverse pass"
+                  f"{' + 1 all-reduce' if world > 1 else ''} + Adam), charged N={N}, B={B} per GPU",
                   {"n_balls": N, "substeps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
-                   "parallelism": f"data-parallel x{world}, one {backend or 'no'} all-reduce per step"},
+                   "parallelism": (f"data-parallel x{world}, one {backend} all-reduce per step" if backend else
+                                   "single GPU, no all-reduce")},
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0)
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]

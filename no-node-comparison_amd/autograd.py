@@ -54,6 +54,9 @@ class EGNOTrain(torch.autograd.Function):
         ctx.model, ctx.B, ctx.N, ctx.Bt = model, B, N, Bt
         ctx.state, ctx.lm, ctx.ef = state, lm, ef
         ctx.n_params = len(params)
+        sink = getattr(model, "_train_state_sink", None)
+        if sink is not None:   # tests: the saved state (its head holds TimeConv's LeakyReLU decisions)
+            sink.append(state)
         # the backward repacks the parameters' current values: saving them lets autograd's version
         # check raise if any was modified in place between forward and backward (e.g. an optimizer
         # step before a second backward), instead of returning gradients for the wrong weights

@@ -1880,11 +1880,14 @@ int nonode_pack_layer(const nonode_layer_weights* w, int variant, int hidden, in
 int nonode_pack_layers(const nonode_layer_weights* const* w, int n_layers, int variant, int hidden,
                        int n_edge_feat, float* const* blobs, void* stream) {
   if (!w || !blobs || n_layers < 0) return fail(NONODE_EINVAL, "pack_layers: null pointer");
+  // every layer is validated before the first launch: a bad entry leaves every blob untouched
+  std::vector<PackArgs> args(n_layers);
+  for (int l = 0; l < n_layers; ++l)
+    if (int rc = pack_args(w[l], variant, hidden, n_edge_feat, blobs[l], &args[l])) return rc;
   for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
     const int cnt = n_layers - l0 < PACK_MAX ? n_layers - l0 : PACK_MAX;
     PackBatch pb{};
-    for (int k = 0; k < cnt; ++k)
-      if (int rc = pack_args(w[l0 + k], variant, hidden, n_edge_feat, blobs[l0 + k], &pb.a[k])) return rc;
+    for (int k = 0; k < cnt; ++k) pb.a[k] = args[l0 + k];
     hipLaunchKernelGGL(pack_kernel, dim3(32, 16, cnt), dim3(256), 0, (hipStream_t)stream, pb);
     if (int rc = check_launch("pack_kernel")) return rc;
   }
@@ -1900,11 +1903,12 @@ int nonode_pack_tconvs(const float* const* tconv_w, int n_layers, int modes, int
     return fail(NONODE_EUNSUPPORTED, "pack_tconv: modes=%d T=%d", modes, T);
   const int M = effective_modes(T, modes);
   const int n = (int)tconv_blob_floats(M);
+  for (int l = 0; l < n_layers; ++l)   // validated before the first launch
+    if (!tconv_w[l] || !blobs[l]) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
   for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
     const int cnt = n_layers - l0 < PACK_MAX ? n_layers - l0 : PACK_MAX;
     TconvPackBatch tb{};
     for (int k = 0; k < cnt; ++k) {
-      if (!tconv_w[l0 + k] || !blobs[l0 + k]) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
       tb.w[k] = tconv_w[l0 + k];
       tb.out[k] = blobs[l0 + k];
     }

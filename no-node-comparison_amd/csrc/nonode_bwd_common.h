@@ -240,7 +240,6 @@ struct TconvBwdArgs {
   int BN, T, M, ntiles;
   const float* h;      // TimeConv input [T][BN][64]
   const float* gout;   // gradient of its output
-  const float* wp;     // forward fragments (tconv_pack_kernel layout)
   const float* wb;     // backward fragments (tconv_pack_bwd_kernel layout)
   float* gh;           // gradient of the input
   float* wpart;        // [grid][M][2][64][64]

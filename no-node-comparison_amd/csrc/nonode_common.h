@@ -13,6 +13,7 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
+#include <vector>
 
 #include "nonode.h"
 

@@ -1811,7 +1811,7 @@ struct BwdWs {
   float *wpart;
   float *stash, *stash_c;                // edge backward pass A -> pass B ((N - 1) n rows)
   float *Pn, *Qn;                        // edge backward pass A -> pass B: node projections (n rows)
-  float *twf, *twb, *tpart, *xpart;
+  float *twb, *tpart, *xpart;
   float *partial;
   size_t floats;
 };
@@ -1831,7 +1831,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   const size_t npad = n + 16 * EB_MAX_BLOCKS;   // (N - 1) x (n + 16 G) handoff rows, G <= EB_MAX_BLOCKS
   w.stash = take(npad * (N - 1) * 64); w.stash_c = take(npad * (N - 1));
   w.Pn = take(n * 64); w.Qn = take(n * 64);
-  w.twf = take((size_t)(1 + 3 * (M - 1)) * 4096); w.twb = take((size_t)M * 2 * 4096);
+  w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take((BN * 3 + TX_THREADS - 1) / TX_THREADS * (2 * 2 * MMAX_T * 2));   // one row per tconvx block
   // gemm_tn_partial partials (one per block), or node_wgrad_kernel's (one [NW_JOBS][64][65] per block)
@@ -1860,6 +1860,9 @@ int pack_bwd_args(const nonode_layer_weights* w, int variant, int hidden, int n_
     return fail(NONODE_EUNSUPPORTED, "pack_layer_bwd: hidden=%d n_edge_feat=%d", hidden, n_edge_feat);
   const bool egno = variant == NONODE_VARIANT_EGNO;
   if (!egno && variant != NONODE_VARIANT_SEGNO) return fail(NONODE_EINVAL, "pack_layer_bwd: variant %d", variant);
+  if (!w->edge_w1 || !w->edge_b1 || !w->edge_w2 || !w->edge_b2 || !w->coord_w1 || !w->coord_b1 ||
+      !w->coord_w2 || !w->coord_b2 || !w->node_w1 || !w->node_b1 || !w->node_w2 || !w->node_b2)
+    return fail(NONODE_EINVAL, "pack_layer_bwd: missing weight pointer");
   if (egno && (!w->vel_w1 || !w->vel_b1 || !w->vel_w2 || !w->vel_b2))
     return fail(NONODE_EINVAL, "pack_layer_bwd: EGNO needs node_v_net weights");
   PackArgs& a = *out;
@@ -1889,11 +1892,14 @@ int nonode_pack_layer_bwd(const nonode_layer_weights* w, int variant, int hidden
 int nonode_pack_layers_bwd(const nonode_layer_weights* const* w, int n_layers, int variant, int hidden,
                            int n_edge_feat, float* const* bblobs, void* stream) {
   if (!w || !bblobs || n_layers < 0) return fail(NONODE_EINVAL, "pack_layer_bwd: null pointer");
+  // every layer is validated before the first launch: a bad entry leaves every blob untouched
+  std::vector<PackArgs> args(n_layers);
+  for (int l = 0; l < n_layers; ++l)
+    if (int rc = pack_bwd_args(w[l], variant, hidden, n_edge_feat, bblobs[l], &args[l])) return rc;
   for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
     const int cnt = n_layers - l0 < PACK_MAX ? n_layers - l0 : PACK_MAX;
     PackBatch pb{};
-    for (int k = 0; k < cnt; ++k)
-      if (int rc = pack_bwd_args(w[l0 + k], variant, hidden, n_edge_feat, bblobs[l0 + k], &pb.a[k])) return rc;
+    for (int k = 0; k < cnt; ++k) pb.a[k] = args[l0 + k];
     hipLaunchKernelGGL(pack_bwd_kernel, dim3(32, 31, cnt), dim3(256), 0, (hipStream_t)stream, pb);
     if (int rc = check_launch("pack_bwd_kernel")) return rc;
   }
@@ -2119,7 +2125,7 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s, const Deferr
   if (int rc = check_launch("tconvx_bwd_kernel")) return rc;
   TconvBwdArgs ta;
   ta.BN = BN; ta.T = T; ta.M = M; ta.ntiles = (BN + 15) / 16;
-  ta.h = r.hs; ta.gout = r.gh; ta.wp = w.twf; ta.wb = w.twb; ta.gh = r.g_hin; ta.wpart = w.tpart;
+  ta.h = r.hs; ta.gout = r.gh; ta.wb = w.twb; ta.gh = r.g_hin; ta.wpart = w.tpart;
   ta.mask = r.mask;
   int TG = num_cus();
   TG = TG < TB_MAX_BLOCKS ? TG : TB_MAX_BLOCKS;

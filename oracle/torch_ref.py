@@ -72,9 +72,12 @@ def egnn_layer(p, pre, x, h, row, col, ef, v, norm=False):
 
 
 def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hidden=64, time_emb_dim=32,
-                 norm=False, use_time_conv=True):
+                 norm=False, use_time_conv=True, lrelu_masks=None, lrelu_record=None):
     """EGNO.forward (egno.py:37-111), num_inputs == 1. Returns (x, v, h), T-major rows.
-    use_time_conv=False skips egno.py:99-107."""
+    use_time_conv=False skips egno.py:99-107. lrelu_masks: per layer a [T, BN, hidden] bool tensor of
+    given LeakyReLU branch decisions (y > 0) for TimeConv's activation (layer_no.py:123), in place of
+    the decisions of this evaluation: a gradient at another evaluation's kinks (tests only);
+    lrelu_record: a list that receives each layer's pre-activation y."""
     BN, E = h.shape[0], row.shape[0]
     temb = timestep_embedding(t_out, time_emb_dim)                     # [Bt, T, Ht]
     Bt = temb.shape[0]
@@ -89,7 +92,11 @@ def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hi
             xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm)
             continue
         h3 = hh.reshape(T, BN, hidden)
-        hh = (h3 + F.leaky_relu(_spectral(h3, p[f"time_conv_modules.{i}.t_conv.weights1"]))).reshape(T * BN, hidden)
+        y = _spectral(h3, p[f"time_conv_modules.{i}.t_conv.weights1"])
+        if lrelu_record is not None:
+            lrelu_record.append(y.detach())
+        y = F.leaky_relu(y) if lrelu_masks is None else torch.where(lrelu_masks[i], y, 0.01 * y)
+        hh = (h3 + y).reshape(T * BN, hidden)
         X = torch.stack([xx - lm, vv], -1).reshape(T, BN, 3, 2)
         X = X + _spectral(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
         xx = X[..., 0].reshape(T * BN, 3) + lm

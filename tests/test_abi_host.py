@@ -59,6 +59,34 @@ def test_status_codes_and_last_error():
         _lib.check(rc)
 
 
+@pytest.mark.parametrize("entry", ["nonode_pack_layers", "nonode_pack_layers_bwd"])
+def test_batched_pack_validates_every_layer_before_any_launch(entry):
+    """A null weight pointer in layer 9 (the second PACK_MAX chunk) fails the batched call before any
+    kernel launch: here, with no GPU, an earlier launch of layers 0-7 would fail as a launch error
+    instead (the pointers are fake and never dereferenced on the host)."""
+    import ctypes
+    L = pkg.lib()
+    nl = 10
+
+    def fake(i):
+        w = _lib.LayerWeights()
+        for name, _ in _lib.LayerWeights._fields_:
+            setattr(w, name, 0x1000 + 64 * i)
+        return w
+
+    ws = [fake(i) for i in range(nl)]
+    WP = ctypes.POINTER(_lib.LayerWeights)
+    blobs = (ctypes.c_void_p * nl)(*[0x100000 + 4096 * i for i in range(nl)])
+    fn = getattr(L, entry)
+    for field in ("edge_w1", "coord_b2", "node_w2"):
+        bad = fake(9)
+        setattr(bad, field, None)
+        arr = (WP * nl)(*[ctypes.pointer(w) for w in ws[:9]], ctypes.pointer(bad))
+        rc = fn(arr, nl, 0, 64, 2, blobs, None)
+        assert rc != 0
+        assert b"missing weight pointer" in L.nonode_last_error()
+
+
 def _egno_ctor(**kw):
     args = dict(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
                 num_timesteps=10, time_emb_dim=32)

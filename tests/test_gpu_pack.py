@@ -42,6 +42,7 @@ def test_batched_packs_equal_per_layer_packs():
     assert torch.equal(a, b)
     # the batched entry validates every layer: a null weight pointer in layer 2 fails the call
     ws[2].edge_w1 = None
-    with pytest.raises(_lib.NonodeError, match="missing weight pointer"):
-        _lib.check(L.nonode_pack_layers((WP * nl)(*[ctypes.pointer(w) for w in ws]), nl, m._pack_variant(),
-                                        m.hidden_nf, m.in_edge_nf, P(*[a[i].data_ptr() for i in range(nl)]), _lib.stream_of(a)))
+    for entry in (L.nonode_pack_layers, L.nonode_pack_layers_bwd):
+        with pytest.raises(_lib.NonodeError, match="missing weight pointer"):
+            _lib.check(entry((WP * nl)(*[ctypes.pointer(w) for w in ws]), nl, m._pack_variant(),
+                             m.hidden_nf, m.in_edge_nf, P(*[a[i].data_ptr() for i in range(nl)]), _lib.stream_of(a)))

@@ -213,9 +213,27 @@ def test_egno_five_mode_gradients_match_reference_golden():
             check_rel(f"m5 grad {k}", got, ref, GTOL)
 
 
+def _hip_lrelu_masks(state, L, T, BN):
+    """TimeConv's LeakyReLU decisions (y > 0) of a HIP training forward, per layer [T, BN, 64], decoded
+    from the head of its saved state (TconvArgs::mask_out: word ((t ntiles + tile) 4 + wave) 4 + q, bit
+    l = column 16 tile + 4 wave + (l >> 4), channel 4 (l & 15) + q)."""
+    ntiles = (BN + 15) // 16
+    nw = L * T * ntiles * 16
+    w = state[:2 * nw].detach().cpu().numpy().view(np.uint8).reshape(L, T, ntiles, 4, 4, 8)
+    bits = np.unpackbits(w, axis=-1, bitorder="little").reshape(L, T, ntiles, 4, 4, 4, 16)   # l = 16 a + b
+    m = bits.transpose(0, 1, 2, 3, 5, 6, 4).reshape(L, T, ntiles * 16, 64)[:, :, :BN]
+    return [torch.from_numpy(m[layer].astype(bool)) for layer in range(L)]
+
+
 def test_egno_five_mode_gradients_at_b512_match_f64_reference():
     """num_modes = 5, T = 8 at the C4 shard size B = 512 (N = 20): every parameter gradient against
-    float64 torch autograd of the op-by-op restatement (oracle/torch_ref.py)."""
+    float64 torch autograd of the op-by-op restatement (oracle/torch_ref.py), at a fixed 1e-5 bar.
+    TimeConv's LeakyReLU has a kink: a pre-activation within rounding of 0 takes one branch in float64
+    and the other in any fp32 evaluation (the fp32 torch path flips the same 2 of 21M elements here), and
+    each flip moves the last TimeConv's weight gradient by ~3e-5 (a sum of ~1e5 gated products per
+    element). The reference gradient is therefore float64 autograd evaluated at the HIP forward's own
+    branch decisions (read from its saved state); the flipped elements themselves are checked to lie at
+    the kink (|y| tiny against the layer's scale)."""
     from oracle import torch_ref as tr
     from tests.test_gpu_parity import _egno_full
     B, N, T, modes = 512, 20, 8, 5
@@ -223,27 +241,43 @@ def test_egno_five_mode_gradients_at_b512_match_f64_reference():
     x, nodes, edges, ea, v, lm, t, _ = _egno_full(B, N, T, seed=32)
     loc_true = torch.randn(B, N, T, 3, generator=torch.Generator().manual_seed(33))
     m.zero_grad(set_to_none=True)
+    m._train_state_sink = []
     xo, _, _ = m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)
+    masks = _hip_lrelu_masks(m._train_state_sink.pop(), m.n_layers, T, B * N)
+    del m._train_state_sink
     loss, _ = _loss_like_reference(xo, loc_true.to(x.device), T, B, N)
     loss.backward()
     torch.cuda.synchronize()
-    p = {k: q.detach().cpu().double().requires_grad_(True) for k, q in m.state_dict().items()}
     r, c = tr.full_edges(B, N)
     d = lambda a: a.detach().cpu().double()  # noqa: E731
-    xr, _, _ = tr.egno_forward(p, d(x), d(nodes), r, c, d(ea), d(v), d(lm), t.cpu(), T=T)
-    lr, _ = _loss_like_reference(xr, loc_true.double(), T, B, N)
-    lr.backward()
+    sd = m.state_dict()
+
+    def f64_grads(**kw):
+        p = {k: q.detach().cpu().double().requires_grad_(True) for k, q in sd.items()}
+        xr, _, _ = tr.egno_forward(p, d(x), d(nodes), r, c, d(ea), d(v), d(lm), t.cpu(), T=T, **kw)
+        lr, _ = _loss_like_reference(xr, loc_true.double(), T, B, N)
+        lr.backward()
+        return lr, p
+
+    ys = []
+    lr, p = f64_grads(lrelu_record=ys)
     assert abs(float(loss.detach()) - float(lr.detach())) <= 1e-6 * abs(float(lr.detach()))
-    # the same autograd in fp32: the conditioning of each gradient at this size (the last layer's
-    # TimeConv weights sum ~1e5 LeakyReLU-gated products per element); bar = max(1e-5, 2x its error)
-    p32 = {k: q.detach().cpu().float().requires_grad_(True) for k, q in m.state_dict().items()}
-    f = lambda a: a.detach().cpu().float()  # noqa: E731
-    x32, _, _ = tr.egno_forward(p32, f(x), f(nodes), r, c, f(ea), f(v), f(lm), t.cpu(), T=T)
-    _loss_like_reference(x32, loc_true.float(), T, B, N)[0].backward()
+    nflip = 0
+    for layer, (mk, y) in enumerate(zip(masks, ys)):
+        flip = mk != (y > 0)
+        nflip += int(flip.sum())
+        assert int(flip.sum()) <= 64, (layer, int(flip.sum()))
+        if flip.any():
+            assert float(y[flip].abs().max()) <= 1e-5 * float(y.abs().max()), layer   # at the kink
+    _, pk = f64_grads(lrelu_masks=masks)
     for k, q in m.named_parameters():
-        ref = p[k].grad
+        ref = pk[k].grad
         if ref is None or float(ref.abs().max()) == 0:
             assert q.grad is None or float(q.grad.abs().max()) == 0, k
         else:
-            own = maxnorm_rel(p32[k].grad.numpy(), ref.numpy())
-            check_rel(f"m5 B=512 grad {k}", q.grad, ref, max(GTOL_F64, 2.0 * own))
+            check_rel(f"m5 B=512 grad {k} (f64 at the HIP kinks)", q.grad, ref, GTOL_F64)
+    # at the float64 forward's own kinks: within the fixed bar everywhere but where a flip moved it
+    worst = max(maxnorm_rel(q.grad.detach().cpu().numpy(), p[k].grad.numpy()) for k, q in m.named_parameters()
+                if p[k].grad is not None and float(p[k].grad.abs().max()) > 0)
+    assert nflip > 0 or worst <= GTOL_F64
+
