@@ -259,11 +259,14 @@ constexpr int EW_WC2 = 2 * 64 * 65;       // dwc2 [1][65],  column 64 = dbc2
 constexpr int EW_FEAT = EW_WC2 + 68;      // dW1 scalar-input columns [64][NF + 1] (NF = 1 + ne <= 5)
 constexpr int EW_STRIDE = EW_FEAT + 64 * 6;
 constexpr int EB_MAX_BLOCKS = 256;        // edge_bwd grid cap: EB_MAX_BLOCKS * 4 wave partials
+constexpr int EB_N_MAX = 115;             // largest N whose pass A tables fit at one tile per chunk (2N senders)
 constexpr int ROWT = 68;                  // transpose-tile row stride (floats)
 constexpr int EB_TSTRIDE = 2 * 16 * ROWT; // per-wave transpose tile (two [16][ROWT] operands)
 
 struct EdgeBwdArgs {
   int n_graphs, N, ne, ef_mod, ct, s_max;
+  int gtab;    // pass B with the sender sums GB / GX added straight into HBM (float atomics) instead of
+               // wave-private LDS tables: the large-N form (the tables' 4 x s_max rows do not fit)
   int segno;   // SEGNO_GCL (gcl.py:97-100): every edge's translation r c is clamped to +-100 before the
                // mean, so its gradient passes only where |r_d c| <= 100 (EGNO clamps the mean instead)
   const float* h; const float* x; const float* ef; const float* bb;
@@ -287,14 +290,14 @@ struct EdgeBwdArgs {
 constexpr int EB_VSTAGE = BOFF_SCAL + 64 - BOFF_FEAT;   // feature k-steps + vectors + scalars
 // staged fp16 hi/lo fragments: pass A W2, Wc1, Wc1^T (+ EB_VSTAGE), pass B W2^T
 constexpr int EB_HSTAGE_A = 3 * 4096, EB_HSTAGE_B = 4096;
-size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out) {
+size_t edge_bwd_lds_floats(int pass, int ct, int N, int* s_max_out, int gtab = 0) {
   const int s_max = ((16 * ct - 1) / N + 2) * N;
   if (s_max_out) *s_max_out = s_max;
   // sP, sGM [ct*16][ROWP]; sQ [s_max][ROWP]; sX [s_max][4]; sGF [ct*16][4]; 4 x tile;
-  // PASS 1: 4 x (sGA [ct*16][ROWP], sGB [s_max][ROWP], sGX [s_max][4])
+  // PASS 1: 4 x (sGA [ct*16][ROWP], sGB [s_max][ROWP], sGX [s_max][4]); gtab: 4 x sGA only
   // + the fp16 hi/lo fragment sets staged once
   return (pass ? EB_HSTAGE_B : EB_HSTAGE_A + EB_VSTAGE) + (size_t)ct * 16 * ROWP * (pass ? 1 : 2) + (size_t)s_max * ROWP + (size_t)s_max * 4 + (size_t)ct * 16 * 4 +
-         4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (size_t)s_max * (ROWP + 4)) : 0);
+         4 * (size_t)EB_TSTRIDE + (pass ? 4 * ((size_t)ct * 16 * ROWP + (gtab ? 0 : (size_t)s_max * (ROWP + 4))) : 0);
 }
 
 // acc[ot][it] += sum over the unit's 16 edges of G[e] (x) A[e], accumulated in image-column order
@@ -523,9 +526,12 @@ __device__ __forceinline__ float edge_sum16(float v) {
 // z1 and does the rest of the reverse: dW2, db2, W2^T, the W1 scalar columns and GA / GB / GX.
 // OPT: 1 = EGNO norm=True (radial input normalised, basic.py:140-141), 2 = SEGNO tanh=True (coordinate
 // output through tanh, gcl.py:57-59); each its own copy of the body (no per-edge select by default)
-template <int NE, int PASS, int OPT>
+// GT: pass B's sender sums, 0 = LDS tables, 1 = HBM atomics (EdgeBwdArgs::gtab, large N), 2 = read gtab
+// (the option variants); each its own copy for OPT 0 / 3, so the default loop carries no gtab branch
+template <int NE, int PASS, int OPT, int GT>
 __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   constexpr bool rnorm = OPT == 1, ctanh = OPT == 2;
+  const bool gtab = PASS == 1 && (GT == 2 ? p.gtab != 0 : GT == 1);
   // OPT 0: EGNO, OPT 3: SEGNO (compile-time: no per-edge branch); the option variants read p.segno
   const bool segno = OPT == 0 ? false : (OPT == 3 ? true : p.segno != 0);
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -610,7 +616,8 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
     // ---- A: tables ----
     if (PASS == 1) {
       for (int i = tid; i < NW * rows * ROWP; i += NW * 64) sGA[i] = 0.f;
-      for (int i = tid; i < NW * p.s_max * (ROWP + 4); i += NW * 64) sGB[i] = 0.f;   // sGB and sGX
+      if (!gtab)
+        for (int i = tid; i < NW * p.s_max * (ROWP + 4); i += NW * 64) sGB[i] = 0.f;   // sGB and sGX
     }
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
@@ -685,8 +692,14 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       store_ecl(myGA + rl_ * ROWP, v, g);
       const int rr = rbase + rl_;
       if (g == 0 && rr < nend) {
-        f4* xr = reinterpret_cast<f4*>(myGX + (rr - s0) * 4);
-        *xr += f4{gxR0, gxR1, gxR2, 0.f};
+        if (gtab) {   // large N: no sender tables, the receiver side joins the HBM sums too
+          atomicAdd(p.GX + (size_t)rr * 4 + 0, gxR0);
+          atomicAdd(p.GX + (size_t)rr * 4 + 1, gxR1);
+          atomicAdd(p.GX + (size_t)rr * 4 + 2, gxR2);
+        } else {
+          f4* xr = reinterpret_cast<f4*>(myGX + (rr - s0) * 4);
+          *xr += f4{gxR0, gxR1, gxR2, 0.f};
+        }
       }
       zero4(gaR);
       gxR0 = gxR1 = gxR2 = 0.f;
@@ -927,7 +940,19 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       gxR0 += gr0;
       gxR1 += gr1;
       gxR2 += gr2;
-      if (rvalid) {
+      if (rvalid && gtab) {   // large N: straight into the (zeroed) HBM sums
+        float* gb = p.GB + (size_t)(s0 + sl) * HID + 4 * g;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) atomicAdd(gb + 16 * mt + q, gz1[mt][q]);
+        if (g == 0) {
+          float* gx = p.GX + (size_t)(s0 + sl) * 4;
+          atomicAdd(gx + 0, -gr0);
+          atomicAdd(gx + 1, -gr1);
+          atomicAdd(gx + 2, -gr2);
+        }
+      } else if (rvalid) {
         f4 t[4];
         load_ecl(t, myGB + sl * ROWP, g);
 #pragma unroll
@@ -1214,12 +1239,12 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       if (r < nend) p.GA[(size_t)r * HID + ch] = ((sGA[o] + sGA[rows * ROWP + o]) + sGA[2 * rows * ROWP + o]) +
                                                  sGA[3 * rows * ROWP + o];
     }
-    for (int i = tid; i < S * HID; i += NW * 64) {
+    for (int i = tid; i < (gtab ? 0 : S * HID); i += NW * 64) {
       const int sl = i / HID, ch = i - sl * HID;
       const int o = sl * ROWP + ch, st = p.s_max * ROWP;
       atomicAdd(p.GB + (size_t)(s0 + sl) * HID + ch, ((sGB[o] + sGB[st + o]) + sGB[2 * st + o]) + sGB[3 * st + o]);
     }
-    for (int i = tid; i < S * 3; i += NW * 64) {
+    for (int i = tid; i < (gtab ? 0 : S * 3); i += NW * 64) {
       const int sl = i / 3, d = i - 3 * sl;
       const int o = sl * 4 + d, st = p.s_max * 4;
       atomicAdd(p.GX + (size_t)(s0 + sl) * 4 + d, ((sGX[o] + sGX[st + o]) + sGX[2 * st + o]) + sGX[3 * st + o]);
@@ -1300,23 +1325,40 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
 
 template <int NE, int PASS>
 __global__ __launch_bounds__(256) void edge_bwd_kernel(EdgeBwdArgs p) {
-  if (p.bb[BOFF_SCAL + SC_NORM] != 0.f) edge_bwd_body<NE, PASS, 1>(p);        // wave-uniform
-  else if (p.bb[BOFF_SCAL + SC_TANH] != 0.f) edge_bwd_body<NE, PASS, 2>(p);
-  else if (p.segno) edge_bwd_body<NE, PASS, 3>(p);
-  else edge_bwd_body<NE, PASS, 0>(p);
+  if (p.bb[BOFF_SCAL + SC_NORM] != 0.f) edge_bwd_body<NE, PASS, 1, 2>(p);        // wave-uniform
+  else if (p.bb[BOFF_SCAL + SC_TANH] != 0.f) edge_bwd_body<NE, PASS, 2, 2>(p);
+  else if (p.segno) {
+    if constexpr (PASS == 1) {
+      if (p.gtab) { edge_bwd_body<NE, PASS, 3, 1>(p); return; }
+    }
+    edge_bwd_body<NE, PASS, 3, 0>(p);
+  } else {
+    if constexpr (PASS == 1) {
+      if (p.gtab) { edge_bwd_body<NE, PASS, 0, 1>(p); return; }
+    }
+    edge_bwd_body<NE, PASS, 0, 0>(p);
+  }
 }
 // per-pass chunk size (tiles per LDS chunk) and dynamic LDS bytes
-int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_max_out, size_t* lds_out) {
+// (gtab_out: pass B takes the large-N form, EdgeBwdArgs::gtab, when its sender tables do not fit)
+int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_max_out, size_t* lds_out,
+                    int* gtab_out = nullptr) {
   const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
   int ct = 8 < tiles_per ? 8 : tiles_per;
-  int s_max = 0;
+  while (ct > 1 && ct * (N - 1) > 512) --ct;   // pass A's per-wave pair mask: <= 64 pairs per wave and chunk
+  int s_max = 0, gtab = 0;
   while (ct > 1 && edge_bwd_lds_floats(pass, ct, N, &s_max) * 4 > 160 * 1024) --ct;
   size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max) * 4;
-  if (lds > 160 * 1024)
+  if (lds > 160 * 1024 && pass == 1) {
+    gtab = 1;
+    lds = edge_bwd_lds_floats(pass, ct, N, &s_max, 1) * 4;
+  }
+  if (lds > 160 * 1024 || ct * (N - 1) > 512)
     return fail(NONODE_EUNSUPPORTED, "edge backward: N=%d too large (pass %d LDS tables %zu bytes > 160 KB)", N, pass, lds);
   const size_t red = (size_t)4 * EW_STRIDE * 4;   // the end-of-kernel partial combine
   lds = lds > red ? lds : red;
   *ct_out = ct; *s_max_out = s_max; *lds_out = lds;
+  if (gtab_out) *gtab_out = gtab;
   return NONODE_OK;
 }
 
@@ -1333,7 +1375,7 @@ int edge_bwd_fits(const char* who, int n_graphs, int N) {
   for (int pass = 0; pass < 2; ++pass)
     if (edge_bwd_config(pass, n_graphs, N, edge_bwd_grid(n_graphs), &ct, &s_max, &lds))
       return fail(NONODE_EUNSUPPORTED, "%s: N=%d too large for the edge backward (pass %d LDS tables > 160 KB; "
-                  "training supports N <= 31)", who, N, pass);
+                  "training supports N <= %d)", who, N, pass, EB_N_MAX);
   return NONODE_OK;
 }
 
@@ -1351,7 +1393,7 @@ int launch_edge_bwd(int ne, EdgeBwdArgs a, int G, hipStream_t s) {
       hipLaunchKernelGGL(k0, dim3(G), dim3(256), lds, s, a);
     }
     if (int rc = check_launch("edge_bwd_kernel<pass 0>")) return rc;
-    if (int rc = edge_bwd_config(1, a.n_graphs, a.N, G, &a.ct, &a.s_max, &lds)) return rc;
+    if (int rc = edge_bwd_config(1, a.n_graphs, a.N, G, &a.ct, &a.s_max, &lds, &a.gtab)) return rc;
     {
       ProfScope prof(PROF_EDGE_BWD1, s);
       hipLaunchKernelGGL(k1, dim3(G), dim3(256), lds, s, a);
@@ -2049,7 +2091,7 @@ int egnn_layer_reverse(const LayerRev& r, const BwdWs& w, hipStream_t s, Deferre
   {
     const int G = edge_bwd_grid(r.n_graphs);
     EdgeBwdArgs ea;
-    ea.n_graphs = r.n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = r.ef_mod; ea.ct = 0; ea.s_max = 0;
+    ea.n_graphs = r.n_graphs; ea.N = N; ea.ne = ne; ea.ef_mod = r.ef_mod; ea.ct = 0; ea.s_max = 0; ea.gtab = 0;
     ea.segno = 0;
     ea.h = r.he; ea.x = r.xe; ea.ef = ne ? r.edge_fea : r.bb; ea.bb = r.bb; ea.gF = w.gF; ea.gM = w.gM;
     ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
@@ -2444,7 +2486,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       const int G = edge_bwd_grid(B);
       EdgeBwdArgs ea;
       ea.segno = 1;
-      ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0;
+      ea.n_graphs = B; ea.N = N; ea.ne = ne; ea.ef_mod = B; ea.ct = 0; ea.s_max = 0; ea.gtab = 0;
       ea.h = hs; ea.x = st.xs + t * n * 3; ea.ef = ne ? edge_attr : bblob; ea.bb = bblob; ea.gF = w.gF;
       ea.gM = w.gM; ea.GA = w.GA; ea.GB = w.GB; ea.GX = w.GX; ea.wpart = w.wpart;
       ea.stash = w.stash; ea.stash_c = w.stash_c; ea.Pn = w.Pn; ea.Qn = w.Qn;

@@ -113,10 +113,11 @@ def _layer_bwd(m, i, n_graphs, N, h, x, v, ef, gxo, gvo, gho):
     return grads, ghi, gxi, gvi
 
 
-@pytest.mark.parametrize("N", [26, 31])
+@pytest.mark.parametrize("N", [26, 31, 64, 100, 115])
 def test_egnn_layer_bwd_large_n_matches_float64_oracle(N):
-    """The layer entry point at the top of the training range (N <= 31, set by the edge backward's
-    LDS tables), against the float64 reverse pass of oracle/egno_grad.py (basic.py:167-186)."""
+    """The layer entry point up to the top of the training range (N <= 115, set by pass A's LDS tables;
+    N > 31 takes pass B's large-N form), against the float64 reverse pass of oracle/egno_grad.py
+    (basic.py:167-186)."""
     B, i = 3, 2
     c = _egno_case(B, N, 10, seed=N)
     m = _egno(T=10, seed=N)
@@ -145,11 +146,11 @@ def test_layer_bwd_rejects_n_beyond_the_tables_before_any_launch():
     lg = _lib.LayerGrads()
     t = torch.zeros(16, device=DEV)
     P = _lib.ptr
-    N = 40
+    N = 116
     ws = L.nonode_egnn_layer_bwd_workspace_bytes(2, N)
     rc = L.nonode_egnn_layer_bwd(_lib.VARIANT_EGNO, 2, N, 2, 2, *([P(t)] * 9), ctypes.byref(lg), P(t), P(t), P(t),
                                  P(t), ws, _lib.stream_of(t))
-    assert rc != 0 and b"egnn_layer_bwd: N=40 too large" in L.nonode_last_error()
+    assert rc != 0 and b"egnn_layer_bwd: N=116 too large" in L.nonode_last_error()
 
 
 def test_layer_bwd_rejects_segno_and_small_workspace():

@@ -77,8 +77,11 @@ def test_egno_train_forward_equals_inference_forward():
         check_rel("a.detach()", a.detach().cpu(), b.cpu(), 1e-6)
 
 
-# (2, 31, 4): the largest N whose per-chunk sender tables fit pass B's LDS
-@pytest.mark.parametrize("B,N,T", [(2, 5, 10), (3, 9, 4), (1, 20, 10), (1, 26, 4), (2, 31, 4)])
+# (2, 31, 4): the largest N whose per-chunk sender tables fit pass B's LDS; N >= 32: pass B's large-N form
+# (sender sums straight into HBM; up to N = 115, the largest N pass A's tables fit: tests/test_gpu_layer_bwd.py)
+# 
+@pytest.mark.parametrize("B,N,T", [(2, 5, 10), (3, 9, 4), (1, 20, 10), (1, 26, 4), (2, 31, 4), (2, 32, 2), (1, 64, 4),
+                                   (1, 100, 4)])
 def test_egno_gradients_match_oracle(B, N, T):
     c = _egno_case(B, N, T, seed=B * 100 + N)
     m = _egno(T=T, seed=N)
@@ -99,9 +102,9 @@ def test_egno_gradients_match_oracle(B, N, T):
 
 
 def test_egno_training_rejects_n_beyond_the_edge_backward_tables():
-    """N = 40 needs more LDS for the edge backward's sender tables than a CU has: the backward
-    raises the library's error instead of running a kernel that does not fit."""
-    B, N, T = 1, 40, 2
+    """N = 116 needs more LDS for pass A's per-chunk sender tables than a CU has: the backward raises
+    the library's error instead of running a kernel that does not fit."""
+    B, N, T = 1, 116, 2
     c = _egno_case(B, N, T, seed=3)
     m = _egno(T=T, seed=3)
     inp = {k: _dev(v) for k, v in c.items()}

@@ -109,7 +109,8 @@ def test_segno_gradients_match_reference_golden():
 
 
 @pytest.mark.parametrize("B,N,T,recurrent,cw", [(3, 7, 4, True, 1.0), (2, 20, 10, True, 1.0), (4, 5, 10, False, 1.0),
-                                                (2, 20, 3, True, 0.5), (5, 2, 6, True, 1.0), (1, 31, 3, True, 1.0)])
+                                                (2, 20, 3, True, 0.5), (5, 2, 6, True, 1.0), (1, 31, 3, True, 1.0),
+                                                (1, 64, 3, True, 1.0), (1, 100, 2, True, 1.0)])
 def test_segno_gradients_match_f64_reference(B, N, T, recurrent, cw):
     m = _segno(seed=B * 10 + N, recurrent=recurrent, cw=cw)
     case = _case(B, N, seed=N + T)
