@@ -604,41 +604,83 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   const int ntw = (nend - nb + 15) >> 4;
   const int nch = (ntw + p.ct - 1) / p.ct;
   STAMP_DECL   // diagnostic section stamps (NONODE_STAMP builds): PASS 1 slots 0-12, PASS 0 13-15
-  for (int ci = 0; ci < nch; ++ci) {
+  // chunk ci: ctc tiles from row rbase; its senders are the S rows of the graphs it touches, from s0
+  struct Chunk { int ctc, rbase, s0, S; };
+  auto chunk_at = [&](int ci) __attribute__((always_inline)) {
+    Chunk c;
     const int c0 = (ci * ntw) / nch;
-    const int ctc = ((ci + 1) * ntw) / nch - c0;
-    const int rbase = nb + c0 * 16;
-    const int r_last = min(rbase + ctc * 16, nend) - 1;
-    const int g_lo = rbase / N, g_hi = r_last / N;
-    const int s0 = g_lo * N;
-    const int S = (g_hi - g_lo + 1) * N;
+    c.ctc = ((ci + 1) * ntw) / nch - c0;
+    c.rbase = nb + c0 * 16;
+    const int r_last = min(c.rbase + c.ctc * 16, nend) - 1;
+    const int g_lo = c.rbase / N, g_hi = r_last / N;
+    c.s0 = g_lo * N;
+    c.S = (g_hi - g_lo + 1) * N;
+    return c;
+  };
+  // The chunk's global rows (positions, gF and, in pass B, pass A's projections P / Q) are all
+  // requested into registers before any is stored, and pass B's wave-private sum tables are zeroed while
+  // they are in flight: one memory latency per chunk instead of one per loop trip (this phase was 17% of
+  // pass B). (Requesting the next chunk's rows before this chunk's phase C instead measured no faster at
+  // C4 and slower for SEGNO's small per-substep launches.)
+  constexpr int KS = PASS == 1 ? 4 : 1;   // f4 rows staged per thread (ct = 1, N = 20: 896 of 1024)
+  f4 st4[KS];
+  float stx = 0.f, stf = 0.f;
+  auto pq_at = [&](const Chunk& c, int i) __attribute__((always_inline)) {   // P of the receiver rows (zero past
+    const int nP4 = c.ctc * 16 * 16;                                          // the range), Q of the senders
+    if (i < nP4) {
+      const int rr = c.rbase + (i >> 4);
+      return rr < nend ? reinterpret_cast<const f4*>(p.Pn + (size_t)rr * HID)[i & 15] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int i2 = i - nP4;
+    return reinterpret_cast<const f4*>(p.Qn + (size_t)(c.s0 + (i2 >> 4)) * HID)[i2 & 15];
+  };
+  auto x_at = [&](const Chunk& c, int i) __attribute__((always_inline)) {
+    const int s_ = i / 3;
+    return p.x[(size_t)(c.s0 + s_) * 3 + (i - 3 * s_)];
+  };
+  auto gf_at = [&](const Chunk& c, int i) __attribute__((always_inline)) {
+    const int rr = c.rbase + i / 4;
+    return rr < nend ? p.gF[(size_t)rr * 4 + (i & 3)] : 0.f;
+  };
+  auto stage = [&](const Chunk& c) __attribute__((always_inline)) {
+    const int nT = PASS == 1 ? (c.ctc * 16 + c.S) * 16 : 0;
+    stx = tid < c.S * 3 ? x_at(c, tid) : 0.f;
+    stf = tid < c.ctc * 64 ? gf_at(c, tid) : 0.f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int i = tid + k * NW * 64;
+      if (i < nT) st4[k] = pq_at(c, i);
+    }
+  };
+  for (int ci = 0; ci < nch; ++ci) {
+    const Chunk cc = chunk_at(ci);
+    const int ctc = cc.ctc, rbase = cc.rbase, s0 = cc.s0, S = cc.S;
     const int nsT = (S + 15) >> 4;
     // ---- A: tables ----
-    if (PASS == 1) {
-      for (int i = tid; i < NW * rows * ROWP; i += NW * 64) sGA[i] = 0.f;
-      if (!gtab)
-        for (int i = tid; i < NW * p.s_max * (ROWP + 4); i += NW * 64) sGB[i] = 0.f;   // sGB and sGX
-    }
-    for (int i = tid; i < S * 3; i += NW * 64) {
-      const int s = i / 3, d = i - 3 * s;
-      sX[s * 4 + d] = p.x[(size_t)(s0 + s) * 3 + d];
-    }
-    for (int i = tid; i < ctc * 16 * 4; i += NW * 64) {
-      const int rr = rbase + i / 4;
-      sGF[i] = rr < nend ? p.gF[(size_t)rr * 4 + (i & 3)] : 0.f;
-    }
-    if (PASS == 1) {
-      // pass A's node projections: P of the receiver rows (zero past the range), Q of the senders
-      for (int i = tid; i < ctc * 16 * 16; i += NW * 64) {
-        const int rl = i >> 4, c4 = i & 15;
-        const int rr = rbase + rl;
-        const f4 v = rr < nend ? reinterpret_cast<const f4*>(p.Pn + (size_t)rr * HID)[c4] : f4{0.f, 0.f, 0.f, 0.f};
-        *reinterpret_cast<f4*>(sP + rl * ROWP + 4 * c4) = v;
+    stage(cc);
+    {
+      const int nX = S * 3, nF = ctc * 16 * 4;
+      const int nP4 = PASS == 1 ? ctc * 16 * 16 : 0, nT = nP4 + (PASS == 1 ? S * 16 : 0);
+      auto pq_put = [&](int i, f4 v) {
+        if (i < nP4) *reinterpret_cast<f4*>(sP + (i >> 4) * ROWP + 4 * (i & 15)) = v;
+        else *reinterpret_cast<f4*>(sQ + ((i - nP4) >> 4) * ROWP + 4 * ((i - nP4) & 15)) = v;
+      };
+      if (PASS == 1) {
+        const f4 z = {0.f, 0.f, 0.f, 0.f};
+        for (int i = tid; i < NW * rows * ROWP / 4; i += NW * 64) reinterpret_cast<f4*>(sGA)[i] = z;
+        if (!gtab)
+          for (int i = tid; i < NW * p.s_max * (ROWP + 4) / 4; i += NW * 64) reinterpret_cast<f4*>(sGB)[i] = z;   // sGB, sGX
       }
-      for (int i = tid; i < S * 16; i += NW * 64) {
-        const int sl = i >> 4, c4 = i & 15;
-        *reinterpret_cast<f4*>(sQ + sl * ROWP + 4 * c4) = reinterpret_cast<const f4*>(p.Qn + (size_t)(s0 + sl) * HID)[c4];
+      if (tid < nX) sX[(tid / 3) * 4 + tid % 3] = stx;
+      if (tid < nF) sGF[tid] = stf;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int i = tid + k * NW * 64;
+        if (i < nT) pq_put(i, st4[k]);
       }
+      for (int i = tid + NW * 64; i < nX; i += NW * 64) sX[(i / 3) * 4 + i % 3] = x_at(cc, i);   // larger chunks
+      for (int i = tid + NW * 64; i < nF; i += NW * 64) sGF[i] = gf_at(cc, i);
+      for (int i = tid + KS * NW * 64; i < nT; i += NW * 64) pq_put(i, pq_at(cc, i));
     }
     for (int job = wave; job < (PASS == 0 ? ctc + nsT : 0); job += NW) {
       const bool isP = job < ctc;
@@ -704,26 +746,47 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
       zero4(gaR);
       gxR0 = gxR1 = gxR2 = 0.f;
     };
+    // a lane's receiver geometry in tile tau (one integer division per tile, not per unit): row rl in
+    // the chunk, in range, graph-local index n, the graph's first row in the sender table, edge rows
+    struct LT { int tau, rl, n, sb; bool rv; size_t efb; };
+    auto lane_tile = [&](int tau) __attribute__((always_inline)) {
+      LT t;
+      t.tau = tau;
+      t.rl = 16 * tau + e;
+      const int r = rbase + t.rl;
+      t.rv = r < nend;
+      const int rc = t.rv ? r : nend - 1;
+      const int gr = rc / N;
+      t.n = rc - gr * N;
+      t.sb = gr * N - s0;
+      t.efb = ((size_t)(gr % p.ef_mod) * N + t.n) * Nm1;
+      return t;
+    };
+    // unit u = tau (N - 1) + k - 1 of the chunk, stepped without a division
+    auto unit_tk = [&](int u, int& tau, int& k) __attribute__((always_inline)) {
+      tau = u / Nm1;
+      k = u - tau * Nm1 + 1;
+    };
+    auto step_tk = [&](int& tau, int& k, int by) __attribute__((always_inline)) {
+      k += by;
+      while (k > Nm1) { k -= Nm1; ++tau; }
+    };
     // the wave's next unit's edge features and (pass B) handoff block are requested one unit ahead,
     // so their global-memory latency overlaps this unit's work
-    auto unit_src = [&](int uu, const float*& efp_o, size_t& sunit_o) {
-      const int tau_ = uu / Nm1, k_ = uu - tau_ * Nm1 + 1;
-      const int r_ = rbase + 16 * tau_ + e;
-      const int rc_ = r_ < nend ? r_ : nend - 1;
-      const int gr_ = rc_ / N, n_ = rc_ - gr_ * N;
-      int j_ = n_ + k_;
+    auto unit_src = [&](const LT& t, int k_, const float*& efp_o, size_t& sunit_o) __attribute__((always_inline)) {
+      int j_ = t.n + k_;
       j_ = (j_ >= N) ? j_ - N : j_;
-      const int jj_ = (j_ < n_) ? j_ : j_ - 1;
-      efp_o = p.ef + (((size_t)(gr_ % p.ef_mod) * N + n_) * Nm1 + jj_) * NE;
-      sunit_o = (size_t)(k_ - 1) * ((size_t)p.n_graphs * N + 16 * gridDim.x) + rbase + 16 * tau_ + 16 * blockIdx.x;
+      const int jj_ = (j_ < t.n) ? j_ : j_ - 1;
+      efp_o = p.ef + (t.efb + jj_) * NE;
+      sunit_o = (size_t)(k_ - 1) * ((size_t)p.n_graphs * N + 16 * gridDim.x) + rbase + 16 * t.tau + 16 * blockIdx.x;
     };
     float efn[NE > 0 ? NE : 1];
     f4 gzn[4];
     float cn = 0.f;
-    auto prefetch = [&](int uu) {
+    auto prefetch = [&](const LT& t, int k_) __attribute__((always_inline)) {
       const float* ep;
       size_t su;
-      unit_src(uu, ep, su);
+      unit_src(t, k_, ep, su);
 #pragma unroll
       for (int kk = 0; kk < NE; ++kk) efn[kk] = ep[kk];
       if constexpr (PASS == 1) {
@@ -736,17 +799,11 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
     constexpr int NEP = NE > 0 ? NE : 1;
     // one unit (16 edges) through the whole reverse pass of this PASS (the single-unit form: every
     // unit of pass B, pass A's odd last unit and its pairs whose activations leave the fp16 range)
-    auto unit_one = [&](int u, const float (&fe_in)[NEP], const f4 (&gz_in)[4], float c_in) __attribute__((always_inline)) {
-      const int tau = u / Nm1, k = u - tau * Nm1 + 1;
-      const int rl = 16 * tau + e;
-      const int r = rbase + rl;
-      const bool rvalid = r < nend;
-      const int rc = rvalid ? r : nend - 1;
-      const int gr = rc / N, n = rc - gr * N;
+    auto unit_one = [&](const LT& lt, int k, const float (&fe_in)[NEP], const f4 (&gz_in)[4], float c_in) __attribute__((always_inline)) {
+      const int tau = lt.tau, rl = lt.rl, n = lt.n, sb = lt.sb;
+      const bool rvalid = lt.rv;
       int j = n + k;
       j = (j >= N) ? j - N : j;
-      const int jj = (j < n) ? j : j - 1;
-      const int sb = gr * N - s0;
       const int sl = sb + j, rls = sb + n;
       const float r0 = sX[rls * 4 + 0] - sX[sl * 4 + 0];
       const float r1 = sX[rls * 4 + 1] - sX[sl * 4 + 1];
@@ -977,7 +1034,9 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
     auto load_ef = [&](int uu, float (&dst)[NEP]) __attribute__((always_inline)) {
       const float* ep;
       size_t su;
-      unit_src(uu, ep, su);
+      int tau_, k_;
+      unit_tk(uu, tau_, k_);
+      unit_src(lane_tile(tau_), k_, ep, su);
 #pragma unroll
       for (int kk = 0; kk < NE; ++kk) dst[kk] = ep[kk];
     };
@@ -1190,7 +1249,10 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           for (int b = 0; b < (t >> 1); ++b) mm &= mm - 1;
           uu = 2 * (wave + NW * __builtin_ctzll(mm)) + (t & 1);
         }
-        prefetch(uu);
+        int tau_u, k_u;
+        unit_tk(uu, tau_u, k_u);
+        const LT lt_u = lane_tile(tau_u);
+        prefetch(lt_u, k_u);
         float fe_in[NEP];
 #pragma unroll
         for (int kk = 0; kk < NEP; ++kk) fe_in[kk] = efn[kk];
@@ -1203,10 +1265,16 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
         } else {
           zero4(gz_in);
         }
-        unit_one(uu, fe_in, gz_in, c_in);
+        unit_one(lt_u, k_u, fe_in, gz_in, c_in);
       }
     } else {
-      if (u_first < U) prefetch(u_first);
+      // the current and the next unit as (tile geometry, sender offset), stepped by NW units
+      int tau_n, k_n;
+      unit_tk(u_first < U ? u_first : 0, tau_n, k_n);
+      LT lt_n = lane_tile(tau_n);
+      int k_c = k_n;
+      LT lt_c = lt_n;
+      if (u_first < U) prefetch(lt_n, k_n);
       for (int u = u_first; u < U; u += NW) {
         // the weight fragments are loop-invariant: without this barrier the compiler hoists all four
         // 64x64 matrices (256 VGPRs) out of the loop and spills
@@ -1221,8 +1289,14 @@ __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
           for (int mt = 0; mt < 4; ++mt) gz_in[mt] = gzn[mt];
           c_in = cn;
         }
-        prefetch(u + NW < U ? u + NW : u);
-        unit_one(u, fe_in, gz_in, c_in);
+        if (u + NW < U) {
+          step_tk(tau_n, k_n, NW);
+          if (tau_n != lt_n.tau) lt_n = lane_tile(tau_n);
+        }
+        prefetch(lt_n, k_n);
+        unit_one(lt_c, k_c, fe_in, gz_in, c_in);
+        lt_c = lt_n;
+        k_c = k_n;
       }
     }
     if (PASS == 1 && cur_tau >= 0) flush_ga(cur_tau);
@@ -1346,9 +1420,10 @@ int edge_bwd_config(int pass, int n_graphs, int N, int G, int* ct_out, int* s_ma
   const int tiles_per = (((n_graphs + G - 1) / G) * N + 15) / 16;
   int ct = 8 < tiles_per ? 8 : tiles_per;
   while (ct > 1 && ct * (N - 1) > 512) --ct;   // pass A's per-wave pair mask: <= 64 pairs per wave and chunk
-  int s_max = 0, gtab = 0;
-  while (ct > 1 && edge_bwd_lds_floats(pass, ct, N, &s_max) * 4 > 160 * 1024) --ct;
-  size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max) * 4;
+  static const int force_gtab = getenv_int("NONODE_GTAB");   // (A/B switch: the large-N form at any N)
+  int s_max = 0, gtab = pass == 1 && force_gtab;
+  while (ct > 1 && edge_bwd_lds_floats(pass, ct, N, &s_max, gtab) * 4 > 160 * 1024) --ct;
+  size_t lds = edge_bwd_lds_floats(pass, ct, N, &s_max, gtab) * 4;
   if (lds > 160 * 1024 && pass == 1) {
     gtab = 1;
     lds = edge_bwd_lds_floats(pass, ct, N, &s_max, 1) * 4;
