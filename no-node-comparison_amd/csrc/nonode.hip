@@ -209,209 +209,6 @@ __device__ unsigned long long g_stamp[16];
 #define STAMP_FLUSH
 #endif
 
-// ---- TimeConv + TimeConv_x fused into the EGNO layer launch (inference) -------------------------
-// The layer kernel's workgroups own whole samples (all T frames of their graphs, "sample-major"
-// chunks), so each can run the layer's TimeConv (layer_no.py:80-178, egno.py:99-108) over its own
-// columns (b, n) first and then the EGNN layer over the same samples: one launch per layer instead of
-// two, and the TimeConv input (the previous layer's output, written by the same workgroup index, so
-// the same XCD) is read from that XCD's L2. The tile work is tconv_kernel's (below), for a workgroup's
-// column range [c0, cend) instead of the whole [0, BN).
-struct TcFuse {
-  const float* h; const float* x; const float* v; const float* lm;   // inputs (h: null on the first layer)
-  const float* wp; const float* wx;                                  // packed mixing fragments, raw TimeConv_x
-  float* h_out; float* x_out; float* v_out;                          // outputs (v in place)
-  const float* hin; int din; const float* emb_w; int emb_ld; const float* etab; int Bt;   // first layer
-  int first, frames, T, M, Mfull, BN;
-};
-constexpr int TCF_MM = 2, TCF_TB = 10;   // the fused form's mode / frame bounds (C2: 2 modes, T = 10)
-// one 16-column tile [c0, c0 + 16) of the TimeConv, columns >= cend left alone; 4 waves
-template <int MM, int TB>
-__device__ __forceinline__ void tconv_tile_fused(const TcFuse& f, int c0, int cend, float (*sX)[16][ROWP],
-                                                 const float* sCos, const float* sSin, int lane, int wave, int e,
-                                                 int g) {
-  const int T = f.T, M = f.M, BN = f.BN;
-  const int col = c0 + e;
-  const bool cvalid = col < cend;
-  const int c = cvalid ? col : cend - 1;
-  const int ecol = 4 * wave + (lane >> 4), chs = 4 * (lane & 15);
-  const int scol = c0 + ecol;
-  const bool svalid = scol < cend;
-  const int sc = svalid ? scol : cend - 1;
-  f4 base = {0.f, 0.f, 0.f, 0.f};
-  const float* et = nullptr;
-  auto hin_part = [&](size_t r) {
-    f4 b = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < f.din; ++k) {
-      const float hv = f.hin[r * f.din + k];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = fmaf(f.emb_w[(chs + q) * f.emb_ld + k], hv, b[q]);
-    }
-    return b;
-  };
-  if (f.first) {
-    if (!f.frames) base = hin_part((size_t)sc);
-    et = f.etab + ((size_t)(sc % f.Bt) * T) * 64 + chs;
-  }
-  auto hval = [&](int t) -> f4 {
-    if (f.first) return *reinterpret_cast<const f4*>(et + t * 64) + (f.frames ? hin_part((size_t)t * BN + sc) : base);
-    return *reinterpret_cast<const f4*>(f.h + ((size_t)t * BN + sc) * 64 + chs);
-  };
-  // x / v channels (TimeConv_x): wave 3, lane (d = g, column e), d < 3
-  if (wave == 3 && g < 3 && cvalid) {
-    const int d = g;
-    auto lm_at = [&](int t) { return f.lm[((f.frames ? (size_t)t * BN : 0) + c) * 3 + d]; };
-    float xs[TB], vs[TB], lms[TB];
-#pragma unroll
-    for (int t = 0; t < TB; ++t) {
-      const int tc = t < T ? t : T - 1;
-      const size_t row = (f.first && !f.frames) ? (size_t)c : ((size_t)tc * BN + c);
-      lms[t] = lm_at(tc);
-      xs[t] = f.x[row * 3 + d] - lms[t];
-      vs[t] = f.v[row * 3 + d];
-    }
-    float yr[MM][2], yi[MM][2];
-#pragma unroll
-    for (int m = 0; m < MM; ++m) {
-      if (m < M) {
-        float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < TB; ++t) {
-          if (t < T) {
-            const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
-            Xr[0] = fmaf(xs[t], cs, Xr[0]); Xi[0] = fmaf(-xs[t], sn, Xi[0]);
-            Xr[1] = fmaf(vs[t], cs, Xr[1]); Xi[1] = fmaf(-vs[t], sn, Xi[1]);
-          }
-        }
-        const float cm = (m == 0 || 2 * m == T) ? 1.f : 2.f;
-#pragma unroll
-        for (int o = 0; o < 2; ++o) {
-          float ar = 0.f, ai = 0.f;
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const float wr = f.wx[(((size_t)i * 2 + o) * f.Mfull + m) * 2 + 0];
-            const float wi = f.wx[(((size_t)i * 2 + o) * f.Mfull + m) * 2 + 1];
-            ar += Xr[i] * wr - Xi[i] * wi;
-            ai += Xr[i] * wi + Xi[i] * wr;
-          }
-          yr[m][o] = ar * cm; yi[m][o] = ai * cm;
-        }
-      }
-    }
-    const float invT = 1.0f / (float)T;
-#pragma unroll
-    for (int t = 0; t < TB; ++t) {
-      if (t < T) {
-        float y0 = 0.f, y1 = 0.f;
-#pragma unroll
-        for (int m = 0; m < MM; ++m) {
-          if (m < M) {
-            const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
-            y0 += yr[m][0] * cs - yi[m][0] * sn;
-            y1 += yr[m][1] * cs - yi[m][1] * sn;
-          }
-        }
-        const size_t row = (size_t)t * BN + c;
-        f.x_out[row * 3 + d] = xs[t] + y0 * invT + lms[t];
-        f.v_out[row * 3 + d] = vs[t] + y1 * invT;
-      }
-    }
-  }
-  // step 1: truncated DFT of this wave's input channels (every frame's h kept for the residual)
-  f4 hvs[TB];
-#pragma unroll
-  for (int t = 0; t < TB; ++t) hvs[t] = hval(t < T ? t : T - 1);
-  {
-    f4 Xr[MM], Xs[MM];
-#pragma unroll
-    for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
-#pragma unroll
-    for (int t = 0; t < TB; ++t) {
-      if (t < T) {
-        const f4 hv = hvs[t];
-#pragma unroll
-        for (int m = 0; m < MM; ++m) {
-          if (m < M) {
-            Xr[m] += hv * sCos[m * TMAX + t];
-            if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
-          }
-        }
-      }
-    }
-    *reinterpret_cast<f4*>(&sX[0][ecol][chs]) = Xr[0];
-#pragma unroll
-    for (int m = 1; m < MM; ++m) {
-      if (m < M) {
-        *reinterpret_cast<f4*>(&sX[2 * m - 1][ecol][chs]) = Xr[m];
-        *reinterpret_cast<f4*>(&sX[2 * m][ecol][chs]) = Xs[m];
-      }
-    }
-  }
-  __syncthreads();
-  // step 2: channel mixing on MFMA (output tile mo = wave)
-  f4 Yr[MM], Yi[MM];
-  auto mix = [&](f4& acc, int mat, int vec) {
-    f4 in[4];
-    load_ecl(in, &sX[vec][e][0], g);
-    const float* wf = f.wp + (size_t)mat * 4096;
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const f4 a = *reinterpret_cast<const f4*>(wf + ((wave * 4 + mt) * 64 + lane) * 4);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
-    }
-  };
-  Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
-  mix(Yr[0], 0, 0);
-#pragma unroll
-  for (int m = 1; m < MM; ++m) {
-    if (m < M) {
-      const int mat = 1 + 3 * (m - 1);
-      Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
-      Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
-      mix(Yr[m], mat + 0, 2 * m - 1);
-      mix(Yr[m], mat + 1, 2 * m);
-      mix(Yi[m], mat + 1, 2 * m - 1);
-      mix(Yi[m], mat + 2, 2 * m);
-    }
-  }
-  __syncthreads();
-  {
-    const int chm = 16 * wave + 4 * g;
-    *reinterpret_cast<f4*>(&sX[0][e][chm]) = Yr[0];
-#pragma unroll
-    for (int m = 1; m < MM; ++m) {
-      if (m < M) {
-        *reinterpret_cast<f4*>(&sX[2 * m - 1][e][chm]) = Yr[m];
-        *reinterpret_cast<f4*>(&sX[2 * m][e][chm]) = Yi[m];
-      }
-    }
-  }
-  __syncthreads();
-  // step 3: y[t], LeakyReLU(0.01), residual
-  Yr[0] = *reinterpret_cast<const f4*>(&sX[0][ecol][chs]);
-#pragma unroll
-  for (int m = 1; m < MM; ++m) {
-    if (m < M) {
-      Yr[m] = *reinterpret_cast<const f4*>(&sX[2 * m - 1][ecol][chs]);
-      Yi[m] = *reinterpret_cast<const f4*>(&sX[2 * m][ecol][chs]);
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < TB; ++t) {
-    if (t < T) {
-      f4 y = Yr[0];
-#pragma unroll
-      for (int m = 1; m < MM; ++m)
-        if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
-      f4 o = hvs[t];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
-      if (svalid) *reinterpret_cast<f4*>(f.h_out + ((size_t)t * BN + sc) * 64 + chs) = o;
-    }
-  }
-  __syncthreads();   // sX is reused by the next tile
-}
-
 // ---- fused E(n)-equivariant layer ------------------------------------------------------------
 enum { EGNO = 0, SEGNO = 1 };
 
@@ -430,6 +227,11 @@ struct LayerArgs {
   // training forward only (else null): per-receiver message sums (true scale) [n][64] and force
   // sums [n][4] (f summed over the N-1 senders, before the mean and clamp)
   float* m_out; float* f_out;
+  // saved-state substeps (SEGNO training forward, sv_h != null): step s > 0 reads its inputs from
+  // sv_* + s sv_n rows and every step writes its outputs to sv_* + (s + 1) sv_n rows (the last one to
+  // *_out as well) and its message sums to m_out + s sv_n rows: all T substeps in one launch
+  float* sv_h; float* sv_x; float* sv_v;
+  long long sv_n;
   int n_total, n_graphs, N, ne, ef_mod, recurrent;
   // chunking: a unit is cg whole graphs (cpg = 1) or, for large N, one graph cut into cpg chunks of
   // ct receiver tiles; workgroups own whole units (n_units, the last may be short)
@@ -439,13 +241,6 @@ struct LayerArgs {
   // k % 8 (its XCD) owns the same 1/8 of the columns as the TimeConv tiles on that XCD
   int use_perm;
   unsigned short chunk_of[256];
-  // sample-major chunks (EGNO forward, smaj = T frames per sample, else 0): workgroup k owns samples
-  // [k B / G, (k + 1) B / G) with all their frames, its chunks are cg consecutive graphs of the
-  // (sample, frame) order, and rows keep the time-major HBM layout (row = (t B + b) N + n): the body
-  // works on chunk-local rows and maps them to HBM rows (grow). tcf: that layer's TimeConv, run by
-  // each workgroup over its own samples before the layer (tcfuse = 1)
-  int smaj, tcfuse;
-  TcFuse tcf;
 };
 
 // LDS of one chunk: ct receiver tiles (P, two message-sum slots, two force-sum slots) and s_rows senders
@@ -477,8 +272,10 @@ size_t layer_lds_floats(int ct, int s_rows, int keep = 0) {
 // OPT: the variant's constructor option (EGNO norm=True: radial input normalised; SEGNO tanh=True:
 // coordinate output through tanh), compiled into its own copy of the body so the default path's
 // hot loop carries no per-edge select; the kernel picks the copy once from the blob's flag.
-template <int VARIANT, int KF, int NW, bool OPT>
-__device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
+// SAVE: the saved-state substeps (LayerArgs::sv_h, SEGNO training), its own copy so the inference
+// instances carry none of it (one runtime branch cost C3 +4.5%)
+template <int VARIANT, int KF, int NW, bool OPT, bool SAVE = false>
+__device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)[NW + 1]) {
   constexpr bool PAIR = NW == 4;
   constexpr bool rnorm = OPT && VARIANT == EGNO;    // basic.py:140-141
   constexpr bool ctanh = OPT && VARIANT == SEGNO;   // gcl.py:57-59
@@ -511,44 +308,8 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
 
   const int G = gridDim.x;
   const int cb = p.use_perm ? (int)p.chunk_of[blockIdx.x] : (int)blockIdx.x;
-  const bool smaj = VARIANT == EGNO && p.smaj > 0;   // sample-major chunks (LayerArgs::smaj)
-  const int Ts = smaj ? p.smaj : 1, Bs = smaj ? p.n_graphs / Ts : 1;
-  const int sb0 = (int)(((long long)cb * Bs) / G), sb1 = (int)(((long long)(cb + 1) * Bs) / G);
-  const int npos = (sb1 - sb0) * Ts;                 // smaj: this workgroup's graphs, (sample, frame) order
-  const int ch0 = smaj ? 0 : (int)(((long long)cb * p.n_units) / G) * p.cpg;        // this workgroup's chunks
-  const int ch1 = smaj ? (npos + p.cg - 1) / p.cg : (int)(((long long)(cb + 1) * p.n_units) / G) * p.cpg;
-  // HBM row of row r of chunk position pos0 (smaj: r chunk-local; else r is already the HBM row)
-  auto grow = [&](int pos0, int r) __attribute__((always_inline)) -> size_t {
-    if (!smaj) return (size_t)r;
-    const int gl = r / N, n = r - gl * N;
-    const int P = pos0 + gl, b = P / Ts, t = P - b * Ts;
-    return ((size_t)t * Bs + b) * N + n;
-  };
-  // the HBM graph index (time-major t B + b) of chunk-local graph gl: its edge features' row
-  auto ggraph = [&](int pos0, int gl) __attribute__((always_inline)) {
-    const int P = pos0 + gl, b = P / Ts, t = P - b * Ts;
-    return t * Bs + b;
-  };
-  auto pos_of = [&](int ci) __attribute__((always_inline)) { return smaj ? sb0 * Ts + ci * p.cg : 0; };
-  if constexpr (VARIANT == EGNO && NW == 4) {
-    if (smaj && p.tcfuse) {   // this layer's TimeConv over the workgroup's columns [sb0 N, sb1 N) first
-      const TcFuse& f = p.tcf;
-      float(*tsX)[16][ROWP] = reinterpret_cast<float(*)[16][ROWP]>(sP);   // the chunk tables' space
-      float* tCos = sP + (2 * TCF_MM - 1) * 16 * ROWP;
-      float* tSin = tCos + TCF_MM * TMAX;
-      if (tid < f.M * f.T) {
-        const int m = tid / f.T, t = tid - (tid / f.T) * f.T;
-        const double ang = 2.0 * (double)m * (double)t / (double)f.T;
-        tCos[m * TMAX + t] = (float)cospi(ang);
-        tSin[m * TMAX + t] = (float)sinpi(ang);
-      }
-      __syncthreads();
-      const int c1 = sb1 * N;
-      for (int tc0 = sb0 * N; tc0 < c1; tc0 += 16)
-        tconv_tile_fused<TCF_MM, TCF_TB>(f, tc0, c1, tsX, tCos, tSin, lane, wave, e, g);
-      // (each tile ends with a barrier: its outputs are visible to the whole workgroup and the LDS is free)
-    }
-  }
+  const int ch0 = (int)(((long long)cb * p.n_units) / G) * p.cpg;        // this workgroup's chunks
+  const int ch1 = (int)(((long long)(cb + 1) * p.n_units) / G) * p.cpg;
   __syncthreads();
   // message / force sums start at zero; every node-update job zeroes the rows it consumed, so the
   // next chunk's edge phase finds them zero
@@ -556,11 +317,6 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   for (int i = tid; i < 2 * p.ct * 16 * 4; i += NW * 64) sF[i] = 0.f;
   // rows of chunk ci: receivers [rbase, nend), senders [s0, s0 + S)
   auto chunk_at = [&](int ci, int& rbase, int& nend, int& s0, int& S) __attribute__((always_inline)) {
-    if (smaj) {         // chunk-local rows of min(cg, npos - ci cg) graphs
-      const int cgc = min(p.cg, npos - ci * p.cg);
-      rbase = 0; nend = cgc * N; s0 = 0; S = nend;
-      return;
-    }
     if (p.cpg == 1) {   // cg whole graphs: the chunk's rows are its receivers and senders alike
       const int g_lo = ci * p.cg, g_hi = min(g_lo + p.cg, p.n_graphs);
       rbase = g_lo * N; nend = g_hi * N; s0 = rbase; S = nend - rbase;
@@ -608,7 +364,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     }
   };
   auto proj_job = [&](const float* __restrict__ hI, const float* blob, int rbase, int nend, int s0, int S,
-                      int job, int pos0) __attribute__((always_inline)) {
+                      int job) __attribute__((always_inline)) {
     int joff = 0;
     asm volatile("" : "+s"(joff));   // weight reads stay in the job (LICM would pin them in VGPRs)
     blob += joff;
@@ -616,7 +372,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       const int local = job * 16 + e;
       const bool valid = rbase + local < nend;
       f4 hin[4];
-      load_ecl(hin, hI + grow(pos0, valid ? rbase + local : nend - 1) * HID, g);
+      load_ecl(hin, hI + (size_t)(valid ? rbase + local : nend - 1) * HID, g);
       if (keep && valid) store_ecl(sH + local * ROWP, hin, g);
       proj_tile(hin, blob, local, valid);
       return;
@@ -647,33 +403,34 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
     if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
     if (valid && !isP && g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;   // sender flag
   };
-  auto load_sx = [&](const float* __restrict__ xI, const float* __restrict__ vI, int s0, int S, int pos0) __attribute__((always_inline)) {
+  auto load_sx = [&](const float* __restrict__ xI, const float* __restrict__ vI, int s0, int S) __attribute__((always_inline)) {
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
-      sX[s * 4 + d] = xI[grow(pos0, s0 + s) * 3 + d];
-      if (keep) sVl[s * 4 + d] = vI[grow(pos0, s0 + s) * 3 + d];
+      sX[s * 4 + d] = xI[(size_t)(s0 + s) * 3 + d];
+      if (keep) sVl[s * 4 + d] = vI[(size_t)(s0 + s) * 3 + d];
     }
   };
   STAMP_DECL
-  // edge-unit ranges of the waves for the last chunk shape (each wave its own copy)
-  __shared__ int s_cut[NW][NW + 1];
-  int* cut = s_cut[wave];
+  int* cut = s_cut[wave];   // (static LDS of the kernel: one array for every body copy)
   int cut_ctc = -1, cut_vl = -1;
   #pragma unroll 1
   for (int step = 0; step < p.steps; ++step) {
-  const float* __restrict__ hI = step == 0 ? p.h : p.pp_h[(step - 1) & 1];
-  const float* __restrict__ xI = step == 0 ? p.x : p.pp_x[(step - 1) & 1];
-  const float* __restrict__ vI = step == 0 ? p.v : p.pp_v[(step - 1) & 1];
-  float* hO = step == p.steps - 1 ? p.h_out : p.pp_h[step & 1];
-  float* xO = step == p.steps - 1 ? p.x_out : p.pp_x[step & 1];
-  float* vO = step == p.steps - 1 ? p.v_out : p.pp_v[step & 1];
+  constexpr bool save = VARIANT == SEGNO && SAVE;   // (LayerArgs::sv_h)
+  const bool last = step == p.steps - 1;
+  const float* __restrict__ hI = step == 0 ? p.h : (save ? p.sv_h + step * p.sv_n * HID : p.pp_h[(step - 1) & 1]);
+  const float* __restrict__ xI = step == 0 ? p.x : (save ? p.sv_x + step * p.sv_n * 3 : p.pp_x[(step - 1) & 1]);
+  const float* __restrict__ vI = step == 0 ? p.v : (save ? p.sv_v + step * p.sv_n * 3 : p.pp_v[(step - 1) & 1]);
+  float* hO = save ? p.sv_h + (step + 1) * p.sv_n * HID : (last ? p.h_out : p.pp_h[step & 1]);
+  float* xO = save ? p.sv_x + (step + 1) * p.sv_n * 3 : (last ? p.x_out : p.pp_x[step & 1]);
+  float* vO = save ? p.sv_v + (step + 1) * p.sv_n * 3 : (last ? p.v_out : p.pp_v[step & 1]);
+  float* mO = p.m_out ? p.m_out + (save ? step * p.sv_n * HID : 0) : nullptr;
   if (!fused || step == 0) {   // ---------------- phase A of the step's first chunk ----------------
     int rbase, nend, s0, S;
     chunk_at(ch0, rbase, nend, s0, S);
-    load_sx(xI, vI, s0, S, pos_of(ch0));
+    load_sx(xI, vI, s0, S);
     const int J = proj_jobs(rbase, nend, S);
     #pragma unroll 1
-    for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job, pos_of(ch0));
+    for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job);
     STAMP(6);
     __syncthreads();
     STAMP(7);
@@ -750,7 +507,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         const int gr = rc / N;
         const int n = rc - gr * N;
         const int sb = gr * N - s0;
-        const size_t ebase = ((size_t)((smaj ? ggraph(pos_of(ci), gr) : gr) % p.ef_mod) * N + n) * Nm1;
+        const size_t ebase = ((size_t)(gr % p.ef_mod) * N + n) * Nm1;
         int voff = 0;
         asm volatile("" : "+v"(voff));   // keeps the vector reads per segment (not hoisted), LDS space kept
         const float* vFEAT = vFEAT_ + voff;
@@ -1178,7 +935,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
       int nrb = 0, nne = 0, ns0 = 0, nS = 0;
       if (has_next) {
         chunk_at(ci + 1, nrb, nne, ns0, nS);
-        load_sx(xI, vI, ns0, nS, pos_of(ci + 1));
+        load_sx(xI, vI, ns0, nS);
       }
       const int J = ctc + (has_next ? proj_jobs(nrb, nne, nS) : 0);
       constexpr int C_COST = 4;
@@ -1200,7 +957,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         asm volatile("" : "+s"(joff));   // weight reads stay in the job (LICM would pin them in VGPRs)
         const float* bj = blob + joff;
         if (j >= ctc) {
-          proj_job(hI, bj, nrb, nne, ns0, nS, j - ctc, pos_of(ci + 1));
+          proj_job(hI, bj, nrb, nne, ns0, nS, j - ctc);
           continue;
         }
         const int tau = j;
@@ -1212,7 +969,7 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         f4 in8[8];
         f4 hr[4], Mr[4], Mb[4];
         if (keep) load_ecl(hr, sH + lc * ROWP, g);
-        else load_ecl(hr, hI + grow(pos_of(ci), rc) * HID, g);
+        else load_ecl(hr, hI + (size_t)rc * HID, g);
         load_ecl(Mr, sM + rl * ROWP, g);
         load_ecl(Mb, sM + slotM + rl * ROWP, g);
   #pragma unroll
@@ -1231,9 +988,9 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
         }
         float x0, x1, x2, v0, v1, v2;
         if (fused) { x0 = sX[lc * 4 + 0]; x1 = sX[lc * 4 + 1]; x2 = sX[lc * 4 + 2]; }
-        else { const size_t gr3 = grow(pos_of(ci), rc) * 3; x0 = xI[gr3 + 0]; x1 = xI[gr3 + 1]; x2 = xI[gr3 + 2]; }
+        else { const size_t gr3 = (size_t)rc * 3; x0 = xI[gr3 + 0]; x1 = xI[gr3 + 1]; x2 = xI[gr3 + 2]; }
         if (keep) { v0 = sVl[lc * 4 + 0]; v1 = sVl[lc * 4 + 1]; v2 = sVl[lc * 4 + 2]; }
-        else { const size_t gr3 = grow(pos_of(ci), rc) * 3; v0 = vI[gr3 + 0]; v1 = vI[gr3 + 1]; v2 = vI[gr3 + 2]; }
+        else { const size_t gr3 = (size_t)rc * 3; v0 = vI[gr3 + 0]; v1 = vI[gr3 + 1]; v2 = vI[gr3 + 2]; }
         float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
         if (VARIANT == EGNO) {
           // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
@@ -1278,23 +1035,30 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
   #pragma unroll
           for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
         }
-        if (rvalid && p.m_out) {
+        if (rvalid && mO) {
           f4 mt4[4];
   #pragma unroll
           for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[mt] * NEG_LN2;    // sM holds -log2e * sum m
-          store_ecl(p.m_out + grow(pos_of(ci), r) * HID, mt4, g);
-          if (g == 0 && p.f_out) *reinterpret_cast<f4*>(p.f_out + grow(pos_of(ci), r) * 4) = f4{F0, F1, F2, 0.f};
+          store_ecl(mO + (size_t)r * HID, mt4, g);
+          if (g == 0 && p.f_out) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
         }
         const bool next = fused && step + 1 < p.steps;   // fused: this tile's rows of step + 1 in LDS
-        if (rvalid && !(keep && next)) {
-          const size_t ro = grow(pos_of(ci), r);
+        if (rvalid && (save || !(keep && next))) {
+          const size_t ro = (size_t)r;
           store_ecl(hO + ro * HID, hn, g);
+          if (save && last) store_ecl(p.h_out + ro * HID, hn, g);
           if (g == 0) {
             float* xo = xO + ro * 3;
             xo[0] = nx0; xo[1] = nx1; xo[2] = nx2;
             if (VARIANT == SEGNO) {
               float* vo = vO + ro * 3;
               vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
+              if (save && last) {
+                float* xo2 = p.x_out + ro * 3;
+                float* vo2 = p.v_out + ro * 3;
+                xo2[0] = nx0; xo2[1] = nx1; xo2[2] = nx2;
+                vo2[0] = nv0; vo2[1] = nv1; vo2[2] = nv2;
+              }
             }
           }
         }
@@ -1320,10 +1084,20 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p) {
 
 template <int VARIANT, int KF, int NW>
 __global__ __launch_bounds__(NW * 64) void egnn_layer_kernel(LayerArgs p) {
+  // edge-unit ranges of the waves for the last chunk shape (each wave its own copy); declared here
+  // once: the body copies below would each add their own static LDS to the 159 KB dynamic tables
+  __shared__ int s_cut[NW][NW + 1];
+  if constexpr (VARIANT == SEGNO) {
+    if (p.sv_h) {   // wave-uniform
+      if (p.blob[OFF_SCAL + SC_TANH] != 0.f) egnn_layer_body<VARIANT, KF, NW, true, true>(p, s_cut);
+      else egnn_layer_body<VARIANT, KF, NW, false, true>(p, s_cut);
+      return;
+    }
+  }
   if (p.blob[OFF_SCAL + (VARIANT == SEGNO ? SC_TANH : SC_NORM)] != 0.f)   // wave-uniform
-    egnn_layer_body<VARIANT, KF, NW, true>(p);
+    egnn_layer_body<VARIANT, KF, NW, true>(p, s_cut);
   else
-    egnn_layer_body<VARIANT, KF, NW, false>(p);
+    egnn_layer_body<VARIANT, KF, NW, false>(p, s_cut);
 }
 
 // ---- temporal spectral layers -----------------------------------------------------------------
@@ -1709,7 +1483,7 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
                  const float* v, const float* ef, const float* blob, float dt, float cw, int recurrent,
                  float* h_out, float* x_out, float* v_out, hipStream_t stream, int steps = 1,
                  float* const* pp = nullptr, float* m_out = nullptr, float* f_out = nullptr,
-                 int xcd_cols = 0, int smaj = 0, const TcFuse* tcf = nullptr) {
+                 int xcd_cols = 0, float* const* sv = nullptr) {
   const int n_total = n_graphs * N;
   const int cus = num_cus();
   // graphs per chunk: at most the graphs per CU, at most 8 tiles, within LDS; among those the one
@@ -1735,32 +1509,23 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   }
   const int s_rows = cg * N;
   const int n_units = (n_graphs + cg - 1) / cg;
-  int G = n_units < cus ? n_units : cus;
-  if (smaj) {   // workgroups own whole samples (all smaj frames): at most one per sample
-    const int Bs = n_graphs / smaj;
-    if (VARIANT != EGNO || cpg != 1 || Bs * smaj != n_graphs || steps != 1)
-      return fail(NONODE_EINVAL, "layer: sample-major chunks need whole-graph EGNO chunks");
-    G = Bs < cus ? Bs : cus;
-  }
+  const int G = n_units < cus ? n_units : cus;
   // substep fusion needs one whole-graph chunk per workgroup; keeping h, v in LDS needs the room
   const int fuse = steps > 1 && cpg == 1 && n_units <= cus;
   const int keep = fuse && layer_lds_floats(ct, s_rows, 1) * 4 <= LDS_MAX && !getenv_int("NONODE_NO_KEEP");
-  size_t lds = layer_lds_floats(ct, s_rows, keep) * 4;
-  if (tcf) {   // the fused TimeConv's tile (sX, twiddles) in the chunk tables' space
-    const size_t need = (8192 + EDGE_STAGE_FLOATS + (size_t)(2 * TCF_MM - 1) * 16 * ROWP +
-                         2 * TCF_MM * TMAX) * 4;
-    lds = lds > need ? lds : need;
-  }
+  const size_t lds = layer_lds_floats(ct, s_rows, keep) * 4;
   LayerArgs a;
   a.h = h; a.x = x; a.v = v; a.ef = ef; a.blob = blob;
   a.h_out = h_out; a.x_out = x_out; a.v_out = v_out;
   a.n_total = n_total; a.n_graphs = n_graphs; a.N = N; a.ne = ne; a.ef_mod = ef_mod;
   a.cg = cg; a.cpg = cpg; a.n_units = n_units; a.ct = ct; a.s_rows = s_rows;
-  if (steps < 1 || (steps > 1 && !pp)) return fail(NONODE_EINVAL, "layer: steps=%d", steps);
+  if (steps < 1 || (steps > 1 && !pp && !sv)) return fail(NONODE_EINVAL, "layer: steps=%d", steps);
   a.steps = steps;
   a.fuse = fuse && !getenv_int("NONODE_NO_FUSE");
   a.keep = a.fuse && keep;
   a.m_out = m_out; a.f_out = f_out;
+  a.sv_h = sv ? sv[0] : nullptr; a.sv_x = sv ? sv[1] : nullptr; a.sv_v = sv ? sv[2] : nullptr;
+  a.sv_n = n_total;
   for (int i = 0; i < 2; ++i) {
     a.pp_h[i] = pp ? pp[i] : nullptr;
     a.pp_x[i] = pp ? pp[2 + i] : nullptr;
@@ -1768,11 +1533,6 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   }
   a.recurrent = recurrent; a.inv_deg = 1.0f / (float)(N - 1); a.dt = dt; a.cw = cw;
   a.use_perm = 0;
-  a.smaj = smaj;
-  a.tcfuse = tcf != nullptr;
-  if (tcf) a.tcf = *tcf;
-  else memset(&a.tcf, 0, sizeof(a.tcf));
-  if (smaj) xcd_cols = 0;   // workgroup k owns the same samples in every layer (same XCD, its L2)
   if (xcd_cols > 0 && G % 8 == 0 && G <= 256 && xcd_on()) {
     // chunk c starts at column (first receiver row mod xcd_cols); its XCD block is that column's
     // eighth. Fill each XCD's G/8 slots (k = x, x + 8, ...) from its block, overflow anywhere.
@@ -2014,29 +1774,6 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
       if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hb[i], xb[i], v_out, edge_fea,
                                       blobs[l], 0.f, 1.f, 0, hb[o], xb[o], nullptr, s, 1, nullptr, nullptr, nullptr,
                                       BN))
-        return rc;
-    }
-    return NONODE_OK;
-  }
-  // fused TimeConv (TcFuse): sample-major layer launches that run their TimeConv first (2 modes,
-  // T <= 10, N < 64: the C2 configuration), opt-in NONODE_TCFUSE=1: measured slower than the separate
-  // launches (C2 1.002 vs 0.939 ms)
-  const int Me = effective_modes(T, modes);
-  if (Me <= TCF_MM && T <= TCF_TB && N < 64 && getenv_int("NONODE_TCFUSE")) {
-    for (int l = 0; l < n_layers; ++l) {
-      TcFuse f{};
-      f.BN = BN; f.T = T; f.M = Me; f.Mfull = modes; f.frames = frames;
-      f.wp = tconv_blobs[l]; f.wx = tconvx_w[l];
-      f.h_out = hB; f.x_out = xB; f.v_out = v_out; f.lm = loc_mean;
-      f.first = l == 0;
-      if (l == 0) {
-        f.h = nullptr; f.x = x; f.v = v;
-        f.hin = h; f.din = in_node; f.emb_w = emb_w; f.emb_ld = emb_ld; f.etab = etab; f.Bt = Bt;
-      } else {
-        f.h = h_out; f.x = x_out; f.v = v_out;
-      }
-      if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hB, xB, v_out, edge_fea, blobs[l], 0.f,
-                                      1.f, 0, h_out, x_out, nullptr, s, 1, nullptr, nullptr, nullptr, 0, T, &f))
         return rc;
     }
     return NONODE_OK;

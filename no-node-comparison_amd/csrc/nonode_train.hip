@@ -2390,6 +2390,7 @@ struct SegnoNodeBwdArgs {
   const float* bb;
   float* gv; float* gF; float* gM; float* ghp;           // outputs
   float* op_z; float* op_gz;                             // GEMM operands (node MLP weight gradients)
+  float* GB; float* GX;                                  // the edge backward's sender sums: zeroed here
 };
 
 // reverse of  v' = v + cw mean_j clamp(r_ij c_ij) dt ;  x' = x + v' dt   (gcl.py:255-257, 242)
@@ -2434,7 +2435,10 @@ __global__ __launch_bounds__(256) void segno_node_bwd_kernel(SegnoNodeBwdArgs p)
     store_ecl(p.gM + o, gM, g);
     store_ecl(p.op_z + o, z, g);
     store_ecl(p.op_gz + o, gz, g);
+    const f4 z4[4] = {};
+    store_ecl(p.GB + o, z4, g);
     if (g == 0) {
+      *reinterpret_cast<f4*>(p.GX + (size_t)r * 4) = z4[0];
       const float f = p.dt * p.cw / (float)(p.N - 1);
       float gvt[3];
 #pragma unroll
@@ -2488,16 +2492,18 @@ int nonode_segno_forward_train(int B, int N, int T, int n_edge_feat, const float
   hipMemcpyAsync(st.hs, h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
   hipMemcpyAsync(st.xs, x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   hipMemcpyAsync(st.vs, v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  for (int t = 0; t < T; ++t) {
-    if (int rc = launch_layer<SEGNO>(B, N, n_edge_feat, B, st.hs + t * n * 64, st.xs + t * n * 3, st.vs + t * n * 3,
-                                     edge_attr, blob, 1.0f / (float)T, coords_weight, recurrent,
-                                     st.hs + (t + 1) * n * 64, st.xs + (t + 1) * n * 3, st.vs + (t + 1) * n * 3, s, 1,
-                                     nullptr, st.Ms + t * n * 64, nullptr))
-      return rc;
+  if (T == 0) {
+    hipMemcpyAsync(h_out, h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+    hipMemcpyAsync(x_out, x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+    hipMemcpyAsync(v_out, v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+    return check_launch("segno_forward_train");
   }
-  hipMemcpyAsync(h_out, st.hs + T * n * 64, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  hipMemcpyAsync(x_out, st.xs + T * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  hipMemcpyAsync(v_out, st.vs + T * n * 3, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  // all T substeps in one launch of the inference layer kernel (fused substeps where a workgroup owns
+  // one whole-graph chunk), saving every substep's outputs and message sums (LayerArgs::sv_h)
+  float* const sv[3] = {st.hs, st.xs, st.vs};
+  if (int rc = launch_layer<SEGNO>(B, N, n_edge_feat, B, h, x, v, edge_attr, blob, 1.0f / (float)T, coords_weight,
+                                   recurrent, h_out, x_out, v_out, s, T, nullptr, st.Ms, nullptr, 0, sv))
+    return rc;
   return check_launch("segno_forward_train");
 }
 
@@ -2551,10 +2557,9 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
     na.n = (int)n; na.N = N; na.recurrent = recurrent; na.dt = 1.0f / (float)T; na.cw = coords_weight;
     na.h = hs; na.M = Ms; na.gxo = gx; na.gvo = gv; na.gho = gh; na.bb = bblob;
     na.gv = w.gv[nxt]; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp; na.op_z = w.op_z; na.op_gz = w.op_gz;
+    na.GB = w.GB; na.GX = w.GX;
     hipLaunchKernelGGL(segno_node_bwd_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, na);
     if (int rc = check_launch("segno_node_bwd_kernel")) return rc;
-    hipMemsetAsync(w.GB, 0, n * 64 * sizeof(float), s);
-    hipMemsetAsync(w.GX, 0, n * 4 * sizeof(float), s);
     ReduceJob rj[REDUCE_BATCH_MAX];   // the substep's edge- and node-level reductions: one launch
     int nrj = 0;
     {

@@ -385,24 +385,6 @@ def test_egno_c2_whole_batch_matches_f64_reference():
     check_rel("C2 h (512 samples)", ho, hr, TOL)
 
 
-@pytest.mark.parametrize("B", [4, 512])
-def test_egno_fused_timeconv_launch_matches_separate_launches(monkeypatch, B):
-    """NONODE_TCFUSE=1 (opt-in: measured slower): sample-major layer launches that run
-    their TimeConv first give the separate launches' results (same per-receiver sum order: the unit
-    split depends only on the chunk's graph count and N), at B=4 and at the C2 size."""
-    N, T = 20, 10
-    m = _egno(T=T, seed=4)
-    x, nodes, edges, ea, v, lm, t, _ = _egno_full(B, N, T, seed=8)
-    with torch.no_grad():
-        monkeypatch.delenv("NONODE_TCFUSE", raising=False)
-        ref = [a.clone() for a in m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)]
-        monkeypatch.setenv("NONODE_TCFUSE", "1")
-        fused = [a.clone() for a in m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)]
-    for name, a, b in zip(("x", "v", "h"), fused, ref):
-        assert torch.isfinite(a).all()
-        check_rel(f"fused TimeConv {name} (B={B})", a.cpu(), b.cpu(), 1e-6)
-
-
 def test_segno_c3_whole_batch_matches_f64_reference():
     """The whole C3 batch (B=512, N=20, 10 substeps) against the f64 torch restatement (scatter mean:
     the same values as gcl.py:16-23's dense mean, tests/test_torch_ref.py)."""
