@@ -2391,6 +2391,8 @@ struct SegnoNodeBwdArgs {
   float* gv; float* gF; float* gM; float* ghp;           // outputs
   float* op_z; float* op_gz;                             // GEMM operands (node MLP weight gradients)
   float* GB; float* GX;                                  // the edge backward's sender sums: zeroed here
+  int nmain;                                             // workgroups of the node reverse; further ones:
+  ReduceBatchArgs rb; int rb_count, rb_gx;               // the previous substep's deferred reductions
 };
 
 // reverse of  v' = v + cw mean_j clamp(r_ij c_ij) dt ;  x' = x + v' dt   (gcl.py:255-257, 242)
@@ -2398,6 +2400,13 @@ struct SegnoNodeBwdArgs {
 // gF is the gradient of the per-receiver sum of the clamped edge translations (the per-edge clamp
 // mask is applied by edge_bwd_kernel, which recomputes r c)
 __global__ __launch_bounds__(256) void segno_node_bwd_kernel(SegnoNodeBwdArgs p) {
+  if ((int)blockIdx.x >= p.nmain) {   // a deferred gemm_reduce_batch job (rb_gx workgroups per job)
+    const int b = (int)blockIdx.x - p.nmain, jj = b / p.rb_gx;
+    const ReduceJob& r = p.rb.j[jj];
+    gemm_reduce_body(r.partial, r.nblk, r.M, r.N, r.dst, r.ld, r.col0, r.cs, r.bias, r.accumulate, r.scale, r.split,
+                     r.col1, r.pstride, b - jj * p.rb_gx);
+    return;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, e = lane & 15, g = lane >> 4;
   const int r0 = (blockIdx.x * 4 + wave) * 16;
   if (r0 >= p.n) return;
@@ -2531,13 +2540,11 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
   const size_t n = (size_t)B * N;
   const SegnoState st = segno_state(const_cast<void*>(state), B, N, T);
   BwdWs w = bwd_ws(workspace, B, N, 1, 1);
-  float *gx = w.gx[0], *gv = w.gv[0], *gh = w.gh[0];
-  if (g_x) hipMemcpyAsync(gx, g_x, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  else hipMemsetAsync(gx, 0, n * 3 * sizeof(float), s);
-  if (g_v) hipMemcpyAsync(gv, g_v, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  else hipMemsetAsync(gv, 0, n * 3 * sizeof(float), s);
-  if (g_h) hipMemcpyAsync(gh, g_h, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  else hipMemsetAsync(gh, 0, n * 64 * sizeof(float), s);
+  // the output gradients are read in place (every kernel only reads them); null ones are zeros
+  const float *gx = g_x, *gv = g_v, *gh = g_h;
+  if (!g_x) { hipMemsetAsync(w.gx[0], 0, n * 3 * sizeof(float), s); gx = w.gx[0]; }
+  if (!g_v) { hipMemsetAsync(w.gv[0], 0, n * 3 * sizeof(float), s); gv = w.gv[0]; }
+  if (!g_h) { hipMemsetAsync(w.gh[0], 0, n * 64 * sizeof(float), s); gh = w.gh[0]; }
   if (T == 0) {   // no substep: every weight gradient is zero, the input gradients pass through
     hipMemsetAsync(lg.edge_w1, 0, (size_t)64 * ld1 * sizeof(float), s);
     for (float* q : {lg.edge_w2, lg.coord_w1, lg.node_w2}) hipMemsetAsync(q, 0, 64 * 64 * sizeof(float), s);
@@ -2548,6 +2555,11 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
   }
   const int ntile = (int)((n + 15) / 16);
   int cur = 0;
+  // each substep's weight-gradient reductions run in extra workgroups of the next (earlier) substep's
+  // segno_node_bwd_kernel launch (they touch none of its buffers; the partials they read are only
+  // overwritten by the edge backward after it), the last substep's in their own launch
+  ReduceJob prev[REDUCE_BATCH_MAX];
+  int nprev = 0;
   for (int t = T - 1; t >= 0; --t) {
     const int acc = t < T - 1;   // substeps share the weights: add into the gradients after the first
     const float* hs = st.hs + t * n * 64;
@@ -2556,9 +2568,20 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
     SegnoNodeBwdArgs na;
     na.n = (int)n; na.N = N; na.recurrent = recurrent; na.dt = 1.0f / (float)T; na.cw = coords_weight;
     na.h = hs; na.M = Ms; na.gxo = gx; na.gvo = gv; na.gho = gh; na.bb = bblob;
-    na.gv = w.gv[nxt]; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp; na.op_z = w.op_z; na.op_gz = w.op_gz;
+    // the first substep's input gradients go straight to the caller's outputs (when they alias no input)
+    auto out_to = [&](float* dst, const float* in0, const float* in1, float* ws) {
+      return (t == 0 && dst && dst != in0 && dst != in1) ? dst : ws;
+    };
+    float* gv_o = out_to(g_v_in, g_v, g_x, w.gv[nxt]);
+    float* gh_o = out_to(g_h_in, g_h, nullptr, w.gh[nxt]);
+    float* gx_o = out_to(g_x_in, g_x, g_v, w.gx[nxt]);
+    na.gv = gv_o; na.gF = w.gF; na.gM = w.gM; na.ghp = w.ghp; na.op_z = w.op_z; na.op_gz = w.op_gz;
     na.GB = w.GB; na.GX = w.GX;
-    hipLaunchKernelGGL(segno_node_bwd_kernel, dim3((ntile + 3) / 4), dim3(256), 0, s, na);
+    na.nmain = (ntile + 3) / 4;
+    na.rb_count = nprev; na.rb_gx = 1;
+    if (nprev)
+      if (int rc = reduce_batch_args(prev, nprev, &na.rb, &na.rb_gx)) return rc;
+    hipLaunchKernelGGL(segno_node_bwd_kernel, dim3(na.nmain + nprev * na.rb_gx), dim3(256), 0, s, na);
     if (int rc = check_launch("segno_node_bwd_kernel")) return rc;
     ReduceJob rj[REDUCE_BATCH_MAX];   // the substep's edge- and node-level reductions: one launch
     int nrj = 0;
@@ -2581,7 +2604,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
       // edge Linear 1 scalar columns [s | e] (SEGNO order [h_i, h_j, s, e], gcl.py:78)
       red(EW_FEAT, 64, 1 + ne, lg.edge_w1, ld1, nullptr, 2 * HID);
     }
-    const nonode_tu::NodePostArgs pa{(int)n, w.ghp, w.GA, w.GB, gx, w.GX, bblob, w.gh[nxt], w.gx[nxt]};
+    const nonode_tu::NodePostArgs pa{(int)n, w.ghp, w.GA, w.GB, gx, w.GX, bblob, gh_o, gx_o};
     // node-level weight gradients of this substep (edge Linear 1 h_i / h_j blocks, node MLP): one
     // node_wgrad_kernel launch (jobs 0, 1, 3, 4, 5; no node_v MLP) and one reduction launch
     {
@@ -2600,14 +2623,16 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
         rj[nrj++] = ReduceJob{w.partial + (size_t)d[j].job * nonode_tu::NW_PART, nblk, 64, 64, d[j].dst, d[j].ld,
                               d[j].col0, 1, d[j].bias, acc, 1.f, 1 << 30, 0,
                               (long long)nonode_tu::NW_JOBS * nonode_tu::NW_PART};
-      if (int rc = launch_reduce_batch(rj, nrj, s)) return rc;
+      for (int k = 0; k < nrj; ++k) prev[k] = rj[k];
+      nprev = nrj;
     }
     cur = nxt;
-    gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
+    gx = gx_o; gv = gv_o; gh = gh_o;
   }
-  if (g_h_in) hipMemcpyAsync(g_h_in, gh, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  if (g_x_in) hipMemcpyAsync(g_x_in, gx, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
-  if (g_v_in) hipMemcpyAsync(g_v_in, gv, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (int rc = launch_reduce_batch(prev, nprev, s)) return rc;
+  if (g_h_in && g_h_in != gh) hipMemcpyAsync(g_h_in, gh, n * 64 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (g_x_in && g_x_in != gx) hipMemcpyAsync(g_x_in, gx, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (g_v_in && g_v_in != gv) hipMemcpyAsync(g_v_in, gv, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   return check_launch("segno_backward");
 }
 

@@ -213,7 +213,16 @@ class SEGNO(nn.Module):
         """SEGNO.embedding (model.py:73): a torch op on the device, so it is on the autograd tape
         in training."""
         _lib.require_device(his, self.embedding.weight)
-        return torch.nn.functional.linear(his.to(torch.float32), self.embedding.weight, self.embedding.bias)
+        x, w = his.to(torch.float32), self.embedding.weight
+        if x.shape[-1] > 8:
+            return torch.nn.functional.linear(x, w, self.embedding.bias)
+        # K = in_node_nf <= 8: broadcast multiply-adds (elementwise kernels, and reductions in the
+        # backward) instead of a K-deep GEMM, for which the BLAS picks a slow tile (83 us at the C3
+        # size for K = 1, the largest torch op of the training step)
+        out = self.embedding.bias + x[..., :1] * w[:, 0]
+        for k in range(1, x.shape[-1]):
+            out = out + x[..., k:k + 1] * w[:, k]
+        return out
 
     @torch.no_grad()
     def _run(self, his, h_in, x, edges, v, edge_attr, T):
