@@ -298,7 +298,7 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
  * nonode_egno_backward runs the same reverse kernels from its saved state instead.
  *
  * nonode_egnn_layer_bwd: EGNN_Layer.forward (basic.py:167-186; variant NONODE_VARIANT_EGNO) over
- * n_graphs fully connected graphs of N nodes (N <= 31: the edge backward's LDS tables; a larger N
+ * n_graphs fully connected graphs of N nodes (N <= 115: the edge backward's LDS tables; a larger N
  * returns NONODE_EUNSUPPORTED before any launch; edge features of graph g from sample
  * g % ef_mod) with inputs h [n][64], x, v [n][3] (n = n_graphs N). blob / bblob from
  * nonode_pack_layer / nonode_pack_layer_bwd. Given dL/dx_out (g_v, g_h: NULL = 0) writes every
