@@ -130,6 +130,31 @@ int nonode_egno_forward_frames(int B, int N, int T, int n_layers, int in_node, i
                                float* x_out, float* v_out, float* h_out,
                                void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- EGNO(flat=True) (main_simulation_simple_no.py --flat; basic.py:38-40: every BaseMLP 4x wide,
+ * 256 hidden channels, with Tanh): forward only ---- */
+/* Floats in one packed flat-layer blob. */
+size_t nonode_flat_blob_floats(void);
+/* Pack one flat EGNN_Layer (variant NONODE_VARIANT_EGNO, optionally | NONODE_LAYER_NORM_RADIAL; hidden 64,
+ * so edge W1 [256][129 + ne], W2 [64][256], coord / node_v W1 [256][64], W2 [1][256], node W1
+ * [256][128], W2 [64][256]) into the flat layer kernels' fragment layout (device -> device). */
+int nonode_pack_layer_flat(const nonode_layer_weights* w, int variant, int hidden, int n_edge_feat,
+                           float* blob, void* stream);
+/* Workspace bytes nonode_egno_forward_flat needs (nonode_egno_workspace_bytes plus n x 580 floats for
+ * the flat layer's node projections and sums, n = B N T). */
+size_t nonode_egno_flat_workspace_bytes(int B, int N, int T, int Bt);
+/* EGNO.forward with flat=True: the arguments of nonode_egno_forward_frames with blobs from
+ * nonode_pack_layer_flat; t_in = NULL takes the single-input layout of nonode_egno_forward
+ * (x, v, loc_mean, h, edge_fea of the B N nodes, broadcast over the frames). */
+int nonode_egno_forward_flat(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                             int time_emb_dim, int modes, int Bt,
+                             const float* x, const float* h, const float* v, const float* loc_mean,
+                             const float* edge_fea, const float* t_in, const float* t_out,
+                             const float* emb_w, const float* emb_b,
+                             const float* const* blobs, const float* const* tconv_blobs,
+                             const float* const* tconvx_w,
+                             float* x_out, float* v_out, float* h_out,
+                             void* workspace, size_t workspace_bytes, void* stream);
+
 /* Workspace bytes nonode_segno_forward_step needs. */
 size_t nonode_segno_workspace_bytes(int B, int N);
 

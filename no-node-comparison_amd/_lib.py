@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("NONODE_LIB") or os.path.join(_HERE, "libnonode.so")
 SYMBOLS = (
     "nonode_version", "nonode_last_error", "nonode_layer_blob_floats", "nonode_pack_layer",
     "nonode_egno_workspace_bytes", "nonode_egno_forward", "nonode_egno_forward_frames", "nonode_segno_workspace_bytes",
+    "nonode_flat_blob_floats", "nonode_pack_layer_flat", "nonode_egno_flat_workspace_bytes", "nonode_egno_forward_flat",
     "nonode_segno_forward_step", "nonode_egno_tconv", "nonode_egnn_layer", "nonode_profile_begin",
     "nonode_profile_end", "nonode_tconv_blob_floats", "nonode_pack_tconv",
     "nonode_bwd_blob_floats", "nonode_pack_layer_bwd", "nonode_egno_train_state_bytes",
@@ -87,6 +88,11 @@ def lib():
                                       + [_sz, _vp])
     L.nonode_egno_forward_frames.argtypes = ([_i] * 9 + [_vp] * 9 + [ctypes.POINTER(_vp)] * 3 + [_vp] * 4
                                              + [_sz, _vp])
+    L.nonode_flat_blob_floats.restype = _sz
+    L.nonode_pack_layer_flat.argtypes = [ctypes.POINTER(LayerWeights), _i, _i, _i, _vp, _vp]
+    L.nonode_egno_flat_workspace_bytes.argtypes = [_i, _i, _i, _i]
+    L.nonode_egno_flat_workspace_bytes.restype = _sz
+    L.nonode_egno_forward_flat.argtypes = L.nonode_egno_forward_frames.argtypes
     L.nonode_segno_workspace_bytes.argtypes = [_i, _i]
     L.nonode_segno_workspace_bytes.restype = _sz
     L.nonode_segno_forward_step.argtypes = ([_i] * 5 + [_vp] * 8 + [_f, _i] + [_vp] * 4 + [_sz, _vp])

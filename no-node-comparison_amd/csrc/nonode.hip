@@ -1718,13 +1718,21 @@ size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt) {
   const size_t n = (size_t)B * N * T;
   return (n * 64 + n * 3 + (size_t)Bt * T * 64 + 64) * sizeof(float);
 }
+size_t nonode_egno_flat_workspace_bytes(int B, int N, int T, int Bt) {
+  return nonode_egno_workspace_bytes(B, N, T, Bt) + (size_t)B * N * T * 580 * sizeof(float);
+}
 
 }  // extern "C"
 
 namespace {
 // nonode_egno_forward / nonode_egno_forward_frames: frames = 1 takes per-frame x, h, v, loc_mean and
 // edge_fea (and t_in for the input-time embedding), frames = 0 the single input replicated over T
-int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+// nonode_flat.hip (included at the end of this unit): one EGNN layer with flat=True
+int launch_flat_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const float* x, const float* v,
+                      const float* ef, const float* blob, float* h_out, float* x_out, float* ws, hipStream_t s);
+// flat: the blobs are flat-layer blobs (nonode_pack_layer_flat), the workspace has the flat layer's
+// n x 580 floats after the common part (nonode_egno_flat_workspace_bytes)
+int egno_forward_impl(int frames, int flat, int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
                         int time_emb_dim, int modes, int Bt,
                         const float* x, const float* h, const float* v, const float* loc_mean,
                         const float* edge_fea, const float* t_in, const float* t_out,
@@ -1744,9 +1752,9 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
   if (!x || !h || !v || (tc && !loc_mean) || !t_out || !emb_w || !emb_b || !blobs || tc != (tconvx_w != nullptr) ||
       !x_out || !v_out || !h_out || !workspace)
     return fail(NONODE_EINVAL, "egno_forward: null pointer");
-  if (workspace_bytes < nonode_egno_workspace_bytes(B, N, T, Bt))
-    return fail(NONODE_EINVAL, "egno_forward: workspace %zu < %zu", workspace_bytes,
-                nonode_egno_workspace_bytes(B, N, T, Bt));
+  const size_t ws_need = flat ? nonode_egno_flat_workspace_bytes(B, N, T, Bt) : nonode_egno_workspace_bytes(B, N, T, Bt);
+  if (workspace_bytes < ws_need)
+    return fail(NONODE_EINVAL, "egno_forward: workspace %zu < %zu", workspace_bytes, ws_need);
   hipStream_t s = (hipStream_t)stream;
   const int BN = B * N;
   const size_t n = (size_t)BN * T;
@@ -1754,6 +1762,14 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
   float* xB = hB + n * 64;
   float* etab = xB + n * 3;
   const int emb_ld = in_node + (t_in ? 2 : 1) * time_emb_dim;
+  float* flat_ws = (float*)((char*)workspace + nonode_egno_workspace_bytes(B, N, T, Bt));
+  auto layer = [&](int l, const float* hi, const float* xi, float* ho, float* xo) {
+    if (flat)
+      return launch_flat_layer(T * B, N, n_edge_feat, frames ? T * B : B, hi, xi, v_out, edge_fea, blobs[l], ho, xo,
+                               flat_ws, s);
+    return launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hi, xi, v_out, edge_fea, blobs[l], 0.f, 1.f,
+                              0, ho, xo, nullptr, s, 1, nullptr, nullptr, nullptr, BN);
+  };
   {
     const int tot = Bt * T * 64;
     hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim,
@@ -1771,10 +1787,7 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
     if (int rc = check_launch("h0_kernel")) return rc;
     for (int l = 0; l < L; ++l) {
       const int i = (L - l) & 1, o = (L - 1 - l) & 1;
-      if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hb[i], xb[i], v_out, edge_fea,
-                                      blobs[l], 0.f, 1.f, 0, hb[o], xb[o], nullptr, s, 1, nullptr, nullptr, nullptr,
-                                      BN))
-        return rc;
+      if (int rc = layer(l, hb[i], xb[i], hb[o], xb[o])) return rc;
     }
     return NONODE_OK;
   }
@@ -1790,9 +1803,7 @@ int egno_forward_impl(int frames, int B, int N, int T, int n_layers, int in_node
       a.h = h_out; a.x = x_out; a.v = v_out; a.lm = loc_mean;
     }
     if (int rc = launch_tconv(l == 0, a, s)) return rc;
-    if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hB, xB, v_out, edge_fea, blobs[l], 0.f, 1.f, 0,
-                                    h_out, x_out, nullptr, s, 1, nullptr, nullptr, nullptr, BN))
-      return rc;
+    if (int rc = layer(l, hB, xB, h_out, x_out)) return rc;
   }
   return NONODE_OK;
 }
@@ -1809,9 +1820,23 @@ int nonode_egno_forward(int B, int N, int T, int n_layers, int in_node, int n_ed
                         const float* const* tconvx_w,
                         float* x_out, float* v_out, float* h_out,
                         void* workspace, size_t workspace_bytes, void* stream) {
-  return egno_forward_impl(0, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v, loc_mean,
+  return egno_forward_impl(0, 0, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v, loc_mean,
                            edge_fea, nullptr, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w, x_out, v_out, h_out,
                            workspace, workspace_bytes, stream);
+}
+
+int nonode_egno_forward_flat(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
+                             int time_emb_dim, int modes, int Bt,
+                             const float* x, const float* h, const float* v, const float* loc_mean,
+                             const float* edge_fea, const float* t_in, const float* t_out,
+                             const float* emb_w, const float* emb_b,
+                             const float* const* blobs, const float* const* tconv_blobs,
+                             const float* const* tconvx_w,
+                             float* x_out, float* v_out, float* h_out,
+                             void* workspace, size_t workspace_bytes, void* stream) {
+  return egno_forward_impl(t_in ? 1 : 0, 1, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v,
+                           loc_mean, edge_fea, t_in, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w, x_out, v_out,
+                           h_out, workspace, workspace_bytes, stream);
 }
 
 int nonode_egno_forward_frames(int B, int N, int T, int n_layers, int in_node, int n_edge_feat,
@@ -1823,7 +1848,7 @@ int nonode_egno_forward_frames(int B, int N, int T, int n_layers, int in_node, i
                                const float* const* tconvx_w,
                                float* x_out, float* v_out, float* h_out,
                                void* workspace, size_t workspace_bytes, void* stream) {
-  return egno_forward_impl(1, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v, loc_mean,
+  return egno_forward_impl(1, 0, B, N, T, n_layers, in_node, n_edge_feat, time_emb_dim, modes, Bt, x, h, v, loc_mean,
                            edge_fea, t_in, t_out, emb_w, emb_b, blobs, tconv_blobs, tconvx_w, x_out, v_out, h_out,
                            workspace, workspace_bytes, stream);
 }
@@ -1922,3 +1947,4 @@ int nonode_debug_stamps(unsigned long long* out16) {
 #include "nonode_rollout.hip"
 #include "nonode_sim.hip"
 #include "nonode_data.hip"
+#include "nonode_flat.hip"

@@ -17,34 +17,37 @@ from .graph import check_full_graph
 
 class _MLP(nn.Module):
     """Two Linear layers with SiLU between (and after, if last_act) — BaseMLP's parameters
-    (basic.py:34-58) under the attribute name ``mlp``."""
+    (basic.py:34-58) under the attribute name ``mlp``. flat (basic.py:38-40): Tanh and a 4x wider
+    hidden layer."""
 
-    def __init__(self, din, dhid, dout, last_act=False):
+    def __init__(self, din, dhid, dout, last_act=False, flat=False):
         super().__init__()
-        layers = [nn.Linear(din, dhid), nn.SiLU(), nn.Linear(dhid, dout)]
+        act = nn.Tanh if flat else nn.SiLU
+        dhid = 4 * dhid if flat else dhid
+        layers = [nn.Linear(din, dhid), act(), nn.Linear(dhid, dout)]
         if last_act:
-            layers.append(nn.SiLU())
+            layers.append(act())
         self.mlp = nn.Sequential(*layers)
 
 
 class _InvariantEdgeNet(nn.Module):
     """Holds the edge-message MLP under ``scalar_net`` (InvariantScalarNet, basic.py:107-123)."""
 
-    def __init__(self, din, hidden):
+    def __init__(self, din, hidden, flat=False):
         super().__init__()
-        self.scalar_net = _MLP(din, hidden, hidden, last_act=True)
+        self.scalar_net = _MLP(din, hidden, hidden, last_act=True, flat=flat)
 
 
 class EGNNLayerParams(nn.Module):
-    """Parameters of one EGNN_Layer (basic.py:147-165); compute lives in the fused HIP kernel.
-    with_v=False has no node_v_net (basic.py:156-160)."""
+    """Parameters of one EGNN_Layer (basic.py:147-165); compute lives in the fused HIP kernel (flat:
+    the 256-wide layer kernels). with_v=False has no node_v_net (basic.py:156-160)."""
 
-    def __init__(self, in_edge_nf, hidden_nf, with_v=True):
+    def __init__(self, in_edge_nf, hidden_nf, with_v=True, flat=False):
         super().__init__()
-        self.edge_message_net = _InvariantEdgeNet(1 + 2 * hidden_nf + in_edge_nf, hidden_nf)
-        self.coord_net = _MLP(hidden_nf, hidden_nf, 1)
-        self.node_v_net = _MLP(hidden_nf, hidden_nf, 1) if with_v else None
-        self.node_net = _MLP(2 * hidden_nf, hidden_nf, hidden_nf)
+        self.edge_message_net = _InvariantEdgeNet(1 + 2 * hidden_nf + in_edge_nf, hidden_nf, flat)
+        self.coord_net = _MLP(hidden_nf, hidden_nf, 1, flat=flat)
+        self.node_v_net = _MLP(hidden_nf, hidden_nf, 1, flat=flat) if with_v else None
+        self.node_net = _MLP(2 * hidden_nf, hidden_nf, hidden_nf, flat=flat)
 
     def weight_struct(self):
         e, c, v, n = (self.edge_message_net.scalar_net.mlp, self.coord_net.mlp,
@@ -80,8 +83,9 @@ class EGNO(nn.Module):
     Supported: hidden_nf=64, SiLU activation, any num_inputs, norm (the radial input normalised,
     basic.py:140-141), use_time_conv (False: no TimeConv modules, egno.py:27-33, 99-107 skipped).
     with_v=False builds the reference's module tree (no node_v_net) but, as in the reference, cannot
-    run forward (egno.py:95 / basic.py:180-181 need v and node_v_net). flat=True (BaseMLP widened
-    to 4*hidden with Tanh, basic.py:39-41) raises NotImplementedError at construction.
+    run forward (egno.py:95 / basic.py:180-181 need v and node_v_net). flat=True (every BaseMLP 4x
+    wide with Tanh, basic.py:38-40; main_simulation_simple_no.py --flat) runs forward on its own layer
+    kernels (csrc/nonode_flat.hip); its training (a 256-wide reverse pass) raises NotImplementedError.
     """
 
     def __init__(self, n_layers, in_node_nf, in_edge_nf, hidden_nf, activation=nn.SiLU(), device='cpu',
@@ -91,8 +95,6 @@ class EGNO(nn.Module):
         unsupported = []
         if num_inputs < 1:
             unsupported.append(f"num_inputs={num_inputs}")
-        if flat:
-            unsupported.append("flat=True")
         if hidden_nf != 64:
             unsupported.append(f"hidden_nf={hidden_nf}")
         if not isinstance(activation, nn.SiLU):
@@ -111,6 +113,7 @@ class EGNO(nn.Module):
         self.in_node_nf = in_node_nf
         self.in_edge_nf = in_edge_nf
         self.use_time_conv = use_time_conv
+        self.flat = flat
         self.num_timesteps = num_timesteps if not fix_out_size else 10
         self.device = device
         modes = num_modes_for(num_timesteps, num_modes)
@@ -121,7 +124,7 @@ class EGNO(nn.Module):
         # egno.py:12-16: the multi-input model also embeds each frame's input time
         self.embedding = nn.Linear(in_node_nf + (2 if num_inputs > 1 else 1) * time_emb_dim, hidden_nf)
         for _ in range(n_layers):
-            self.layers.append(EGNNLayerParams(in_edge_nf, hidden_nf, with_v))
+            self.layers.append(EGNNLayerParams(in_edge_nf, hidden_nf, with_v, flat))
         if use_time_conv:
             self.time_conv_modules = nn.ModuleList()
             self.time_conv_x_modules = nn.ModuleList()
@@ -139,14 +142,15 @@ class EGNO(nn.Module):
 
     def _packed(self):
         """Packed kernel weights (layer blobs, TimeConv blobs or None without time convolutions),
-        rebuilt whenever a parameter changed in place (optimizer step) or moved."""
+        rebuilt whenever a parameter changed in place (optimizer step) or moved (flat: the flat
+        layer blobs of nonode_pack_layer_flat)."""
         params = [p for l in self.layers for p in l.parameters()] + \
             ([m.t_conv.weights1 for m in self.time_conv_modules] if self.use_time_conv else [])
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._blobs is not None and key == self._blob_key:
             return self._blobs
         L = _lib.lib()
-        n = L.nonode_layer_blob_floats()
+        n = L.nonode_flat_blob_floats() if self.flat else L.nonode_layer_blob_floats()
         dev = self.embedding.weight.device
         blobs = torch.empty(self.n_layers, n, dtype=torch.float32, device=dev)
         tblobs = torch.empty(self.n_layers, L.nonode_tconv_blob_floats(self.num_modes), dtype=torch.float32,
@@ -156,9 +160,14 @@ class EGNO(nn.Module):
         ws = [layer.weight_struct() for layer in self.layers]
         WP = ctypes.POINTER(_lib.LayerWeights)
         P = ctypes.c_void_p * self.n_layers
-        _lib.check(L.nonode_pack_layers((WP * self.n_layers)(*[ctypes.pointer(w) for w in ws]), self.n_layers,
-                                        self._pack_variant(), self.hidden_nf, self.in_edge_nf,
-                                        P(*[blobs[i].data_ptr() for i in range(self.n_layers)]), stream))
+        if self.flat:
+            for i, w in enumerate(ws):
+                _lib.check(L.nonode_pack_layer_flat(ctypes.byref(w), self._pack_variant(), self.hidden_nf,
+                                                    self.in_edge_nf, blobs[i].data_ptr(), stream))
+        else:
+            _lib.check(L.nonode_pack_layers((WP * self.n_layers)(*[ctypes.pointer(w) for w in ws]), self.n_layers,
+                                            self._pack_variant(), self.hidden_nf, self.in_edge_nf,
+                                            P(*[blobs[i].data_ptr() for i in range(self.n_layers)]), stream))
         if self.use_time_conv:
             tws = [m.t_conv.weights1.detach().float().contiguous() for m in self.time_conv_modules]
             _lib.check(L.nonode_pack_tconvs(P(*[t.data_ptr() for t in tws]), self.n_layers, self.num_modes,
@@ -211,6 +220,8 @@ class EGNO(nn.Module):
         if v is None or (loc_mean is None and self.use_time_conv):
             raise ValueError("EGNO.forward needs v and loc_mean (the time convolution stacks "
                              "x - loc_mean with v, egno.py:103-105)")
+        if self.flat and self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            self._no_flat_training()
         if self.num_inputs > 1:
             return self._forward_multi(x, h, edge_index, edge_fea, v, loc_mean, timesteps_in, timesteps_out)
         _lib.require_device(x, h, v, loc_mean, edge_fea, self.embedding.weight)
@@ -269,9 +280,15 @@ class EGNO(nn.Module):
         if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
             from .autograd import egno_forward_train
             return egno_forward_train(self, xf, hf, eff, vf, lmf, t_out, B, N, t_in=t_in)
+        L = _lib.lib()
         with torch.no_grad():
-            return self._launch_forward(_lib.lib().nonode_egno_forward_frames, B, N, xf, hf, vf, lmf, eff, t_out,
-                                        t_in=t_in)
+            return self._launch_forward(L.nonode_egno_forward_flat if self.flat else L.nonode_egno_forward_frames,
+                                        B, N, xf, hf, vf, lmf, eff, t_out, t_in=t_in)
+
+    def _no_flat_training(self):
+        if self.flat:
+            raise NotImplementedError("EGNO(flat=True) training: the MI355X reverse pass is built for the "
+                                      "64-wide SiLU MLPs only (flat=True runs forward / eval)")
 
     def _t_out_f32(self, t_out):
         """timesteps_out as f32 (cached per tensor/version: callers pass the same int64 tensor)."""
@@ -289,6 +306,9 @@ class EGNO(nn.Module):
     def _forward_kernels(self, x, h, edge_fea, v, loc_mean, t_out, B, N):
         f32 = lambda t: None if t is None else t.detach().to(torch.float32).contiguous()  # noqa: E731
         x, h, v, lm, ef = f32(x), f32(h), f32(v), f32(loc_mean), f32(edge_fea)
+        if self.flat:   # nonode_egno_forward_flat: t_in NULL = the single-input embedding
+            return self._launch_forward(_lib.lib().nonode_egno_forward_flat, B, N, x, h, v, lm, ef,
+                                        self._t_out_f32(t_out), t_in=False)
         return self._launch_forward(_lib.lib().nonode_egno_forward, B, N, x, h, v, lm, ef, self._t_out_f32(t_out))
 
     def _launch_forward(self, entry, B, N, x, h, v, lm, ef, tt, t_in=None):
@@ -301,7 +321,8 @@ class EGNO(nn.Module):
         v_out = torch.empty(n, 3, device=dev)
         h_out = torch.empty(n, self.hidden_nf, device=dev)
         L = _lib.lib()
-        ws_bytes = L.nonode_egno_workspace_bytes(B, N, T, tt.shape[0])
+        ws_bytes = (L.nonode_egno_flat_workspace_bytes if self.flat else L.nonode_egno_workspace_bytes)(
+            B, N, T, tt.shape[0])
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
         P = ctypes.c_void_p * self.n_layers
         blob_p = P(*[blobs[i].data_ptr() for i in range(self.n_layers)])
@@ -314,6 +335,6 @@ class EGNO(nn.Module):
                 tt.shape[0], _lib.ptr(x), _lib.ptr(h), _lib.ptr(v), _lib.ptr(lm), _lib.ptr(ef))
         if t_in is None:
             _lib.check(entry(*head, _lib.ptr(tt), *tail))
-        else:
-            _lib.check(entry(*head, _lib.ptr(t_in), _lib.ptr(tt), *tail))
+        else:   # (t_in=False: the flat entry's NULL input-time embedding)
+            _lib.check(entry(*head, _lib.ptr(t_in) if t_in is not False else None, _lib.ptr(tt), *tail))
         return x_out, v_out, h_out

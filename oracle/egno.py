@@ -23,10 +23,12 @@ def linear(x, p, name):
     return x @ p[name + ".weight"].T + p[name + ".bias"]
 
 
-def base_mlp(x, p, name, last_act=False):
-    """BaseMLP (basic.py:34-58): Linear, act, Linear[, act]."""
-    y = linear(silu(linear(x, p, name + ".mlp.0")), p, name + ".mlp.2")
-    return silu(y) if last_act else y
+def base_mlp(x, p, name, last_act=False, flat=False):
+    """BaseMLP (basic.py:34-58): Linear, act, Linear[, act]; flat=True (basic.py:38-40): Tanh, and the
+    hidden width 4x (carried by the weights' shapes)."""
+    act = np.tanh if flat else silu
+    y = linear(act(linear(x, p, name + ".mlp.0")), p, name + ".mlp.2")
+    return act(y) if last_act else y
 
 
 def timestep_embedding(timesteps, embedding_dim=32, max_positions=10000, dtype=np.float32):
@@ -80,9 +82,9 @@ def radial_normalize(s):
     return s / np.maximum(np.abs(s), np.asarray(1e-12, dtype=s.dtype))
 
 
-def egnn_layer(p, prefix, x, h, row, col, edge_fea, v, norm=False):
-    """EGNN_Layer.forward (basic.py:167-186), with_v=True, flat=False; norm normalises the radial
-    input (basic.py:140-141).
+def egnn_layer(p, prefix, x, h, row, col, edge_fea, v, norm=False, flat=False):
+    """EGNN_Layer.forward (basic.py:167-186), with_v=True; norm normalises the radial input
+    (basic.py:140-141); flat: every BaseMLP 4x wide with Tanh (basic.py:38-40).
 
     Edge-MLP input order is [|r|^2, h_i, h_j, e] (InvariantScalarNet basic.py:136-143
     + hij = cat(h[row], h[col], edge_fea) at basic.py:170).
@@ -92,18 +94,18 @@ def egnn_layer(p, prefix, x, h, row, col, edge_fea, v, norm=False):
     if norm:
         s = radial_normalize(s)
     inp = np.concatenate([s, h[row], h[col], edge_fea], axis=-1)
-    m = base_mlp(inp, p, prefix + ".edge_message_net.scalar_net", last_act=True)
-    c = base_mlp(m, p, prefix + ".coord_net")
+    m = base_mlp(inp, p, prefix + ".edge_message_net.scalar_net", last_act=True, flat=flat)
+    c = base_mlp(m, p, prefix + ".coord_net", flat=flat)
     f = rij * c
     tot_f = np.clip(aggregate(f, row, x.shape[0], "mean"), -100, 100)
-    x = x + base_mlp(h, p, prefix + ".node_v_net") * v + tot_f
+    x = x + base_mlp(h, p, prefix + ".node_v_net", flat=flat) * v + tot_f
     tot_m = aggregate(m, row, x.shape[0], "sum")
-    h = base_mlp(np.concatenate([h, tot_m], axis=-1), p, prefix + ".node_net")
+    h = base_mlp(np.concatenate([h, tot_m], axis=-1), p, prefix + ".node_net", flat=flat)
     return x, v, h
 
 
 def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=10,
-                 hidden=64, time_emb_dim=32, capture=None, norm=False, use_time_conv=True):
+                 hidden=64, time_emb_dim=32, capture=None, norm=False, use_time_conv=True, flat=False):
     """EGNO.forward (egno.py:37-111) for num_inputs == 1 (use_time_conv=False skips egno.py:99-107).
 
     x, v, loc_mean: [BN, 3]; h: [BN, in_node]; row/col: [E]; edge_fea: [E, in_edge];
@@ -129,7 +131,7 @@ def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=
     ef = np.tile(edge_fea, (T, 1))
     for i in range(n_layers):
         if not use_time_conv:
-            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
+            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm, flat=flat)
             continue
         hh = time_conv(hh.reshape(T, BN, hidden), p[f"time_conv_modules.{i}.t_conv.weights1"])
         hh = hh.reshape(T * BN, hidden)
@@ -139,7 +141,7 @@ def egno_forward(p, x, h, row, col, edge_fea, v, loc_mean, t_out, n_layers=4, T=
         vv = X[..., 1].reshape(T * BN, 3)
         if capture is not None:
             capture[f"tconv{i}"] = (hh, xx, vv)
-        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm, flat=flat)
         if capture is not None:
             capture[f"layer{i}"] = (xx, vv, hh)
     return xx, vv, hh
@@ -153,7 +155,7 @@ def frame_inputs(num_inputs, T):
 
 
 def egno_forward_multi(p, x, h, row, col, edge_fea, v, loc_mean, t_in, t_out, n_layers=4, T=10,
-                       hidden=64, time_emb_dim=32, norm=False, use_time_conv=True):
+                       hidden=64, time_emb_dim=32, norm=False, use_time_conv=True, flat=False):
     """EGNO.forward (egno.py:37-111) for num_inputs = I > 1.
 
     x, v, loc_mean: [I, BN, 3]; h: [I, BN, in_node]; edge_fea: [I, E, in_edge]; t_in: [Bt, I];
@@ -181,7 +183,7 @@ def egno_forward_multi(p, x, h, row, col, edge_fea, v, loc_mean, t_in, t_out, n_
     ef = edge_fea[f].reshape(T * E, -1)
     for i in range(n_layers):
         if not use_time_conv:
-            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
+            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm, flat=flat)
             continue
         hh = time_conv(hh.reshape(T, BN, hidden), p[f"time_conv_modules.{i}.t_conv.weights1"])
         hh = hh.reshape(T * BN, hidden)
@@ -189,7 +191,7 @@ def egno_forward_multi(p, x, h, row, col, edge_fea, v, loc_mean, t_in, t_out, n_
         X = time_conv_x(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
         xx = X[..., 0].reshape(T * BN, 3) + lm
         vv = X[..., 1].reshape(T * BN, 3)
-        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, ef, vv, norm=norm, flat=flat)
     return xx, vv, hh
 
 

@@ -21,10 +21,12 @@ def _lin(x, p, name):
     return F.linear(x, p[name + ".weight"], p.get(name + ".bias"))
 
 
-def _mlp(x, p, name, last_act=False):
-    """BaseMLP (basic.py:34-58): Linear, SiLU, Linear[, SiLU]."""
-    y = _lin(F.silu(_lin(x, p, name + ".mlp.0")), p, name + ".mlp.2")
-    return F.silu(y) if last_act else y
+def _mlp(x, p, name, last_act=False, flat=False):
+    """BaseMLP (basic.py:34-58): Linear, SiLU, Linear[, SiLU]; flat (basic.py:38-40): Tanh (the 4x
+    hidden width is the weights' shape)."""
+    act = torch.tanh if flat else F.silu
+    y = _lin(act(_lin(x, p, name + ".mlp.0")), p, name + ".mlp.2")
+    return act(y) if last_act else y
 
 
 def timestep_embedding(t, dim=32, max_positions=10000):
@@ -57,22 +59,23 @@ def _scatter(msg, row, n, mean):
     return out
 
 
-def egnn_layer(p, pre, x, h, row, col, ef, v, norm=False):
+def egnn_layer(p, pre, x, h, row, col, ef, v, norm=False, flat=False):
     """EGNN_Layer.forward (basic.py:167-186): with_v, flat=False; norm: F.normalize of the radial
     input (basic.py:140-141)."""
     rij = x[row] - x[col]
     s = (rij * rij).sum(-1, keepdim=True)                         # InvariantScalarNet Gram (basic.py:136-143)
     if norm:
         s = F.normalize(s, p=2, dim=-1)
-    m = _mlp(torch.cat([s, h[row], h[col], ef], -1), p, pre + ".edge_message_net.scalar_net", last_act=True)
-    f = rij * _mlp(m, p, pre + ".coord_net")
-    x = x + _mlp(h, p, pre + ".node_v_net") * v + _scatter(f, row, x.shape[0], True).clamp(-100, 100)
-    h = _mlp(torch.cat([h, _scatter(m, row, x.shape[0], False)], -1), p, pre + ".node_net")
+    m = _mlp(torch.cat([s, h[row], h[col], ef], -1), p, pre + ".edge_message_net.scalar_net", last_act=True,
+             flat=flat)
+    f = rij * _mlp(m, p, pre + ".coord_net", flat=flat)
+    x = x + _mlp(h, p, pre + ".node_v_net", flat=flat) * v + _scatter(f, row, x.shape[0], True).clamp(-100, 100)
+    h = _mlp(torch.cat([h, _scatter(m, row, x.shape[0], False)], -1), p, pre + ".node_net", flat=flat)
     return x, v, h
 
 
 def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hidden=64, time_emb_dim=32,
-                 norm=False, use_time_conv=True, lrelu_masks=None, lrelu_record=None):
+                 norm=False, use_time_conv=True, lrelu_masks=None, lrelu_record=None, flat=False):
     """EGNO.forward (egno.py:37-111), num_inputs == 1. Returns (x, v, h), T-major rows.
     use_time_conv=False skips egno.py:99-107. lrelu_masks: per layer a [T, BN, hidden] bool tensor of
     given LeakyReLU branch decisions (y > 0) for TimeConv's activation (layer_no.py:123), in place of
@@ -89,7 +92,7 @@ def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hi
     lm = loc_mean.repeat(T, 1) if use_time_conv else None
     for i in range(n_layers):
         if not use_time_conv:
-            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm)
+            xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm, flat=flat)
             continue
         h3 = hh.reshape(T, BN, hidden)
         y = _spectral(h3, p[f"time_conv_modules.{i}.t_conv.weights1"])
@@ -101,7 +104,7 @@ def egno_forward(p, x, h, row, col, ef, v, loc_mean, t_out, n_layers=4, T=10, hi
         X = X + _spectral(X, p[f"time_conv_x_modules.{i}.t_conv.weights1"])
         xx = X[..., 0].reshape(T * BN, 3) + lm
         vv = X[..., 1].reshape(T * BN, 3)
-        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm)
+        xx, vv, hh = egnn_layer(p, f"layers.{i}", xx, hh, row_t, col_t, eft, vv, norm=norm, flat=flat)
     return xx, vv, hh
 
 

@@ -646,6 +646,12 @@ def make_segno_tanh(B=2, N=5, T=10, seed=4):
     np.savez_compressed(os.path.join(HERE, "segno_tanh.npz"), **fx)
 
 
+def make_flat():
+    """EGNO(flat=True) (main_simulation_simple_no.py --flat: every BaseMLP 4x wide with Tanh,
+    basic.py:38-40), seed-5 weights."""
+    _egno_opt("egno_flat", 5, flat=True)
+
+
 def make_options():
     _egno_opt("egno_norm", 2, coincide=True, norm=True)
     _egno_opt("egno_notc", 3, use_time_conv=False)
@@ -655,6 +661,9 @@ def make_options():
 if __name__ == "__main__":
     if sys.argv[1:] == ["options"]:
         make_options()
+        sys.exit(0)
+    if sys.argv[1:] == ["flat"]:
+        make_flat()
         sys.exit(0)
     if sys.argv[1:] == ["segno_multi"]:
         make_segno_multi()

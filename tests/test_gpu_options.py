@@ -1,7 +1,8 @@
 """GPU parity of the reference constructor options (tests/test_options.py pins the oracle side):
 EGNO norm=True (radial input normalised, basic.py:140-141), EGNO use_time_conv=False
 (egno.py:27-33, 99-107 skipped), SEGNO tanh=True (coord_mlp ends in nn.Tanh, gcl.py:57-59) --
-forward and training gradients through the HIP kernels.
+forward and training gradients through the HIP kernels; EGNO flat=True (basic.py:38-40, 256-wide
+Tanh MLPs, csrc/nonode_flat.hip) -- forward.
 
 Bars (max-norm relative): 1e-5 against the reference's own outputs / autograd gradients
 (egno_norm / egno_notc / segno_tanh fixtures) and against float64 references on other shapes.
@@ -129,6 +130,65 @@ def test_egno_no_time_conv_multi_input_matches_oracle():
                                        use_time_conv=False)
     with torch.no_grad():
         xo, vo, ho = m(_dev(x), _dev(h), [_dev(row), _dev(col)], _dev(ea), v=_dev(v), loc_mean=None,
+                       timesteps_in=_dev(t_in), timesteps_out=_dev(t_out))
+    check_rel("x", xo.cpu(), xr, TOL)
+    check_rel("v", vo.cpu(), vr, TOL)
+    check_rel("h", ho.cpu(), hr, TOL)
+
+
+FLAT = {"flat": dict(flat=True), "flat_norm": dict(flat=True, norm=True),
+        "flat_notc": dict(flat=True, use_time_conv=False)}
+
+
+def test_egno_flat_forward_matches_reference_golden():
+    """flat=True against the reference's own outputs (egno_flat fixture); training is refused."""
+    fx = load_golden("egno_flat")
+    m = _egno(FLAT["flat"], params_of(fx)).eval()
+    inp = _golden_inputs(fx)
+    with torch.no_grad():
+        x, v, h = _run(m, inp)
+    check_rel("flat x", x.cpu(), fx["out::x"], TOL)
+    check_rel("flat v", v.cpu(), fx["out::v"], TOL)
+    check_rel("flat h", h.cpu(), fx["out::h"], TOL)
+    with pytest.raises(NotImplementedError, match="flat=True"):
+        _run(m.train(), inp)
+
+
+@pytest.mark.parametrize("name", sorted(FLAT))
+@pytest.mark.parametrize("B,N", [(3, 7), (16, 20), (1, 37)])
+def test_egno_flat_forward_matches_f64_oracle(name, B, N):
+    """Ragged receiver tiles (B N T not a multiple of 16), N above one tile, every option pairing."""
+    T = 10
+    m = _egno(FLAT[name], seed=B + 2 * N).eval()
+    case = _egno_case(B, N, T, seed=N + 3)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    f64 = {k: (v.astype(np.float64) if k not in ("row", "col", "t_out") else v) for k, v in case.items()}
+    xr, vr, hr = oe.egno_forward(p, **f64, T=T, **FLAT[name])
+    with torch.no_grad():
+        x, v, h = _run(m, {k: _dev(val) for k, val in case.items()})
+    check_rel("x", x.cpu(), xr, TOL)
+    check_rel("v", v.cpu(), vr, TOL)
+    check_rel("h", h.cpu(), hr, TOL)
+
+
+def test_egno_flat_multi_input_matches_oracle():
+    B, N, T, I = 2, 6, 10, 3
+    m = _egno(FLAT["flat"], seed=23, num_inputs=I).eval()
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((I, B * N, 3)).astype(np.float32)
+    v = rng.standard_normal((I, B * N, 3)).astype(np.float32) * 0.5
+    lm = x.mean(1, keepdims=True).repeat(B * N, 1)
+    h = np.concatenate([np.linalg.norm(v, axis=-1, keepdims=True), np.ones((I, B * N, 1), np.float32)], -1)
+    row, col = tr.full_edges(B, N)
+    ea = rng.standard_normal((I, B * N * (N - 1), 2)).astype(np.float32)
+    t_in = np.tile(np.array([-2.0, -1.0, 0.0], np.float32), (B, 1))
+    t_out = np.tile(np.arange(1, T + 1, dtype=np.float32), (B, 1))
+    p = {k: q.detach().cpu().numpy().astype(np.float64) for k, q in m.state_dict().items()}
+    d = lambda a: a.astype(np.float64)  # noqa: E731
+    xr, vr, hr = oe.egno_forward_multi(p, d(x), d(h), row.numpy(), col.numpy(), d(ea), d(v), d(lm), t_in, t_out, T=T,
+                                       flat=True)
+    with torch.no_grad():
+        xo, vo, ho = m(_dev(x), _dev(h), [_dev(row), _dev(col)], _dev(ea), v=_dev(v), loc_mean=_dev(lm),
                        timesteps_in=_dev(t_in), timesteps_out=_dev(t_out))
     check_rel("x", xo.cpu(), xr, TOL)
     check_rel("v", vo.cpu(), vr, TOL)

@@ -15,7 +15,8 @@ from oracle import segno as osg
 from oracle import torch_ref as tr
 from tests.conftest import load_golden, maxnorm_rel, params_of
 
-EGNO_CASES = [("egno_norm", 2, dict(norm=True)), ("egno_notc", 3, dict(use_time_conv=False))]
+EGNO_CASES = [("egno_norm", 2, dict(norm=True)), ("egno_notc", 3, dict(use_time_conv=False)),
+              ("egno_flat", 5, dict(flat=True))]
 
 
 def _egno(seed, **opts):
@@ -130,9 +131,21 @@ def test_egno_with_v_false_builds_reference_tree_and_cannot_run():
         m(z, torch.zeros(10, 2), pkg.graph.full_edges(2, 5), torch.zeros(40, 2), v=z, loc_mean=z)
 
 
-def test_egno_flat_still_raises():
+def test_egno_flat_is_forward_only_and_packs_egno_layers_only():
+    """flat=True (basic.py:38-40: every BaseMLP 4x wide with Tanh) builds the reference tree and runs
+    forward on its own kernels (tests/test_gpu_options.py); training stops before any device work, and
+    the flat packer refuses SEGNO layers and unknown option bits without touching the device."""
+    m = _egno(0, flat=True)
+    e = m.layers[0].edge_message_net.scalar_net.mlp
+    assert e[0].weight.shape == (256, 2 * 64 + 1 + 2) and isinstance(e[1], torch.nn.Tanh)
+    z = torch.zeros(10, 3)
     with pytest.raises(NotImplementedError, match="flat=True"):
-        _egno(0, flat=True)
+        m.train()(z, torch.zeros(10, 2), pkg.graph.full_edges(2, 5), torch.zeros(40, 2), v=z, loc_mean=z)
+    L = pkg._lib.lib()
+    w = pkg._lib.LayerWeights(*([16] * 16))   # never dereferenced: the variant check fails first
+    for variant in (pkg._lib.VARIANT_SEGNO, pkg._lib.VARIANT_EGNO | pkg._lib.LAYER_TANH_COORD):
+        assert L.nonode_pack_layer_flat(w, variant, 64, 2, 16, None) == 1
+    assert L.nonode_flat_blob_floats() > L.nonode_layer_blob_floats()
 
 
 def test_pack_rejects_option_bits_of_the_other_variant():
