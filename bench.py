@@ -529,6 +529,14 @@ def run_segno(args, world, rank, dev, backend, gravity=False):
     return res
 
 
+def make_adam(args, params, **kw):
+    """The reference's optimizer, torch.optim.Adam with its hyper-parameters (model_confs.yaml:15-17,
+    train_nbody.py), in torch's fused implementation by default (--optimizer fused: the same update,
+    one kernel over every parameter instead of the multi-tensor 'foreach' chain of eight launches;
+    --optimizer foreach is torch's default form)."""
+    return torch.optim.Adam(params, fused=args.optimizer == "fused", foreach=args.optimizer == "foreach", **kw)
+
+
 def run_egno_train(args, world, rank, dev, backend):
     """C4: EGNO training step, charged N=20, T=10, B=512 per GPU (or --global-batch 4096 over the
     ranks): forward with saved state, the reference loss (main_simulation_simple_no.py:273-280),
@@ -549,7 +557,7 @@ def run_egno_train(args, world, rank, dev, backend):
     g = torch.Generator().manual_seed(777)
     loc_true = torch.randn(plan["B_global"], N, T, 3, generator=g)[plan["lo"]:plan["hi"]].to(dev)
     fg = FlatGrads(model.parameters())
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4, weight_decay=1e-8)
+    opt = make_adam(args, model.parameters(), lr=1e-4, weight_decay=1e-8)
 
     def loss_of(x):
         pred = x.reshape(T, B, N, 3).permute(1, 2, 0, 3)
@@ -596,6 +604,7 @@ def run_egno_train(args, world, rank, dev, backend):
     res = _result(args, world, plan, el / args.steps * 1e3, value,
                   f"C4: EGNO training step (fwd + bwd{' + 1 all-reduce' if world > 1 else ''} + Adam), charged N={N}, T={T}, B={B} per GPU",
                   {"n_balls": N, "num_timesteps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                   "optimizer": f"torch.optim.Adam ({args.optimizer})",
                    "parallelism": (f"data-parallel x{world}, one {backend} all-reduce per step" if backend else
                                    "single GPU, no all-reduce")},
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0, loss=float(loss.detach()))
@@ -704,7 +713,7 @@ def run_segno_train(args, world, rank, dev, backend):
     his = v.norm(dim=-1, keepdim=True)
     target = x + 0.3 * v
     fg = FlatGrads(model.parameters())
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    opt = make_adam(args, model.parameters(), lr=1e-4)
     w = B * world / plan["B_global"]   # shard-size weight: the all-reduce averages shard means
 
     def step():
@@ -742,6 +751,7 @@ def run_segno_train(args, world, rank, dev, backend):
                   f"SEGNO training step (forward_step of {T} substeps + MSE + HIP reverse pass"
                   f"{' + 1 all-reduce' if world > 1 else ''} + Adam), charged N={N}, B={B} per GPU",
                   {"n_balls": N, "substeps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                   "optimizer": f"torch.optim.Adam ({args.optimizer})",
                    "parallelism": (f"data-parallel x{world}, one {backend} all-reduce per step" if backend else
                                    "single GPU, no all-reduce")},
                   backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0)
@@ -999,6 +1009,8 @@ def parse_args(argv=None):
                     help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4; "
                          "egno_rollout = SURVEY row f1; sim_charged = row f3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--optimizer", choices=["fused", "foreach"], default="fused",
+                    help="torch Adam implementation of the training workloads (same update rule)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU baseline work (median of calls)")
     ap.add_argument("--cpu-samples", type=int, default=0, help="CPU baseline sample size where it is bounded")
     ap.add_argument("--prewarm-ms", type=float, default=300.0,

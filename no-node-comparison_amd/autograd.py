@@ -24,7 +24,8 @@ class EGNOTrain(torch.autograd.Function):
         L = _lib.lib()
         T = model.num_timesteps
         dev = x.device
-        x, h, v, ef, tt = _f32(x), _f32(h), _f32(v), _f32(edge_fea), _f32(t_out)
+        x, h, v, ef = _f32(x), _f32(h), _f32(v), _f32(edge_fea)
+        tt = model._t_out_f32(t_out)   # cached per tensor / version: no int64 -> f32 copy per step
         lm = _f32(loc_mean) if loc_mean is not None else None   # unused without time convolutions
         emb_cols = model.time_emb_dim * (1 if t_in is None else 2)
         Bt = tt.shape[0]
@@ -51,6 +52,9 @@ class EGNOTrain(torch.autograd.Function):
             ti = _f32(t_in)
             _lib.check(L.nonode_egno_forward_train_frames(*head, _lib.ptr(ti), _lib.ptr(tt), *tail))
         ctx.frames = t_in is not None
+        # outputs the loss does not use (v, h for the reference's loss on x) arrive as None rather
+        # than as zero-filled tensors: the library zeroes its own output-gradient buffers for them
+        ctx.set_materialize_grads(False)
         ctx.model, ctx.B, ctx.N, ctx.Bt = model, B, N, Bt
         ctx.state, ctx.lm, ctx.ef = state, lm, ef
         ctx.n_params = len(params)
@@ -137,6 +141,7 @@ class SEGNOStepTrain(torch.autograd.Function):
                                                 _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.stream_of(x)))
         ctx.model, ctx.T, ctx.B, ctx.N = model, T, B, N
         ctx.state, ctx.ea = state, ea
+        ctx.set_materialize_grads(False)   # unused outputs: None, zeroed by the library (see EGNOTrain)
         ctx.save_for_backward(*params)   # version check of the parameters (see EGNOTrain.forward)
         return x_out, h_out, v_out
 

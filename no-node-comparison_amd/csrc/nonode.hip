@@ -192,16 +192,20 @@ __global__ void pack_kernel(PackBatch pb) {
 #if NONODE_STAMP
 __device__ unsigned long long g_stamp[16];
 #define STAMP_DECL unsigned long long st_acc[16] = {}, st_last = __builtin_amdgcn_s_memtime();
+// (stamp_here: a constexpr of the enclosing body, so one build can stamp some instances only: the
+// stamped 8-wave SEGNO layer crashes LLVM's register allocator)
 #define STAMP(i)                                                   \
   do {                                                             \
-    __builtin_amdgcn_sched_barrier(0);                             \
-    const unsigned long long _t = __builtin_amdgcn_s_memtime();    \
-    st_acc[i] += _t - st_last;                                     \
-    st_last = _t;                                                  \
-    __builtin_amdgcn_sched_barrier(0);                             \
+    if constexpr (stamp_here) {                                    \
+      __builtin_amdgcn_sched_barrier(0);                           \
+      const unsigned long long _t = __builtin_amdgcn_s_memtime();  \
+      st_acc[i] += _t - st_last;                                   \
+      st_last = _t;                                                \
+      __builtin_amdgcn_sched_barrier(0);                           \
+    }                                                              \
   } while (0)
 #define STAMP_FLUSH                                                \
-  if (lane == 0)                                                   \
+  if (stamp_here && lane == 0)                                     \
     for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_stamp[_i], st_acc[_i]);
 #else
 #define STAMP_DECL
@@ -277,6 +281,7 @@ size_t layer_lds_floats(int ct, int s_rows, int keep = 0) {
 template <int VARIANT, int KF, int NW, bool OPT, bool SAVE = false>
 __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)[NW + 1]) {
   constexpr bool PAIR = NW == 4;
+  [[maybe_unused]] constexpr bool stamp_here = VARIANT == EGNO && NW == 4 && !OPT;   // (NONODE_STAMP builds)
   constexpr bool rnorm = OPT && VARIANT == EGNO;    // basic.py:140-141
   constexpr bool ctanh = OPT && VARIANT == SEGNO;   // gcl.py:57-59
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1374,12 +1379,14 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
 }
 
-// etab[b][t][o] = emb_b[o] + sum_k emb_w[o][din+k] * temb(t_out[b][t])[k]   (layer_no.py:8-17)
+// etab[b][t][o] = emb_b[o] + sum_k emb_w[o][din+k] * temb(t_out[b][t])[k]   (layer_no.py:8-17);
+// trig_out (training forward, else null): the [Bt][T][ncol] time-embedding values themselves
 // multi-input (t_in != null, egno.py:44-49, 77-79): emb_w columns are [h | temb(t_in) | temb(t_out)]
 // and t_in[b][t] is the input time of frame t's input
 __global__ __launch_bounds__(256) void temb_kernel(int Bt, int T, int din, int dim, const float* t_out,
                                                    const float* emb_w, int emb_ld, const float* emb_b,
-                                                   float* etab, const float* t_in = nullptr) {
+                                                   float* etab, const float* t_in = nullptr,
+                                                   float* trig_out = nullptr) {
   // a 256-thread block owns 4 (b, t) rows x 64 outputs; each row's sin / cos table (<= 2 * 64
   // values, dim <= 64 is checked by the host) is computed once into LDS instead of once per output
   __shared__ float trig[4][128];
@@ -1396,6 +1403,7 @@ __global__ __launch_bounds__(256) void temb_kernel(int Bt, int T, int din, int d
       const float fk = expf((float)(k % half) * -scale);
       const float arg = tv * fk;
       trig[row][c] = k < half ? sinf(arg) : cosf(arg);
+      if (trig_out) trig_out[(size_t)bt * ncol + c] = trig[row][c];   // training: the embedding's inputs
     }
   }
   __syncthreads();
@@ -1425,26 +1433,24 @@ __global__ void embed_kernel(int n_nodes, int din, const float* in, const float*
 // ---- first-layer inputs without a TimeConv (training forward; EGNO use_time_conv=False) -----------
 // h0[t*BN + c] = emb_w[:, :din] h_in[c] + etab[c % Bt][t]   (egno.py:63-76; same arithmetic as
 // tconv_kernel<true>), and x, v replicated over T (egno.py:89-96)
-// frames = 1 (num_inputs > 1): h_in, x, v are per frame ([T*BN] rows) instead of replicated
+// frames = 1 (num_inputs > 1): h_in, x, v are per frame ([T*BN] rows) instead of replicated;
+// hin_out (training forward, else null): a copy of the h_in rows (the embedding's inputs)
 __global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, const float* emb_w, int emb_ld,
                           const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr,
-                          int frames) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= BN * 64) return;
-  const int o = idx & 63, c = idx >> 6;
-  auto hin_part = [&](size_t r) {
-    float b = 0.f;
-    for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[r * din + k], b);
-    return b;
-  };
-  const float base = frames ? 0.f : hin_part((size_t)c);
-  const float* et = etab + (size_t)(c % Bt) * T * 64;
-  for (int t = 0; t < T; ++t) {
-    const size_t row = (size_t)t * BN + c;
-    const size_t src = frames ? row : (size_t)c;
-    h0[row * 64 + o] = et[t * 64 + o] + (frames ? hin_part(row) : base);
-    if (o < 3) { xr[row * 3 + o] = x[src * 3 + o]; vr[row * 3 + o] = v[src * 3 + o]; }
-  }
+                          int frames, float* hin_out = nullptr) {
+  // one thread per output (row, o): every store of the launch is independent (one coalesced 256-byte
+  // row per 64 threads), so the whole [T*BN][64] table streams at full occupancy
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)T * BN * 64) return;
+  const int o = (int)(idx & 63);
+  const int row = (int)(idx >> 6);   // (n rows of 256 B: n < 2^31 for any table that fits in HBM)
+  const int t = row / BN, c = row - t * BN;
+  const size_t src = frames ? (size_t)row : (size_t)c;
+  float b = 0.f;
+  for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[src * din + k], b);
+  h0[(size_t)row * 64 + o] = etab[((size_t)(c % Bt) * T + t) * 64 + o] + b;
+  if (o < 3) { xr[(size_t)row * 3 + o] = x[src * 3 + o]; vr[(size_t)row * 3 + o] = v[src * 3 + o]; }
+  if (hin_out && o < din && (frames || t == 0)) hin_out[src * din + o] = hin[src * din + o];
 }
 
 // ---- host-side launchers ----------------------------------------------------------------------
@@ -1782,7 +1788,7 @@ int egno_forward_impl(int frames, int flat, int B, int N, int T, int n_layers, i
     float* hb[2] = {h_out, hB};
     float* xb[2] = {x_out, xB};
     const int L = n_layers;
-    hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
+    hipLaunchKernelGGL(h0_kernel, dim3((unsigned)(((size_t)T * BN * 64 + 255) / 256)), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
                        etab, x, v, hb[L & 1], xb[L & 1], v_out, frames);
     if (int rc = check_launch("h0_kernel")) return rc;
     for (int l = 0; l < L; ++l) {

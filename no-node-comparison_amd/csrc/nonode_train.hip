@@ -13,11 +13,8 @@
 //                     170-173, 107-144): per-receiver / per-sender sums GA, GB and gx terms
 //   node_wgrad_kernel gh = part + W_A^T GA + W_B^T GB,  gx = gx + edge terms (and the node-level GEMMs)
 //   tconvx_bwd / tconv_bwd  TimeConv_x / TimeConv reverse (layer_no.py:80-178)
-// Weight gradients are GEMMs over edges or nodes, C = sum_k G[k] (x) A[k]: the kernels above write
-// the per-row operands, gemm_tn_partial sums K-slices per workgroup and gemm_reduce adds the
-// partials in a fixed order (deterministic).
-//
-// Stage 1 of the training path: exact f32 MFMAs (16x16x4) for every matrix product.
+// Weight gradients are sums over edges or nodes, C = sum_k G[k] (x) A[k]: the kernels above keep
+// per-workgroup partials and gemm_reduce_batch adds them in a fixed order (deterministic).
 
 #include "nonode_bwd_common.h"
 
@@ -212,30 +209,6 @@ __device__ __forceinline__ void amfma4_block(f4 (&acc)[4][4], const float (&gv)[
         "s_nop 11"
         : "+a"(acc[ot][0]), "+a"(acc[ot][1]), "+a"(acc[ot][2]), "+a"(acc[ot][3])
         : "v"(gv[ot]), "v"(av[0]), "v"(av[1]), "v"(av[2]), "v"(av[3]));
-}
-
-// ---- training-forward helpers (h0_kernel: nonode.hip) ----------------------------------------
-// emb_in[t*BN + c] = [h_in[c], temb(t_out[c % Bt][t])]  (the embedding Linear's input rows)
-// rows [h_in | temb(t_out)], or [h_in | temb(t_in) | temb(t_out)] when t_in != null (egno.py:77-79)
-__global__ void emb_in_kernel(int BN, int T, int din, int dim, int Bt, const float* hin, const float* t_out,
-                              float* emb_in, const float* t_in, int frames) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  const int w = din + (t_in ? 2 : 1) * dim;
-  if (idx >= BN * T * w) return;
-  const int k = idx % w, row = idx / w;
-  const int t = row / BN, c = row - t * BN;
-  float val;
-  if (k < din) {
-    val = hin[(size_t)(frames ? row : c) * din + k];
-  } else {
-    const int kq = k - din, which = kq / dim, kk = kq - which * dim, half = dim / 2;
-    const float scale = (float)(log(10000.0) / (double)(half - 1));
-    const float tv = ((t_in && which == 0) ? t_in : t_out)[(size_t)(c % Bt) * T + t];
-    const int j = kk < half ? kk : kk - half;
-    const float arg = tv * expf((float)j * -scale);
-    val = kk < half ? sinf(arg) : cosf(arg);
-  }
-  emb_in[idx] = val;
 }
 
 // ---- edge backward (basic.py:107-144, 167-173 reversed) ----------------------------------------
@@ -531,6 +504,7 @@ __device__ __forceinline__ float edge_sum16(float v) {
 template <int NE, int PASS, int OPT, int GT>
 __device__ __forceinline__ void edge_bwd_body(const EdgeBwdArgs& p) {
   constexpr bool rnorm = OPT == 1, ctanh = OPT == 2;
+  [[maybe_unused]] constexpr bool stamp_here = OPT == 0 && GT == 0;   // (NONODE_STAMP builds)
   const bool gtab = PASS == 1 && (GT == 2 ? p.gtab != 0 : GT == 1);
   // OPT 0: EGNO, OPT 3: SEGNO (compile-time: no per-edge branch); the option variants read p.segno
   const bool segno = OPT == 0 ? false : (OPT == 3 ? true : p.segno != 0);
@@ -1618,125 +1592,112 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
   }
 }
 
-// ---- weight-gradient GEMMs ---------------------------------------------------------------------
-// partial[wave][i][j] = sum over this wave's K-slice of G[k*ldg + i] * A[k*lda + j]  (j < N), and
-// partial[wave][i][N] = sum_k G[k][i] (the bias gradient). M, N <= 64. Each wave streams its rows
-// straight into v_mfma_f32_16x16x4_f32: lane (l & 15, l >> 4) supplies G[k0 + (l>>4)][16 ti + (l&15)]
-// as the A operand and A[k0 + (l>>4)][16 tj + (l&15)] as the B operand, so K runs along the lane
-// groups and the 64 x 64 result stays in 16 accumulator tiles. HBM-bound (one pass over G and A).
-// V4 (M = N = 64, row strides and bases 16-byte aligned): lane il holds channels 4 il .. 4 il + 3 of
-// its row as ONE float4 per operand (16 lanes = one 256-byte row), i.e. MFMA index 16 t + il stands
-// for channel 4 il + t; the epilogue maps the accumulator back.
-constexpr int GEMM_UNR = 8;
-template <bool V4>
-__device__ __forceinline__ void gemm_tn_body(const float* __restrict__ G, int ldg, int M, const float* __restrict__ A,
-                                             int lda, int N, long long K, long long kslice, float* partial) {
-  const int lane = threadIdx.x & 63, il = lane & 15, kr = lane >> 4;
-  const long long gw = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const long long k0 = gw * kslice, k1 = min(K, k0 + kslice);
-  f4 acc[4][4];
+// ---- embedding Linear gradient (egno.py:63-76 reversed) ------------------------------------------
+// dW[o][k] = sum over the rows r = t BN + c of gh0[r][o] in[r][k] and db[o] = sum_r gh0[r][o], where the
+// embedding's input row is in[r] = [h_in[frames ? r : c], trig[(c % Bt) T + t]]: the raw time embedding
+// of the row's sample and frame (layer_no.py:8-17), which temb_kernel writes into the saved state in the
+// training forward (h0_kernel saves h_in). The input rows themselves are never materialised.
+// A block walks 64-row tiles (grid-stride, the next tile's rows requested before this tile's sums):
+// gh0 rows and input rows staged in LDS, thread (o, q) adds rows 16 q .. 16 q + 15 of the tile into
+// column o (the input row is an LDS broadcast). The four row quarters are added in order and one
+// partial per block is written in gemm_reduce's layout: column block cb (input columns 64 cb ..) is
+// [blocks][64][nc_cb + 1], block 0's column nc_0 = the bias. gemm_reduce_batch adds them in block order.
+constexpr int EG_TILE = 64;
+constexpr int EG_MAX_BLOCKS = 512;
+template <int NCMAX>   // in_node + time-embedding columns: <= 40 or <= 136 (in_node <= 8, 2 x 64)
+__global__ __launch_bounds__(256) void emb_grad_kernel(int BN, int T, int Bt, int din, int ncol, int frames,
+                                                       const float* __restrict__ gh0, const float* __restrict__ hin,
+                                                       const float* __restrict__ trig, float* part) {
+  __shared__ float sG[EG_TILE][65];
+  __shared__ __attribute__((aligned(16))) float sA[EG_TILE][NCMAX];   // input rows, zero past column ld
+  __shared__ float sR[4][64][33];
+  const int tid = threadIdx.x, o = tid & 63, q = tid >> 6;
+  const int ld = din + ncol;
+  const int n = BN * T;   // (the host checks n < 2^31)
+  const int ntile = (n + EG_TILE - 1) / EG_TILE;
+  constexpr int KA = EG_TILE * NCMAX / 256;   // input-row values per thread and tile
+  f4 rg[4];
+  float ra[KA];
+  auto fetch = [&](int tile) {
+    const int r0 = tile * EG_TILE;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f4{0.f, 0.f, 0.f, 0.f};
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-  if constexpr (V4) {
-    // software-pipelined: the next trip's GEMM_UNR row groups are in flight while this trip's MFMAs
-    // run (kslice is a multiple of 4 GEMM_UNR here, so only the grid's last wave has a ragged trip)
-    constexpr int S = 4 * GEMM_UNR;   // rows per trip
-    float4 g0[GEMM_UNR], a0[GEMM_UNR], g1[GEMM_UNR], a1[GEMM_UNR];   // ping-pong buffers: no copies
-    auto fetch = [&](float4 (&gb)[GEMM_UNR], float4 (&ab)[GEMM_UNR], long long k) {
-#pragma unroll
-      for (int u = 0; u < GEMM_UNR; ++u) {
-        // unconditional loads from a clamped row (a conditional load becomes a branch with a
-        // vmcnt(0) wait inside it); rows past k1 are zeroed at use
-        const long long row = k + 4 * u + kr, rc = row < k1 ? row : k1 - 1;
-        gb[u] = reinterpret_cast<const float4*>(G + rc * ldg)[il];
-        ab[u] = reinterpret_cast<const float4*>(A + rc * lda)[il];
-      }
-    };
-    auto compute = [&](const float4 (&gb)[GEMM_UNR], const float4 (&ab)[GEMM_UNR], long long k) {
-#pragma unroll
-      for (int u = 0; u < GEMM_UNR; ++u) {
-        const bool ok = k + 4 * u + kr < k1;
-        const float gv[4] = {ok ? gb[u].x : 0.f, ok ? gb[u].y : 0.f, ok ? gb[u].z : 0.f, ok ? gb[u].w : 0.f};
-        const float av[4] = {ok ? ab[u].x : 0.f, ok ? ab[u].y : 0.f, ok ? ab[u].z : 0.f, ok ? ab[u].w : 0.f};
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bsum[t] += gv[t];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[a], av[b], acc[a][b]);
-      }
-    };
-    // the next trip's rows are in flight while this trip's MFMAs run (kslice is a multiple of S
-    // here, so only the grid's last wave has a ragged trip)
-    // (fetches are unconditional, clamped rows past k1: a conditional fetch makes the wait counter
-    // merge at the join fall back to vmcnt(0))
-    if (k0 < k1) {
-      fetch(g0, a0, k0);
-      for (long long k = k0; k < k1; k += 2 * S) {
-        fetch(g1, a1, k + S);
-        compute(g0, a0, k);
-        fetch(g0, a0, k + 2 * S);
-        compute(g1, a1, k + S);
-      }
-    }
-  } else {
-  // GEMM_UNR groups of 4 rows per trip: every group's loads are issued before the first MFMA, so a
-  // wave (one per SIMD at the capped grid) keeps GEMM_UNR row groups of HBM latency in flight
-  for (long long k = k0; k < k1; k += 4 * GEMM_UNR) {
-    float gv[GEMM_UNR][4], av[GEMM_UNR][4];
-#pragma unroll
-    for (int u = 0; u < GEMM_UNR; ++u) {
-      const long long row = k + 4 * u + kr;
-      const bool ok = row < k1;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int cg = 16 * t + il;
-        gv[u][t] = (ok && cg < M) ? G[row * ldg + cg] : 0.f;
-        av[u][t] = (ok && cg < N) ? A[row * lda + cg] : 0.f;
-      }
+    for (int u = 0; u < 4; ++u) {   // gh0 rows: 64 x 16 float4
+      const int i = tid + 256 * u, rr = i >> 4;
+      rg[u] = r0 + rr < n ? reinterpret_cast<const f4*>(gh0 + (size_t)(r0 + rr) * 64)[i & 15]
+                          : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < GEMM_UNR; ++u) {
+    for (int u = 0; u < KA; ++u) {
+      const int i = tid + 256 * u, rr = i / NCMAX, k = i - rr * NCMAX;
+      const int r = r0 + rr;
+      float val = 0.f;
+      if (r < n && k < ld) {
+        const int t = r / BN, c = r - t * BN;
+        val = k < din ? hin[(size_t)(frames ? r : c) * din + k] : trig[((size_t)(c % Bt) * T + t) * ncol + (k - din)];
+      }
+      ra[u] = val;
+    }
+  };
+  auto put = [&]() {
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bsum[t] += gv[u][t];
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + 256 * u, rr = i >> 4, c4 = 4 * (i & 15);
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int j = 0; j < 4; ++j) sG[rr][c4 + j] = rg[u][j];
+    }
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = mfma(gv[u][a], av[u][b], acc[a][b]);
+    for (int u = 0; u < KA; ++u) {
+      const int i = tid + 256 * u;
+      sA[i / NCMAX][i % NCMAX] = ra[u];
+    }
+  };
+  float acc[NCMAX], bsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCMAX; ++k) acc[k] = 0.f;
+  int tile = blockIdx.x;
+  if (tile < ntile) fetch(tile);
+  for (; tile < ntile; tile += gridDim.x) {
+    __syncthreads();   // the previous tile's sums have read the LDS rows
+    put();
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntile) fetch(tile + gridDim.x);
+#pragma unroll 2
+    for (int rr = 16 * q; rr < 16 * q + 16; ++rr) {
+      const float gv = sG[rr][o];
+      bsum += gv;
+#pragma unroll
+      for (int k4 = 0; k4 < NCMAX / 4; ++k4) {
+        const f4 a = *reinterpret_cast<const f4*>(&sA[rr][4 * k4]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 * k4 + j] = fmaf(gv, a[j], acc[4 * k4 + j]);
+      }
     }
   }
-  }
-  // the block's four wave partials are added through LDS in wave order: one partial per block
-  __shared__ float red[4][64 * 65];
-  const int NO = M * (N + 1);
-  const int wv = threadIdx.x >> 6;
-  float* out = red[wv];
+  // one partial per block (column blocks of <= 64 inputs, the bias after block 0's columns), the four
+  // row quarters added in order, 32 columns at a time through LDS
+  const int nc0 = ld < 64 ? ld : 64;
+  const size_t base1 = (size_t)gridDim.x * 64 * (nc0 + 1);
+  auto out_at = [&](int oo, int k) -> float* {   // k == ld: the bias
+    if (k == ld) return part + ((size_t)blockIdx.x * 64 + oo) * (nc0 + 1) + nc0;
+    if (k < 64) return part + ((size_t)blockIdx.x * 64 + oo) * (nc0 + 1) + k;
+    return part + base1 + ((size_t)blockIdx.x * 64 + oo) * (ld - 64 + 1) + (k - 64);
+  };
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
+  for (int c0 = 0; c0 < NCMAX; c0 += 32) {
+    __syncthreads();
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        // accumulator: C[4(l>>4)+q][l&15]; V4 index 16 t + r is channel 4 r + t
-        const int i = V4 ? 4 * (4 * kr + q) + a : 16 * a + 4 * kr + q, jj = V4 ? 4 * il + b : 16 * b + il;
-        if (i < M && jj < N) out[i * (N + 1) + jj] = acc[a][b][q];
+    for (int k = 0; k < 32; ++k) sR[q][o][k] = c0 + k < NCMAX ? acc[c0 + k] : 0.f;
+    sR[q][o][32] = bsum;
+    __syncthreads();
+    const int kn = min(32, ld - c0);
+    for (int i = tid; i < 64 * 33; i += 256) {
+      const int oo = i / 33, k = i - oo * 33;
+      if (k < kn || (k == 32 && c0 == 0)) {
+        const float v = ((sR[0][oo][k] + sR[1][oo][k]) + sR[2][oo][k]) + sR[3][oo][k];
+        *out_at(oo, k == 32 ? ld : c0 + k) = v;
       }
-    const float bs = group_sum(bsum[a]);
-    const int ib = V4 ? 4 * il + a : 16 * a + il;
-    if (kr == 0 && ib < M) out[ib * (N + 1) + N] = bs;
+    }
   }
-  __syncthreads();
-  float* dst = partial + (size_t)blockIdx.x * NO;
-  for (int o = threadIdx.x; o < NO; o += 256) dst[o] = ((red[0][o] + red[1][o]) + red[2][o]) + red[3][o];
-}
-template <bool V4>
-__global__ __launch_bounds__(256) void gemm_tn_partial(const float* __restrict__ G, int ldg, int M,
-                                                       const float* __restrict__ A, int lda, int N, long long K,
-                                                       long long kslice, float* partial) {
-  gemm_tn_body<V4>(G, ldg, M, A, lda, N, K, kslice, partial);
 }
 
 // dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
@@ -1862,47 +1823,16 @@ __global__ __launch_bounds__(256) void tconv_wgrad_reduce(TconvReduceArgs a) {
 }
 
 
-struct Gemm {
-  float* partial;
-  int max_waves;
-  hipStream_t s;
-  // C[M][N] = sum_k G[k] (x) A[k] into dst (row stride ld, column (col0 + j) * cs; columns j >= split
-  // at col1 + j - split), bias[i] = sum_k G[k][i]; scale multiplies both
-  int operator()(const float* G, int ldg, int M, const float* A, int lda, int N, long long K, float* dst,
-                 int ld, int col0, float* bias, int accumulate = 0, int cs = 1, float scale = 1.f,
-                 int split = 1 << 30, int col1 = 0) const {
-    if (M > 64 || N > 64) return fail(NONODE_EINVAL, "gemm: M=%d N=%d", M, N);
-    if (K <= 0) return NONODE_OK;
-    long long waves = (K + 31) / 32;                   // >= 32 rows per wave
-    if (waves > max_waves) waves = max_waves;
-    const bool v4 = M == 64 && N == 64 && ldg % 4 == 0 && lda % 4 == 0 && ((uintptr_t)G & 15) == 0 &&
-                    ((uintptr_t)A & 15) == 0;
-    long long kslice = (K + waves - 1) / waves;
-    kslice = v4 ? (kslice + 4 * GEMM_UNR - 1) / (4 * GEMM_UNR) * (4 * GEMM_UNR) : (kslice + 3) & ~3LL;
-    waves = (K + kslice - 1) / kslice;
-    const int nblk = (int)((waves + 3) / 4);
-    const int nparts = nblk;   // one partial per block
-    const int NO = M * (N + 1);
-    if (v4)
-      hipLaunchKernelGGL(gemm_tn_partial<true>, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice,
-                         partial);
-    else
-      hipLaunchKernelGGL(gemm_tn_partial<false>, dim3(nblk), dim3(256), 0, s, G, ldg, M, A, lda, N, K, kslice,
-                         partial);
-    if (int rc = check_launch("gemm_tn_partial")) return rc;
-    hipLaunchKernelGGL(gemm_reduce, dim3((NO + 15) / 16), dim3(256), 0, s, partial, nparts, M, N, dst, ld, col0,
-                       cs, bias, accumulate, scale, split, col1, (long long)NO);
-    return check_launch("gemm_reduce");
-  }
-};
-
 // ---- state layout of the training forward ---------------------------------------------------------
 struct TrainState {
   unsigned long long* mask;   // L x T x ntiles x 16: TimeConv LeakyReLU decisions (TconvArgs::mask_out)
   float *hs, *xs, *vs;        // (L+1) x n x {64, 3, 3}: inputs of each layer's TimeConv (hs[0] = h0)
   float *he, *xe, *ve;        // L x n x {64, 3, 3}: TimeConv outputs = EGNN inputs
   float *Ms, *Fs;             // L x n x {64, 4}: message / force sums of each EGNN layer
-  float *emb_in;              // n x (in_node + temb): embedding Linear inputs
+  // embedding Linear inputs for its weight gradient (emb_grad_kernel): h_in rows (BN, or n with per-frame
+  // inputs) x in_node, then the time-embedding table [Bt][T][temb] (temb_kernel's trig values); the
+  // region is sized n x (in_node + temb), which holds both for any Bt dividing B N
+  float *ein;
   size_t floats;
 };
 TrainState train_state(void* base, int B, int N, int T, int L, int in_node, int temb) {
@@ -1915,7 +1845,7 @@ TrainState train_state(void* base, int B, int N, int T, int L, int in_node, int 
   st.hs = take((L + 1) * n * 64); st.xs = take((L + 1) * n * 3); st.vs = take((L + 1) * n * 3);
   st.he = take(L * n * 64); st.xe = take(L * n * 3); st.ve = take(L * n * 3);
   st.Ms = take(L * n * 64); st.Fs = take(L * n * 4);
-  st.emb_in = take(n * (in_node + temb));
+  st.ein = take(n * (in_node + temb));
   st.floats = (size_t)(2 * mask_words + (L + 1) * n * 70 + L * n * 70 + L * n * 68 + n * (in_node + temb));
   return st;
 }
@@ -1932,7 +1862,6 @@ struct BwdWs {
   float *partial;
   size_t floats;
 };
-constexpr int GEMM_MAX_WAVES = 1024;
 BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   const size_t BN = (size_t)B * N, n = BN * T;
   BwdWs w;
@@ -1951,8 +1880,9 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.twb = take((size_t)M * 2 * 4096);
   w.tpart = take((size_t)TB_MAX_BLOCKS * M * 2 * 4096);
   w.xpart = take((BN * 3 + TX_THREADS - 1) / TX_THREADS * (2 * 2 * MMAX_T * 2));   // one row per tconvx block
-  // gemm_tn_partial partials (one per block), or node_wgrad_kernel's (one [NW_JOBS][64][65] per block)
-  const size_t gparts = (size_t)(GEMM_MAX_WAVES / 4 + 1) * 64 * 65;
+  // node_wgrad_kernel's partials (one [NW_JOBS][64][65] per block), or emb_grad_kernel's (one
+  // [64][<= 137 + 2] per block: two column blocks)
+  const size_t gparts = (size_t)EG_MAX_BLOCKS * 64 * (8 + 2 * 64 + 2);
   const size_t nparts = (size_t)nonode_tu::NW_MAX_BLOCKS * nonode_tu::NW_JOBS * nonode_tu::NW_PART;
   w.partial = take(gparts > nparts ? gparts : nparts);
   w.floats = tot;
@@ -2059,17 +1989,15 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
   float* etab = (float*)workspace + n * 64 + n * 3;
   const int emb_ld = in_node + emb_cols;
   {
+    // temb_kernel also saves the raw time-embedding table and h0_kernel the h_in rows: the inputs of the
+    // embedding's weight gradient (emb_grad_kernel)
     const int tot = Bt * T * 64;
     hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim, t_out,
-                       emb_w, emb_ld, emb_b, etab, t_in);
+                       emb_w, emb_ld, emb_b, etab, t_in, st.ein + n * in_node);
     if (int rc = check_launch("temb_kernel")) return rc;
-    hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
-                       etab, x, v, st.hs, st.xs, st.vs, frames);
+    hipLaunchKernelGGL(h0_kernel, dim3((unsigned)(((size_t)T * BN * 64 + 255) / 256)), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
+                       etab, x, v, st.hs, st.xs, st.vs, frames, st.ein);
     if (int rc = check_launch("h0_kernel")) return rc;
-    const size_t tot2 = n * emb_ld;
-    hipLaunchKernelGGL(emb_in_kernel, dim3((unsigned)((tot2 + 255) / 256)), dim3(256), 0, s, BN, T, in_node,
-                       time_emb_dim, Bt, h, t_out, st.emb_in, t_in, frames);
-    if (int rc = check_launch("emb_in_kernel")) return rc;
   }
   // EGNN_Layer leaves v unchanged (basic.py:186): layer l's input v is TimeConv_x's output ve[l - 1]
   // (vs[0] without time convolutions); the last layer writes x_out, h_out directly
@@ -2291,7 +2219,6 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
   const long long E = (long long)n * (N - 1);
   TrainState st = train_state(const_cast<void*>(state), B, N, T, L, in_node, emb_cols);
   BwdWs w = bwd_ws(workspace, B, N, T, M);
-  Gemm gemm{w.partial, GEMM_MAX_WAVES, s};
   // grads of the final outputs
   // (read in place: the reverse pass only reads the output gradients of a layer)
   const float *gx = g_x, *gv = g_v, *gh = g_h;
@@ -2334,13 +2261,29 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
     gx = w.gx[cur]; gv = w.gv[cur]; gh = w.gh[cur];
   }
   // ---- embedding Linear (egno.py:63-76): dW = sum_rows gh0 (x) [h_in, temb], db = sum gh0 ----
-  const int emb_ld = in_node + emb_cols;
-  // (in column blocks of <= 64: the multi-input embedding has in_node + 2 time_emb_dim inputs)
-  for (int c0 = 0; c0 < emb_ld; c0 += 64) {
-    const int nc = emb_ld - c0 < 64 ? emb_ld - c0 : 64;
-    if (int rc = gemm(gh, 64, 64, st.emb_in + c0, emb_ld, nc, (long long)n, g_emb_w, emb_ld, c0,
-                      c0 == 0 ? g_emb_b : nullptr))
-      return rc;
+  {
+    const int emb_ld = in_node + emb_cols;
+    if (n >= (size_t)1 << 31) return fail(NONODE_EUNSUPPORTED, "egno_backward: %zu embedding rows", n);
+    const long long ntile = ((long long)n + EG_TILE - 1) / EG_TILE;
+    const int nblk = (int)(ntile < EG_MAX_BLOCKS ? ntile : EG_MAX_BLOCKS);
+    const float* hin_s = st.ein;
+    const float* trig_s = st.ein + n * in_node;
+    if (emb_ld <= 40)
+      hipLaunchKernelGGL(emb_grad_kernel<40>, dim3(nblk), dim3(256), 0, s, BN, T, Bt, in_node, emb_cols, frames, gh,
+                         hin_s, trig_s, w.partial);
+    else
+      hipLaunchKernelGGL(emb_grad_kernel<136>, dim3(nblk), dim3(256), 0, s, BN, T, Bt, in_node, emb_cols, frames, gh,
+                         hin_s, trig_s, w.partial);
+    if (int rc = check_launch("emb_grad_kernel")) return rc;
+    const int nc0 = emb_ld < 64 ? emb_ld : 64;
+    ReduceJob jobs[2];
+    jobs[0] = ReduceJob{w.partial, nblk, 64, nc0, g_emb_w, emb_ld, 0, 1, g_emb_b, 0, 1.f, 1 << 30, 0,
+                        (long long)64 * (nc0 + 1)};
+    int nj = 1;
+    if (emb_ld > 64)
+      jobs[nj++] = ReduceJob{w.partial + (size_t)nblk * 64 * (nc0 + 1), nblk, 64, emb_ld - 64, g_emb_w, emb_ld, 64, 1,
+                             nullptr, 0, 1.f, 1 << 30, 0, (long long)64 * (emb_ld - 64 + 1)};
+    if (int rc = launch_reduce_batch(jobs, nj, s)) return rc;
   }
   return NONODE_OK;
 }

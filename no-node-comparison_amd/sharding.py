@@ -77,7 +77,7 @@ class FlatGrads:
     Every parameter's .grad is a view into one contiguous buffer (fp32 for the models), so autograd accumulates
     straight into it and the step needs a single all-reduce (sum) of the flat buffer (0.81 MB
     for EGNO) followed by a division by the world size: with equal shards this is the gradient of
-    the global mean loss. With world size 1 (or no process group) it is a no-op."""
+    the global mean loss. With world size 1 (or no process group) allreduce_ is a no-op."""
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
@@ -134,7 +134,10 @@ class FlatGrads:
         return self.flat
 
     def allreduce_(self):
-        self.gather_()
+        """The step's exchange. With world size 1 (or no process group) there is nothing to reduce,
+        so the parameters keep autograd's gradient tensors as they are (no gather into the buffer)
+        and None is returned; otherwise the reduced flat buffer."""
         if not _initialized() or dist.get_world_size() == 1:
-            return self.flat
+            return None
+        self.gather_()
         return self.exchange_()
