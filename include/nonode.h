@@ -316,6 +316,20 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
                           float* g_x_in, float* g_v_in, void* workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * The embedding Linear of SEGNO (SEGNO/models/model.py:73, h = embedding(his), 64 outputs) as a
+ * forward / backward pair, for a training caller that keeps it off the autograd tape:
+ * nonode_embedding_forward: out[n][o] = bias[o] + sum_k weight[o][k] in[n][k] (in_features <= 40);
+ * nonode_embedding_backward: grad_weight [64][in_features] = sum_n grad_out[n] (x) in[n], grad_bias =
+ * sum_n grad_out[n] (written; a fixed summation order: deterministic).
+ */
+int nonode_embedding_forward(int n_rows, int in_features, const float* in, const float* weight, const float* bias,
+                             float* out, void* stream);
+size_t nonode_embedding_backward_workspace_bytes(int n_rows, int in_features);
+int nonode_embedding_backward(int n_rows, int in_features, const float* in, const float* grad_out,
+                              float* grad_weight, float* grad_bias, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
+/*
  * Layer-granular reverse passes (SURVEY §8(b) egno_layer_bwd / spectral_tconv_bwd): autograd of ONE
  * EGNN_Layer or ONE TimeConv + TimeConv_x given that block's inputs and the gradients of its outputs,
  * for a caller that differentiates the blocks separately. Each recomputes what it needs of its forward

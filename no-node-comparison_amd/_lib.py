@@ -5,6 +5,7 @@ no CPU fallback: if the library is missing or the tensors are not on a ROCm devi
 """
 import ctypes
 import os
+import weakref
 
 import torch  # load torch's HIP runtime first so libnonode.so binds to the same libamdhip64
 
@@ -30,6 +31,7 @@ SYMBOLS = (
     "nonode_egnn_layer_bwd_workspace_bytes", "nonode_egnn_layer_bwd",
     "nonode_egno_tconv_bwd_workspace_bytes", "nonode_egno_tconv_bwd",
     "nonode_pack_layers", "nonode_pack_layers_bwd", "nonode_pack_tconvs",
+    "nonode_embedding_forward", "nonode_embedding_backward_workspace_bytes", "nonode_embedding_backward",
 )
 
 VARIANT_EGNO = 0
@@ -63,6 +65,28 @@ class LayerGrads(ctypes.Structure):
 
 
 _lib = None
+_packed_modules = weakref.WeakSet()
+_step_hook = None
+
+
+def track_packs(module):
+    """Register a module whose packed weight blobs are cached under its parameters' tensor versions
+    (EGNO._packed, SEGNO._packed, ...). torch's fused optimizers (Adam(fused=True) and the like)
+    update parameters in place WITHOUT bumping those versions, so the key alone would keep stale
+    blobs after such a step: a global optimizer step post-hook drops the packs of every tracked
+    module that shares a parameter with the optimizer that stepped. module._drop_packs() does it."""
+    global _step_hook
+    _packed_modules.add(module)
+    if _step_hook is None:
+        import torch.optim.optimizer as topt
+        _step_hook = topt.register_optimizer_step_post_hook(_after_optimizer_step)
+
+
+def _after_optimizer_step(optimizer, args, kwargs):
+    ids = {id(p) for g in optimizer.param_groups for p in g["params"]}
+    for m in list(_packed_modules):
+        if any(id(p) in ids for p in m.parameters()):
+            m._drop_packs()
 
 
 def lib():
@@ -124,6 +148,10 @@ def lib():
     L.nonode_segno_backward_workspace_bytes.restype = _sz
     L.nonode_segno_backward.argtypes = ([_i] * 4 + [_f, _i] + [_vp] * 6 + [ctypes.POINTER(LayerGrads)]
                                         + [_vp] * 4 + [_sz, _vp])
+    L.nonode_embedding_forward.argtypes = [_i, _i] + [_vp] * 5
+    L.nonode_embedding_backward_workspace_bytes.argtypes = [_i, _i]
+    L.nonode_embedding_backward_workspace_bytes.restype = _sz
+    L.nonode_embedding_backward.argtypes = [_i, _i] + [_vp] * 5 + [_sz, _vp]
     L.nonode_egnn_layer_bwd_workspace_bytes.argtypes = [_i, _i]
     L.nonode_egnn_layer_bwd_workspace_bytes.restype = _sz
     L.nonode_egnn_layer_bwd.argtypes = ([_i] * 5 + [_vp] * 9 + [ctypes.POINTER(LayerGrads)] + [_vp] * 4

@@ -117,60 +117,74 @@ def egno_forward_train(model, x, h, edge_fea, v, loc_mean, t_out, B, N, t_in=Non
     return EGNOTrain.apply(model, x, h, edge_fea, v, loc_mean, t_out, t_in, B, N, *params)
 
 
+def _segno_forward(ctx, model, h, x, v, edge_attr, T, B, N):
+    """nonode_segno_forward_train from an embedded h (f32, contiguous): (x, h, v) after T substeps;
+    ctx keeps the saved state for _segno_backward."""
+    L = _lib.lib()
+    dev = x.device
+    x, v, ea = _f32(x), _f32(v), _f32(edge_attr)
+    blob = model._packed()
+    n = B * N
+    x_out = torch.empty(n, 3, device=dev)
+    v_out = torch.empty(n, 3, device=dev)
+    h_out = torch.empty(n, model.hidden_nf, device=dev)
+    st_bytes = L.nonode_segno_train_state_bytes(B, N, T)
+    state = torch.empty((st_bytes + 3) // 4, dtype=torch.float32, device=dev)
+    _lib.check(L.nonode_segno_forward_train(B, N, T, model.in_edge_nf, _lib.ptr(h), _lib.ptr(x), _lib.ptr(v),
+                                            _lib.ptr(ea), _lib.ptr(blob), float(model.coords_weight),
+                                            int(bool(model.recurrent)), _lib.ptr(x_out), _lib.ptr(v_out),
+                                            _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.stream_of(x)))
+    ctx.model, ctx.T, ctx.B, ctx.N = model, T, B, N
+    ctx.state, ctx.ea = state, ea
+    ctx.set_materialize_grads(False)   # unused outputs: None, zeroed by the library (see EGNOTrain)
+    return x_out, h_out, v_out
+
+
+def _segno_backward(ctx, gx, gh, gv, want_h, want_x, want_v):
+    """nonode_segno_backward: ({GCL parameter name: gradient}, g_h, g_x, g_v) with each input gradient
+    None unless wanted (the library writes only the requested ones)."""
+    model, T, B, N = ctx.model, ctx.T, ctx.B, ctx.N
+    L = _lib.lib()
+    dev = ctx.state.device
+    n = B * N
+    bblob = model._packed_bwd()
+    names = model.gcl_param_names()
+    named = dict(model.named_parameters())
+    grads = {nm: torch.empty_like(named[nm]) for nm in names if nm is not None}
+    lg = _lib.LayerGrads(*[grads[nm].data_ptr() if nm is not None else None for nm in names])
+    ws_bytes = L.nonode_segno_backward_workspace_bytes(B, N)
+    ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
+    gx = _f32(gx) if gx is not None else None
+    gv = _f32(gv) if gv is not None else None
+    gh = _f32(gh) if gh is not None else None
+    g_h = torch.empty(n, model.hidden_nf, device=dev) if want_h else None
+    g_x = torch.empty(n, 3, device=dev) if want_x else None
+    g_v = torch.empty(n, 3, device=dev) if want_v else None
+    _lib.check(L.nonode_segno_backward(B, N, T, model.in_edge_nf, float(model.coords_weight),
+                                       int(bool(model.recurrent)), _lib.ptr(ctx.ea), _lib.ptr(bblob),
+                                       _lib.ptr(ctx.state), _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh),
+                                       ctypes.byref(lg), _lib.ptr(g_h), _lib.ptr(g_x), _lib.ptr(g_v),
+                                       _lib.ptr(ws), ws_bytes, _lib.stream_of(ws)))
+    ctx.state = None
+    return grads, g_h, g_x, g_v
+
+
 class SEGNOStepTrain(torch.autograd.Function):
     """SEGNO.forward_step (SEGNO/models/model.py:95-102) on the autograd tape: T substeps of
-    SEGNO_GCL (gcl.py:111-119) from an embedded h. Forward: nonode_segno_forward_train (the inference
-    kernels, one launch per substep, saving each substep's state); backward: nonode_segno_backward
-    (gradients of the shared GCL weights and of h, x, v)."""
+    SEGNO_GCL (gcl.py:111-119) from an embedded h. Forward: nonode_segno_forward_train (one launch
+    for the T substeps, saving each substep's state); backward: nonode_segno_backward (gradients of
+    the shared GCL weights and of h, x, v)."""
 
     @staticmethod
     def forward(ctx, model, h, x, v, edge_attr, T, B, N, *params):
-        L = _lib.lib()
-        dev = x.device
-        h, x, v, ea = _f32(h), _f32(x), _f32(v), _f32(edge_attr)
-        blob = model._packed()
-        n = B * N
-        x_out = torch.empty(n, 3, device=dev)
-        v_out = torch.empty(n, 3, device=dev)
-        h_out = torch.empty(n, model.hidden_nf, device=dev)
-        st_bytes = L.nonode_segno_train_state_bytes(B, N, T)
-        state = torch.empty((st_bytes + 3) // 4, dtype=torch.float32, device=dev)
-        _lib.check(L.nonode_segno_forward_train(B, N, T, model.in_edge_nf, _lib.ptr(h), _lib.ptr(x), _lib.ptr(v),
-                                                _lib.ptr(ea), _lib.ptr(blob), float(model.coords_weight),
-                                                int(bool(model.recurrent)), _lib.ptr(x_out), _lib.ptr(v_out),
-                                                _lib.ptr(h_out), _lib.ptr(state), st_bytes, _lib.stream_of(x)))
-        ctx.model, ctx.T, ctx.B, ctx.N = model, T, B, N
-        ctx.state, ctx.ea = state, ea
-        ctx.set_materialize_grads(False)   # unused outputs: None, zeroed by the library (see EGNOTrain)
         ctx.save_for_backward(*params)   # version check of the parameters (see EGNOTrain.forward)
-        return x_out, h_out, v_out
+        return _segno_forward(ctx, model, _f32(h), x, v, edge_attr, T, B, N)
 
     @staticmethod
     def backward(ctx, gx, gh, gv):
-        model, T, B, N = ctx.model, ctx.T, ctx.B, ctx.N
+        model = ctx.model
         _ = ctx.saved_tensors   # raises if a parameter changed in place since the forward
-        L = _lib.lib()
-        dev = ctx.state.device
-        n = B * N
-        bblob = model._packed_bwd()
-        names = model.gcl_param_names()
-        named = dict(model.named_parameters())
-        grads = {nm: torch.empty_like(named[nm]) for nm in names if nm is not None}
-        lg = _lib.LayerGrads(*[grads[nm].data_ptr() if nm is not None else None for nm in names])
-        ws_bytes = L.nonode_segno_backward_workspace_bytes(B, N)
-        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
-        gx = _f32(gx) if gx is not None else None
-        gv = _f32(gv) if gv is not None else None
-        gh = _f32(gh) if gh is not None else None
-        g_h = torch.empty(n, model.hidden_nf, device=dev)
-        g_x = torch.empty(n, 3, device=dev)
-        g_v = torch.empty(n, 3, device=dev)
-        _lib.check(L.nonode_segno_backward(B, N, T, model.in_edge_nf, float(model.coords_weight),
-                                           int(bool(model.recurrent)), _lib.ptr(ctx.ea), _lib.ptr(bblob),
-                                           _lib.ptr(ctx.state), _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh),
-                                           ctypes.byref(lg), _lib.ptr(g_h), _lib.ptr(g_x), _lib.ptr(g_v),
-                                           _lib.ptr(ws), ws_bytes, _lib.stream_of(g_h)))
-        ctx.state = None
+        grads, g_h, g_x, g_v = _segno_backward(ctx, gx, gh, gv, *ctx.needs_input_grad[1:4])
         out = [grads.get(nm) for nm, _ in model.module.named_parameters(prefix="module")]
         return (None, g_h, g_x, g_v, None, None, None, None) + tuple(out)
 
@@ -179,3 +193,45 @@ def segno_step_train(model, h, x, v, edge_attr, T, B, N):
     """forward_step that records the kernels' backward on the autograd tape."""
     params = [p for _, p in model.module.named_parameters()]
     return SEGNOStepTrain.apply(model, h, x, v, edge_attr, T, B, N, *params)
+
+
+class SEGNOTrain(torch.autograd.Function):
+    """SEGNO.forward in training with one input (SEGNO/models/model.py:53-102, train_nbody.py:168): the
+    embedding Linear (model.py:73) and forward_step's T substeps as ONE node of the tape. The
+    embedding runs as nonode_embedding_forward and its weight gradient as nonode_embedding_backward
+    from the g_h the reverse pass returns, instead of broadcast torch ops and their autograd reverse."""
+
+    @staticmethod
+    def forward(ctx, model, his, x, v, edge_attr, T, B, N, *params):
+        L = _lib.lib()
+        his = _f32(his)
+        h = torch.empty(B * N, model.hidden_nf, device=x.device)
+        ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
+        _lib.check(L.nonode_embedding_forward(B * N, his.shape[1], _lib.ptr(his), _lib.ptr(ew), _lib.ptr(eb),
+                                              _lib.ptr(h), _lib.stream_of(his)))
+        ctx.save_for_backward(*params)
+        ctx.his = his
+        return _segno_forward(ctx, model, h, x, v, edge_attr, T, B, N)
+
+    @staticmethod
+    def backward(ctx, gx, gh, gv):
+        model = ctx.model
+        _ = ctx.saved_tensors
+        grads, g_h, g_x, g_v = _segno_backward(ctx, gx, gh, gv, True, *ctx.needs_input_grad[2:4])
+        L = _lib.lib()
+        n, din = ctx.his.shape
+        gw = torch.empty_like(model.embedding.weight)
+        gb = torch.empty_like(model.embedding.bias)
+        ws_bytes = L.nonode_embedding_backward_workspace_bytes(n, din)
+        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=g_h.device)
+        _lib.check(L.nonode_embedding_backward(n, din, _lib.ptr(ctx.his), _lib.ptr(g_h), _lib.ptr(gw), _lib.ptr(gb),
+                                               _lib.ptr(ws), ws_bytes, _lib.stream_of(g_h)))
+        ctx.his = None
+        out = [grads.get(nm) for nm, _ in model.module.named_parameters(prefix="module")]
+        return (None, None, g_x, g_v, None, None, None, None, gw, gb) + tuple(out)
+
+
+def segno_train(model, his, x, v, edge_attr, T, B, N):
+    """SEGNO.forward (one input, training): embedding + T substeps on the autograd tape."""
+    params = [model.embedding.weight, model.embedding.bias] + [p for _, p in model.module.named_parameters()]
+    return SEGNOTrain.apply(model, his, x, v, edge_attr, T, B, N, *params)

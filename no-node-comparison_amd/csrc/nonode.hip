@@ -1435,22 +1435,36 @@ __global__ void embed_kernel(int n_nodes, int din, const float* in, const float*
 // tconv_kernel<true>), and x, v replicated over T (egno.py:89-96)
 // frames = 1 (num_inputs > 1): h_in, x, v are per frame ([T*BN] rows) instead of replicated;
 // hin_out (training forward, else null): a copy of the h_in rows (the embedding's inputs)
-__global__ void h0_kernel(int BN, int T, int din, int Bt, const float* hin, const float* emb_w, int emb_ld,
-                          const float* etab, const float* x, const float* v, float* h0, float* xr, float* vr,
-                          int frames, float* hin_out = nullptr) {
-  // one thread per output (row, o): every store of the launch is independent (one coalesced 256-byte
-  // row per 64 threads), so the whole [T*BN][64] table streams at full occupancy
-  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long long)T * BN * 64) return;
-  const int o = (int)(idx & 63);
-  const int row = (int)(idx >> 6);   // (n rows of 256 B: n < 2^31 for any table that fits in HBM)
-  const int t = row / BN, c = row - t * BN;
-  const size_t src = frames ? (size_t)row : (size_t)c;
-  float b = 0.f;
-  for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[src * din + k], b);
-  h0[(size_t)row * 64 + o] = etab[((size_t)(c % Bt) * T + t) * 64 + o] + b;
-  if (o < 3) { xr[(size_t)row * 3 + o] = x[src * 3 + o]; vr[(size_t)row * 3 + o] = v[src * 3 + o]; }
-  if (hin_out && o < din && (frames || t == 0)) hin_out[src * din + o] = hin[src * din + o];
+__global__ __launch_bounds__(256) void h0_kernel(int BN, int T, int din, int Bt, const float* __restrict__ hin,
+                                                 const float* __restrict__ emb_w, int emb_ld,
+                                                 const float* __restrict__ etab, const float* __restrict__ x,
+                                                 const float* __restrict__ v, float* __restrict__ h0,
+                                                 float* __restrict__ xr, float* __restrict__ vr, int frames,
+                                                 float* __restrict__ hin_out = nullptr) {
+  // thread (c, o) writes column o of node c's T rows; its T table reads are all issued before the
+  // stores (restrict: no aliasing), so one memory latency per thread instead of T
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= BN * 64) return;
+  const int o = idx & 63, c = idx >> 6;
+  auto hin_part = [&](size_t r) {
+    float b = 0.f;
+    for (int k = 0; k < din; ++k) b = fmaf(emb_w[o * emb_ld + k], hin[r * din + k], b);
+    return b;
+  };
+  const float base = frames ? 0.f : hin_part((size_t)c);
+  const float* et = etab + (size_t)(c % Bt) * T * 64 + o;
+  float e[TMAX];
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) e[t] = t < T ? et[t * 64] : 0.f;
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    if (t >= T) break;
+    const size_t row = (size_t)t * BN + c;
+    const size_t src = frames ? row : (size_t)c;
+    h0[row * 64 + o] = e[t] + (frames ? hin_part(row) : base);
+    if (o < 3) { xr[row * 3 + o] = x[src * 3 + o]; vr[row * 3 + o] = v[src * 3 + o]; }
+    if (hin_out && o < din && (frames || t == 0)) hin_out[src * din + o] = hin[src * din + o];
+  }
 }
 
 // ---- host-side launchers ----------------------------------------------------------------------
@@ -1788,7 +1802,7 @@ int egno_forward_impl(int frames, int flat, int B, int N, int T, int n_layers, i
     float* hb[2] = {h_out, hB};
     float* xb[2] = {x_out, xB};
     const int L = n_layers;
-    hipLaunchKernelGGL(h0_kernel, dim3((unsigned)(((size_t)T * BN * 64 + 255) / 256)), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
+    hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
                        etab, x, v, hb[L & 1], xb[L & 1], v_out, frames);
     if (int rc = check_launch("h0_kernel")) return rc;
     for (int l = 0; l < L; ++l) {

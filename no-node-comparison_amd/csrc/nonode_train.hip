@@ -1597,107 +1597,106 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
 // embedding's input row is in[r] = [h_in[frames ? r : c], trig[(c % Bt) T + t]]: the raw time embedding
 // of the row's sample and frame (layer_no.py:8-17), which temb_kernel writes into the saved state in the
 // training forward (h0_kernel saves h_in). The input rows themselves are never materialised.
-// A block walks 64-row tiles (grid-stride, the next tile's rows requested before this tile's sums):
-// gh0 rows and input rows staged in LDS, thread (o, q) adds rows 16 q .. 16 q + 15 of the tile into
-// column o (the input row is an LDS broadcast). The four row quarters are added in order and one
-// partial per block is written in gemm_reduce's layout: column block cb (input columns 64 cb ..) is
-// [blocks][64][nc_cb + 1], block 0's column nc_0 = the bias. gemm_reduce_batch adds them in block order.
-constexpr int EG_TILE = 64;
-constexpr int EG_MAX_BLOCKS = 512;
-template <int NCMAX>   // in_node + time-embedding columns: <= 40 or <= 136 (in_node <= 8, 2 x 64)
+// A block takes eg_tpb (>= 1) consecutive 64-row tiles: gh0 rows and input rows (zero past column ld) staged in
+// LDS; thread (o, kg) sums column o of the gradient against the 4-column input blocks kg, kg + 4, ...
+// (LDS broadcasts), wave 0 the bias too, so no cross-wave sum is needed. One partial per block in
+// gemm_reduce's layout: column block cb (inputs 64 cb ..) is [blocks][64][nc_cb + 1], block 0's column
+// nc_0 = the bias; gemm_reduce_batch adds them in block order (deterministic).
+constexpr int EG_TILE = 64, EG_MAX_BLOCKS = 1024;
+// consecutive tiles per block: 1, or more once the rows need more than EG_MAX_BLOCKS blocks (C4: 2 tiles
+// in 800 blocks measured 27.8 us against 31.1 us for 1 tile in 1600 blocks; SEGNO's 160 tiles: 1 tile,
+// 7.0 against 11.3 us)
+inline int eg_tpb(long long rows) {
+  const long long ntile = (rows + EG_TILE - 1) / EG_TILE;
+  const long long t = (ntile + EG_MAX_BLOCKS - 1) / EG_MAX_BLOCKS;
+  return (int)(t > 1 ? t : 1);
+}
+inline int eg_blocks(long long rows) {
+  const long long ntile = (rows + EG_TILE - 1) / EG_TILE, t = eg_tpb(rows);
+  return (int)((ntile + t - 1) / t);
+}
+template <int NCMAX>   // in_node + time-embedding columns, padded to a multiple of 16: <= 48 or <= 144
 __global__ __launch_bounds__(256) void emb_grad_kernel(int BN, int T, int Bt, int din, int ncol, int frames,
                                                        const float* __restrict__ gh0, const float* __restrict__ hin,
-                                                       const float* __restrict__ trig, float* part) {
+                                                       const float* __restrict__ trig, float* __restrict__ part,
+                                                       int tpb) {
   __shared__ float sG[EG_TILE][65];
-  __shared__ __attribute__((aligned(16))) float sA[EG_TILE][NCMAX];   // input rows, zero past column ld
-  __shared__ float sR[4][64][33];
-  const int tid = threadIdx.x, o = tid & 63, q = tid >> 6;
+  __shared__ __attribute__((aligned(16))) float sA[EG_TILE][NCMAX];
+  __shared__ int sRow[EG_TILE][2];   // per tile row: h_in row, time-embedding row (-1: past the rows)
+  const int tid = threadIdx.x, o = tid & 63, kg = tid >> 6;
   const int ld = din + ncol;
   const int n = BN * T;   // (the host checks n < 2^31)
-  const int ntile = (n + EG_TILE - 1) / EG_TILE;
-  constexpr int KA = EG_TILE * NCMAX / 256;   // input-row values per thread and tile
-  f4 rg[4];
-  float ra[KA];
-  auto fetch = [&](int tile) {
-    const int r0 = tile * EG_TILE;
+  constexpr int NB = NCMAX / 4, NBT = NB / 4;   // 4-column input blocks (NCMAX: a multiple of 16), per thread
+  static_assert(NCMAX % 16 == 0, "4 column blocks per thread group");
+  f4 acc[NBT];
+#pragma unroll
+  for (int j = 0; j < NBT; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  for (int it = 0; it < tpb; ++it) {
+    const int r0 = (blockIdx.x * tpb + it) * EG_TILE;
+    if (r0 >= n) break;   // (block-uniform)
+    __syncthreads();      // the previous tile's sums have read the LDS rows
+    if (tid < EG_TILE) {
+      const int r = r0 + tid;
+      const int t = r / BN, c = r - t * BN;
+      sRow[tid][0] = r < n ? (frames ? r : c) : -1;
+      sRow[tid][1] = (c % Bt) * T + t;
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {   // gh0 rows: 64 x 16 float4
       const int i = tid + 256 * u, rr = i >> 4;
-      rg[u] = r0 + rr < n ? reinterpret_cast<const f4*>(gh0 + (size_t)(r0 + rr) * 64)[i & 15]
-                          : f4{0.f, 0.f, 0.f, 0.f};
+      const f4 g4 = r0 + rr < n ? reinterpret_cast<const f4*>(gh0 + (size_t)(r0 + rr) * 64)[i & 15]
+                                : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sG[rr][4 * (i & 15) + q] = g4[q];
     }
-#pragma unroll
-    for (int u = 0; u < KA; ++u) {
-      const int i = tid + 256 * u, rr = i / NCMAX, k = i - rr * NCMAX;
-      const int r = r0 + rr;
-      float val = 0.f;
-      if (r < n && k < ld) {
-        const int t = r / BN, c = r - t * BN;
-        val = k < din ? hin[(size_t)(frames ? r : c) * din + k] : trig[((size_t)(c % Bt) * T + t) * ncol + (k - din)];
-      }
-      ra[u] = val;
-    }
-  };
-  auto put = [&]() {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = tid + 256 * u, rr = i >> 4, c4 = 4 * (i & 15);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) sG[rr][c4 + j] = rg[u][j];
-    }
-#pragma unroll
-    for (int u = 0; u < KA; ++u) {
-      const int i = tid + 256 * u;
-      sA[i / NCMAX][i % NCMAX] = ra[u];
-    }
-  };
-  float acc[NCMAX], bsum = 0.f;
-#pragma unroll
-  for (int k = 0; k < NCMAX; ++k) acc[k] = 0.f;
-  int tile = blockIdx.x;
-  if (tile < ntile) fetch(tile);
-  for (; tile < ntile; tile += gridDim.x) {
-    __syncthreads();   // the previous tile's sums have read the LDS rows
-    put();
     __syncthreads();
-    if (tile + (int)gridDim.x < ntile) fetch(tile + gridDim.x);
-#pragma unroll 2
-    for (int rr = 16 * q; rr < 16 * q + 16; ++rr) {
+    // input rows: thread (rr = tid / 4, kq = tid % 4) stages columns kq, kq + 4, ... of tile row rr, every
+    // address first (a valid one for padding and rows past the range), then all loads, then the stores
+    {
+      constexpr int KE = NCMAX / 4;
+      const int rr = tid >> 2, kq = tid & 3;
+      const int hr = sRow[rr][0], tr = sRow[rr][1];
+      const float* hrow = hin + (size_t)(hr >= 0 ? hr : 0) * din;
+      const float* trow = trig + (size_t)tr * ncol - din;   // column k >= din of the row is trow[k]
+      float val[KE];
+#pragma unroll
+      for (int u = 0; u < KE; ++u) {
+        const int k = kq + 4 * u;
+        const bool live = hr >= 0 && k < ld;
+        val[u] = live ? (k < din ? hrow[k] : trow[k]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < KE; ++u) sA[rr][kq + 4 * u] = val[u];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int rr = 0; rr < EG_TILE; ++rr) {
       const float gv = sG[rr][o];
       bsum += gv;
 #pragma unroll
-      for (int k4 = 0; k4 < NCMAX / 4; ++k4) {
-        const f4 a = *reinterpret_cast<const f4*>(&sA[rr][4 * k4]);
+      for (int j = 0; j < NBT; ++j) {
+        const f4 a = *reinterpret_cast<const f4*>(&sA[rr][4 * (kg + 4 * j)]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[4 * k4 + j] = fmaf(gv, a[j], acc[4 * k4 + j]);
+        for (int q = 0; q < 4; ++q) acc[j][q] = fmaf(gv, a[q], acc[j][q]);
       }
     }
   }
-  // one partial per block (column blocks of <= 64 inputs, the bias after block 0's columns), the four
-  // row quarters added in order, 32 columns at a time through LDS
   const int nc0 = ld < 64 ? ld : 64;
   const size_t base1 = (size_t)gridDim.x * 64 * (nc0 + 1);
-  auto out_at = [&](int oo, int k) -> float* {   // k == ld: the bias
-    if (k == ld) return part + ((size_t)blockIdx.x * 64 + oo) * (nc0 + 1) + nc0;
-    if (k < 64) return part + ((size_t)blockIdx.x * 64 + oo) * (nc0 + 1) + k;
-    return part + base1 + ((size_t)blockIdx.x * 64 + oo) * (ld - 64 + 1) + (k - 64);
+  auto out_at = [&](int k) -> float* {   // k == ld: the bias
+    if (k == ld) return part + ((size_t)blockIdx.x * 64 + o) * (nc0 + 1) + nc0;
+    if (k < 64) return part + ((size_t)blockIdx.x * 64 + o) * (nc0 + 1) + k;
+    return part + base1 + ((size_t)blockIdx.x * 64 + o) * (ld - 64 + 1) + (k - 64);
   };
 #pragma unroll
-  for (int c0 = 0; c0 < NCMAX; c0 += 32) {
-    __syncthreads();
+  for (int j = 0; j < NBT; ++j)
 #pragma unroll
-    for (int k = 0; k < 32; ++k) sR[q][o][k] = c0 + k < NCMAX ? acc[c0 + k] : 0.f;
-    sR[q][o][32] = bsum;
-    __syncthreads();
-    const int kn = min(32, ld - c0);
-    for (int i = tid; i < 64 * 33; i += 256) {
-      const int oo = i / 33, k = i - oo * 33;
-      if (k < kn || (k == 32 && c0 == 0)) {
-        const float v = ((sR[0][oo][k] + sR[1][oo][k]) + sR[2][oo][k]) + sR[3][oo][k];
-        *out_at(oo, k == 32 ? ld : c0 + k) = v;
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int k = 4 * (kg + 4 * j) + q;
+      if (k < ld) *out_at(k) = acc[j][q];
     }
-  }
+  if (kg == 0) *out_at(ld) = bsum;
 }
 
 // dst[i*ld + (col0 + j)*cs] (+)= scale * sum_b partial[b][i][j], bias[i] (+)= scale * sum_b
@@ -1882,7 +1881,7 @@ BwdWs bwd_ws(void* base, int B, int N, int T, int M) {
   w.xpart = take((BN * 3 + TX_THREADS - 1) / TX_THREADS * (2 * 2 * MMAX_T * 2));   // one row per tconvx block
   // node_wgrad_kernel's partials (one [NW_JOBS][64][65] per block), or emb_grad_kernel's (one
   // [64][<= 137 + 2] per block: two column blocks)
-  const size_t gparts = (size_t)EG_MAX_BLOCKS * 64 * (8 + 2 * 64 + 2);
+  const size_t gparts = (size_t)eg_blocks((long long)n) * 64 * (8 + 2 * 64 + 2);
   const size_t nparts = (size_t)nonode_tu::NW_MAX_BLOCKS * nonode_tu::NW_JOBS * nonode_tu::NW_PART;
   w.partial = take(gparts > nparts ? gparts : nparts);
   w.floats = tot;
@@ -1995,7 +1994,7 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
     hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim, t_out,
                        emb_w, emb_ld, emb_b, etab, t_in, st.ein + n * in_node);
     if (int rc = check_launch("temb_kernel")) return rc;
-    hipLaunchKernelGGL(h0_kernel, dim3((unsigned)(((size_t)T * BN * 64 + 255) / 256)), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
+    hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
                        etab, x, v, st.hs, st.xs, st.vs, frames, st.ein);
     if (int rc = check_launch("h0_kernel")) return rc;
   }
@@ -2264,16 +2263,15 @@ int egno_backward_impl(int frames, int emb_cols, int B, int N, int T, int n_laye
   {
     const int emb_ld = in_node + emb_cols;
     if (n >= (size_t)1 << 31) return fail(NONODE_EUNSUPPORTED, "egno_backward: %zu embedding rows", n);
-    const long long ntile = ((long long)n + EG_TILE - 1) / EG_TILE;
-    const int nblk = (int)(ntile < EG_MAX_BLOCKS ? ntile : EG_MAX_BLOCKS);
+    const int nblk = eg_blocks((long long)n), tpb = eg_tpb((long long)n);
     const float* hin_s = st.ein;
     const float* trig_s = st.ein + n * in_node;
-    if (emb_ld <= 40)
-      hipLaunchKernelGGL(emb_grad_kernel<40>, dim3(nblk), dim3(256), 0, s, BN, T, Bt, in_node, emb_cols, frames, gh,
-                         hin_s, trig_s, w.partial);
+    if (emb_ld <= 48)
+      hipLaunchKernelGGL(emb_grad_kernel<48>, dim3(nblk), dim3(256), 0, s, BN, T, Bt, in_node, emb_cols, frames, gh,
+                         hin_s, trig_s, w.partial, tpb);
     else
-      hipLaunchKernelGGL(emb_grad_kernel<136>, dim3(nblk), dim3(256), 0, s, BN, T, Bt, in_node, emb_cols, frames, gh,
-                         hin_s, trig_s, w.partial);
+      hipLaunchKernelGGL(emb_grad_kernel<144>, dim3(nblk), dim3(256), 0, s, BN, T, Bt, in_node, emb_cols, frames, gh,
+                         hin_s, trig_s, w.partial, tpb);
     if (int rc = check_launch("emb_grad_kernel")) return rc;
     const int nc0 = emb_ld < 64 ? emb_ld : 64;
     ReduceJob jobs[2];
@@ -2577,6 +2575,46 @@ int nonode_segno_backward(int B, int N, int T, int n_edge_feat, float coords_wei
   if (g_x_in && g_x_in != gx) hipMemcpyAsync(g_x_in, gx, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   if (g_v_in && g_v_in != gv) hipMemcpyAsync(g_v_in, gv, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
   return check_launch("segno_backward");
+}
+
+// ---- embedding Linear (SEGNO model.py:73: h = embedding(his)) as a forward / backward pair, so that a
+// training caller keeps it off the autograd tape (its broadcast torch ops and their reverse were ~0.1 ms of
+// the C3 training step)
+int nonode_embedding_forward(int n_rows, int in_features, const float* in, const float* weight, const float* bias,
+                             float* out, void* stream) {
+  if (n_rows <= 0 || in_features < 1 || in_features > 40 || (size_t)n_rows * 64 >= ((size_t)1 << 31))
+    return fail(NONODE_EUNSUPPORTED, "embedding_forward: rows=%d in_features=%d", n_rows, in_features);
+  if (!in || !weight || !bias || !out) return fail(NONODE_EINVAL, "embedding_forward: null pointer");
+  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)(((size_t)n_rows * 64 + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, n_rows, in_features, in, weight, bias, out);
+  return check_launch("embedding_forward");
+}
+
+size_t nonode_embedding_backward_workspace_bytes(int n_rows, int in_features) {
+  if (n_rows <= 0 || in_features < 1) return 0;
+  return (size_t)eg_blocks(n_rows) * 64 * (in_features + 1) * sizeof(float);
+}
+
+// grad_weight[o][k] = sum_n grad_out[n][o] in[n][k], grad_bias[o] = sum_n grad_out[n][o] (written, not
+// accumulated): emb_grad_kernel with no time-embedding columns, then the block partials in block order
+int nonode_embedding_backward(int n_rows, int in_features, const float* in, const float* grad_out,
+                              float* grad_weight, float* grad_bias, void* workspace, size_t workspace_bytes,
+                              void* stream) {
+  if (n_rows <= 0 || in_features < 1 || in_features > 40)
+    return fail(NONODE_EUNSUPPORTED, "embedding_backward: rows=%d in_features=%d", n_rows, in_features);
+  if (!in || !grad_out || !grad_weight || !grad_bias || !workspace)
+    return fail(NONODE_EINVAL, "embedding_backward: null pointer");
+  if (workspace_bytes < nonode_embedding_backward_workspace_bytes(n_rows, in_features))
+    return fail(NONODE_EINVAL, "embedding_backward: workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = eg_blocks(n_rows);
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(emb_grad_kernel<48>, dim3(nblk), dim3(256), 0, s, n_rows, 1, 1, in_features, 0, 0, grad_out, in,
+                     in, part, eg_tpb(n_rows));   // (no time-embedding columns: trig is never read)
+  if (int rc = check_launch("emb_grad_kernel")) return rc;
+  const ReduceJob job{part, nblk, 64, in_features, grad_weight, in_features, 0, 1, grad_bias, 0, 1.f, 1 << 30, 0,
+                      (long long)64 * (in_features + 1)};
+  return launch_reduce_batch(&job, 1, s);
 }
 
 }  // extern "C"

@@ -134,9 +134,17 @@ class EGNO(nn.Module):
                 self.time_conv_x_modules.append(_TimeConvParams(2, 2, modes, 0.1))
         self._blobs = None
         self._blob_key = None
+        self._bblobs = None
+        self._bblob_key = None
+        _lib.track_packs(self)   # packs dropped after any optimizer step over these parameters
         self.to(device)
 
     # ---- packed weights (re-packed whenever a parameter changed in place) ----
+    def _drop_packs(self):
+        """Forget the packed blobs (the next forward / backward re-packs): _lib.track_packs."""
+        self._blob_key = None
+        self._bblob_key = None
+
     def _pack_variant(self):
         return _lib.VARIANT_EGNO | (_lib.LAYER_NORM_RADIAL if self.norm else 0)
 
@@ -195,7 +203,7 @@ class EGNO(nn.Module):
         """Backward fragments (unscaled forward + transposed) per layer, rebuilt like _packed()."""
         params = [p for l in self.layers for p in l.parameters()]
         key = tuple((p.data_ptr(), p._version) for p in params)
-        if getattr(self, "_bblobs", None) is not None and key == self._bblob_key:
+        if self._bblobs is not None and key == self._bblob_key:
             return self._bblobs
         L = _lib.lib()
         dev = self.embedding.weight.device

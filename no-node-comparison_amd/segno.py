@@ -8,9 +8,11 @@ discards the integrator result for a single input and returns its inputs. This c
 the integrator result (what the shadowed forward at model.py:28-51 and ``forward_step`` compute);
 ``bug_compat=True`` reproduces the reference's identity behaviour exactly.
 
-Training (train_nbody.py:168-179): in train mode with gradients enabled, the embedding Linear runs
-as a torch op and forward_step goes through autograd.SEGNOStepTrain (the HIP integrator forward
-with saved substeps and its hand-written reverse pass), so loss.backward() reaches every parameter.
+Training (train_nbody.py:168-179): in train mode with gradients enabled, forward goes through
+autograd.SEGNOTrain: the embedding Linear (nonode_embedding_forward / _backward) and the HIP
+integrator forward with saved substeps and its hand-written reverse pass, so loss.backward() reaches
+every parameter. forward_step (an already-embedded h) and several inputs go through
+autograd.SEGNOStepTrain with the embedding as torch ops on the tape.
 """
 import ctypes
 
@@ -97,7 +99,13 @@ class SEGNO(nn.Module):
         self._blob_key = None
         self._bblob = None
         self._bblob_key = None
+        _lib.track_packs(self)   # packs dropped after any optimizer step over these parameters
         self.to(device)
+
+    def _drop_packs(self):
+        """Forget the packed blobs (the next forward / backward re-packs): _lib.track_packs."""
+        self._blob_key = None
+        self._bblob_key = None
 
     def gcl_param_names(self):
         """Parameter names in nonode_layer_grads field order (vel_* = None: coord_mlp_vel is not on
@@ -145,8 +153,9 @@ class SEGNO(nn.Module):
         edge_attr [E, in_edge_nf]. Returns (x, h, v) after T substeps of dt = 1/T.
 
         In train mode with gradients enabled (nn.Module's default state) this records the autograd
-        tape: T single-substep launches that save every substep's state for the reverse pass
-        (autograd.SEGNOStepTrain), slower and heavier in memory than the fused inference launch.
+        tape: the embedding and one training-forward launch of the T substeps that saves every
+        substep's state for the reverse pass (autograd.SEGNOTrain), heavier in memory than the
+        inference launch.
         Inference should run under model.eval() or torch.no_grad(), as the reference's test loops do."""
         if x.dim() == 3:
             return self._forward_multi(his, x, edges, v, edge_attr, int(T), in_steps)
@@ -154,7 +163,13 @@ class SEGNO(nn.Module):
             # the live reference forward returns its inputs (and the embedded h)
             return x, self._embed(his), v
         if self._training():
-            return self._step(self._embed(his), x, edges, v, edge_attr, int(T))
+            if his.shape[-1] > 40:   # (nonode_embedding_* take up to 40 input features)
+                return self._step(self._embed(his), x, edges, v, edge_attr, int(T))
+            # the embedding and the T substeps as one autograd node (autograd.SEGNOTrain)
+            B, N = self._check_inputs(x, edges, v, edge_attr)
+            _lib.require_device(his, self.embedding.weight)
+            from .autograd import segno_train
+            return segno_train(self, his, x, v, edge_attr, int(T), B, N)
         return self._run(his, None, x, edges, v, edge_attr, int(T))
 
     def _forward_multi(self, his, x, edges, v, edge_attr, T, in_steps):
@@ -202,12 +217,18 @@ class SEGNO(nn.Module):
         inference launch."""
         if not self._training():
             return self._run(None, h, x, edges, v, edge_attr, T)
-        _lib.require_device(h, x, v, edge_attr, self.embedding.weight)
+        _lib.require_device(h)
+        B, N = self._check_inputs(x, edges, v, edge_attr)
+        from .autograd import segno_step_train
+        return segno_step_train(self, h, x, v, edge_attr, T, B, N)
+
+    def _check_inputs(self, x, edges, v, edge_attr):
+        """(B, N) of a training call's fully connected graph, after the device and shape checks."""
+        _lib.require_device(x, v, edge_attr, self.embedding.weight)
         B, N = check_full_graph(edges, x.shape[0])
         if edge_attr.shape != (B * N * (N - 1), self.in_edge_nf):
             raise ValueError(f"edge_attr must be [{B * N * (N - 1)}, {self.in_edge_nf}]")
-        from .autograd import segno_step_train
-        return segno_step_train(self, h, x, v, edge_attr, T, B, N)
+        return B, N
 
     def _embed(self, his):
         """SEGNO.embedding (model.py:73): a torch op on the device, so it is on the autograd tape

@@ -112,14 +112,17 @@ def test_egno_training_rejects_n_beyond_the_edge_backward_tables():
         _train_step_grads(m, inp, _dev(np.zeros((B, N, T, 3), np.float32)), T, B, N)
 
 
-def test_egno_adam_step_runs_and_repacks():
+@pytest.mark.parametrize("fused", [False, True])
+def test_egno_adam_step_runs_and_repacks(fused):
     """One optimizer step (Adam as model_confs.yaml:15-17) changes the weights in place; the next
-    forward must use the re-packed blobs (no stale fragments)."""
+    forward must use the re-packed blobs (no stale fragments). fused=True: torch's fused Adam does not
+    bump the parameters' versions, so only the optimizer step hook (_lib.track_packs) drops the packs.
+    lr 1e-2 so that stale weights would miss the bar by far."""
     B, N, T = 2, 6, 10
     c = _egno_case(B, N, T, seed=3)
     m = _egno(seed=4)
     inp = {k: _dev(v) for k, v in c.items()}
-    opt = torch.optim.Adam(m.parameters(), lr=1e-4, weight_decay=1e-8)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=1e-8, fused=fused)
     loc_true = torch.zeros(B, N, T, 3, device=DEV_)
     loss0, _, _, _ = _train_step_grads(m, inp, loc_true, T, B, N)
     opt.step()

@@ -148,13 +148,30 @@ def test_segno_train_forward_equals_inference_forward():
         assert torch.equal(a.detach(), b)
 
 
-def test_segno_adam_step_runs_and_repacks():
+def test_segno_train_model_forward_equals_inference_forward():
+    """SEGNO.forward in training (autograd.SEGNOTrain: nonode_embedding_forward, then the training
+    launch of the T substeps) gives bitwise the inference forward's outputs (the same embedding
+    kernel and layer arithmetic)."""
+    B, N, T = 8, 20, 10
+    m = _segno(seed=3)
+    his, x, v, r, c, ea, _ = _case(B, N, seed=4)
+    args = (_dev(his), _dev(x), [_dev(r), _dev(c)], _dev(v), _dev(ea))
+    xa, ha, va = m(*args, T=T)
+    assert xa.requires_grad
+    with torch.no_grad():
+        xb, hb, vb = m(*args, T=T)
+    for a, b in ((xa, xb), (ha, hb), (va, vb)):
+        assert torch.equal(a.detach(), b)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_segno_adam_step_runs_and_repacks(fused):
     """An optimizer step changes the GCL weights in place; the next forward must use the re-packed
-    forward and backward blobs."""
+    forward and backward blobs (fused=True: no version bump, only the optimizer step hook drops them)."""
     B, N, T = 2, 6, 5
     m = _segno(seed=5)
     case = _case(B, N, seed=6)
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, fused=fused)
     _hip_step(m, *case, T)
     opt.step()
     loss, _ = _hip_step(m, *case, T)
