@@ -281,6 +281,7 @@ size_t layer_lds_floats(int ct, int s_rows, int keep = 0) {
 template <int VARIANT, int KF, int NW, bool OPT, bool SAVE = false>
 __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)[NW + 1]) {
   constexpr bool PAIR = NW == 4;
+  constexpr bool TRIPLE = PAIR && VARIANT == EGNO;   // three-unit iterations before the pairs
   [[maybe_unused]] constexpr bool stamp_here = VARIANT == EGNO && NW == 4 && !OPT;   // (NONODE_STAMP builds)
   constexpr bool rnorm = OPT && VARIANT == EGNO;    // basic.py:140-141
   constexpr bool ctanh = OPT && VARIANT == SEGNO;   // gcl.py:57-59
@@ -653,6 +654,77 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)
           float e0[KF], e1[KF];
           fetch_ef(min(k, kp_hi) + kof, e0);
           fetch_ef(min(k + 1, kp_hi) + kof, e1);
+          // EGNO: three units per iteration first, a third independent chain for the stalls at the
+          // stage boundaries (C2 layer -1.5 us; SEGNO's C3 launch measured
+          // +1 us with it, so SEGNO keeps pairs only); then pairs, then single units
+          if (TRIPLE && k + 2 <= kp_hi) {
+            float e2[KF];
+            fetch_ef(min(k + 2, kp_hi) + kof, e2);
+#pragma unroll 1
+            for (; k + 2 <= kp_hi; k += 3) {
+              float n0[KF], n1[KF], n2[KF];
+              fetch_ef(min(k + 3, kp_hi) + kof, n0);
+              fetch_ef(min(k + 4, kp_hi) + kof, n1);
+              fetch_ef(min(k + 5, kp_hi) + kof, n2);
+              f4 a0[4], a1[4], a2[4], m0[4], m1[4], m2[4], pm[4];
+              float r00, r01, r02, r10, r11, r12, r20, r21, r22;
+              float f00, f01, f02, f10, f11, f12, f20, f21, f22;
+              float cA, cB, cC;
+              bool okA, okB, okC;
+              head2(k + kof, e0, a0, r00, r01, r02, okA);
+              head2(k + 1 + kof, e1, a1, r10, r11, r12, okB);
+              head2(k + 2 + kof, e2, a2, r20, r21, r22, okC);
+              silu_ecl(a0);
+              silu_ecl(a1);
+              silu_ecl(a2);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) { m0[mt] = rB2[mt]; m1[mt] = rB2[mt]; m2[mt] = rB2[mt]; }
+              {
+                h8 ah0[2], al0[2], ah1[2], al1[2], ah2[2], al2[2];
+                h16_split(a0, ah0, al0);
+                h16_split(a1, ah1, al1);
+                h16_split(a2, ah2, al2);
+                mfma_h16r3(m0, m1, m2, rw2, ah0, al0, ah1, al1, ah2, al2, us_w2);
+              }
+              silu_ecl(m0);
+              silu_ecl(m1);
+              silu_ecl(m2);
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) {
+                pm[mt] = add4(add4(m0[mt], m1[mt]), m2[mt]);
+                a0[mt] = rBC1[mt];
+                a1[mt] = rBC1[mt];
+                a2[mt] = rBC1[mt];
+              }
+              {
+                h8 mh0[2], ml0[2], mh1[2], ml1[2], mh2[2], ml2[2];
+                h16_split(m0, mh0, ml0);
+                h16_split(m1, mh1, ml1);
+                h16_split(m2, mh2, ml2);
+                mfma_h16r3(a0, a1, a2, rwc1, mh0, ml0, mh1, ml1, mh2, ml2, us_wc1);
+              }
+              edge_f(a0, r00, r01, r02, f00, f01, f02, cA);
+              edge_f(a1, r10, r11, r12, f10, f11, f12, cB);
+              edge_f(a2, r20, r21, r22, f20, f21, f22, cC);
+              const bool redo = (okA && !__builtin_isfinite(cA)) || (okB && !__builtin_isfinite(cB)) ||
+                                (okC && !__builtin_isfinite(cC));
+              if (__builtin_expect(__any(redo), 0)) {
+                int kg = k;
+                asm volatile("" : "+v"(kg));
+                f4 x0[4], x1[4], x2[4];
+                exact_unit(kg + kof, e0, x0, f00, f01, f02);
+                exact_unit(kg + 1 + kof, e1, x1, f10, f11, f12);
+                exact_unit(kg + 2 + kof, e2, x2, f20, f21, f22);
+#pragma unroll
+                for (int mt = 0; mt < 4; ++mt) pm[mt] = (x0[mt] + x1[mt]) + x2[mt];
+              }
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) msum[mt] = add4(msum[mt], pm[mt]);
+              fs0 += (f00 + f10) + f20; fs1 += (f01 + f11) + f21; fs2 += (f02 + f12) + f22;
+#pragma unroll
+              for (int kf = 0; kf < KF; ++kf) { e0[kf] = n0[kf]; e1[kf] = n1[kf]; e2[kf] = n2[kf]; }
+            }
+          }
 #pragma unroll 1
           for (; k + 1 <= kp_hi; k += 2) {
             float n0[KF], n1[KF];

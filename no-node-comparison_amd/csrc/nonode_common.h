@@ -328,6 +328,34 @@ __device__ __forceinline__ void mfma_h16r2(f4 (&acc0)[4], f4 (&acc1)[4], const H
   }
 }
 
+// three edge units through register-resident fragments (the triple loop, NONODE_TRIPLE builds)
+__device__ __forceinline__ void mfma_h16r3(f4 (&acc0)[4], f4 (&acc1)[4], f4 (&acc2)[4], const H16Frags& f,
+                                           const h8 (&x0h)[2], const h8 (&x0l)[2], const h8 (&x1h)[2],
+                                           const h8 (&x1l)[2], const h8 (&x2h)[2], const h8 (&x2l)[2], unsigned us) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const h8 x0s = h8_scale(x0h[s], us), x1s = h8_scale(x1h[s], us), x2s = h8_scale(x2h[s], us);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      acc0[mo] = mfma16(f.hi[s][mo], x0h[s], acc0[mo]);
+      acc1[mo] = mfma16(f.hi[s][mo], x1h[s], acc1[mo]);
+      acc2[mo] = mfma16(f.hi[s][mo], x2h[s], acc2[mo]);
+    }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      acc0[mo] = mfma16(f.lo[s][mo], x0s, acc0[mo]);
+      acc1[mo] = mfma16(f.lo[s][mo], x1s, acc1[mo]);
+      acc2[mo] = mfma16(f.lo[s][mo], x2s, acc2[mo]);
+    }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      acc0[mo] = mfma16(f.hi[s][mo], x0l[s], acc0[mo]);
+      acc1[mo] = mfma16(f.hi[s][mo], x1l[s], acc1[mo]);
+      acc2[mo] = mfma16(f.hi[s][mo], x2l[s], acc2[mo]);
+    }
+  }
+}
+
 // f4 sum as four plain v_add_f32: the backend would emit two v_pk_add_f32, which cost more than the
 // plain ops they replace when issued beside MFMAs (MI355X_MICROARCH.md constants table)
 __device__ __forceinline__ f4 add4(f4 a, f4 b) {
