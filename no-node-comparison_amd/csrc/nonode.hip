@@ -1437,12 +1437,14 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       f4 o = hvs[t];
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
-      if (p.mask_out) {   // wave-uniform (training forward only)
+      if (p.mask_out) {   // wave-uniform (training forward only): lanes 0..3 store the 4 ballots at once
+        unsigned long long mine = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const unsigned long long bits = __ballot(y[q] > 0.f);
-          if (lane == q) p.mask_out[(((size_t)t * ntiles + tile) * 4 + wave) * 4 + q] = bits;
+          mine = lane == q ? bits : mine;
         }
+        if (lane < 4) p.mask_out[(((size_t)t * ntiles + tile) * 4 + wave) * 4 + lane] = mine;
       }
       if (svalid) {
         *reinterpret_cast<f4*>(p.h_out + ((size_t)t * BN + sc) * 64 + chs) = o;

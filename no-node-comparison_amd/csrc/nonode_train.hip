@@ -2019,7 +2019,7 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
     if (int rc = launch_layer<EGNO>(T * B, N, n_edge_feat, frames ? T * B : B, hin, xin, vin, edge_fea, blobs[l], 0.f,
                                     1.f, 0, last ? h_out : st.hs + (l + 1) * n * 64,
                                     last ? x_out : st.xs + (l + 1) * n * 3, nullptr, s, 1, nullptr,
-                                    st.Ms + l * n * 64, st.Fs + l * n * 4))
+                                    st.Ms + l * n * 64, st.Fs + l * n * 4, tc ? BN : 0))   // XCD order as the TimeConv's
       return rc;
   }
   hipMemcpyAsync(v_out, tc ? st.ve + (L - 1) * n * 3 : st.vs, n * 3 * sizeof(float), hipMemcpyDeviceToDevice, s);
