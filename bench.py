@@ -238,7 +238,7 @@ def build_egno_case(B, N, T, seed, dev, world=1, rank=0, plan=None):
 
 # ---------------------------------------------------------------------------------------------------
 # CPU baseline: the reference's torch operators on the host cores (oracle/torch_ref.py)
-def cpu_time(fn, budget_s, min_calls=1, max_calls=20):
+def cpu_time(fn, budget_s, min_calls=10, max_calls=20):
     """Median wall time of fn() over as many calls as fit in budget_s (at least min_calls)."""
     times, out = [], None
     t_all = time.perf_counter()
@@ -251,7 +251,7 @@ def cpu_time(fn, budget_s, min_calls=1, max_calls=20):
     return float(np.median(times)), len(times), out
 
 
-def cpu_baseline_time(fn, budget_s, min_calls=1, max_calls=20):
+def cpu_baseline_time(fn, budget_s, min_calls=10, max_calls=20):
     """cpu_time of the CPU baseline on baseline_threads() torch threads. The threads actually used are
     recorded by _baseline (called inside the same context)."""
     with _BaselineThreads():
@@ -366,7 +366,20 @@ def run_egno(args, world, rank, dev, backend):
     model = pkg.EGNO(n_layers=4, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=2,
                      num_timesteps=T, time_emb_dim=32, device=dev).eval()
     case = build_egno_case(B, N, T, seed=1234, dev=dev, plan=plan)
-    call = lambda: model(case["x"], case["h"], case["edges"], case["edge_fea"], v=case["v"],  # noqa: E731
+    r0, c0 = case["edges"]
+
+    def edges():
+        """--edges: fixed = one edge list for every step (validated once); get_edges = a fresh list per
+        step from harness.get_edges (nonode_full_edges, valid by construction); fresh = fresh device
+        tensors the boundary has never seen (copies), checked on the device every step -- the
+        reference loop's fresh get_edges(...).to(device) per batch (main_simulation_simple_no.py:217-218)"""
+        if args.edges == "get_edges":
+            return pkg.harness.get_edges(B, N, dev)
+        if args.edges == "fresh":
+            return [r0.clone(), c0.clone()]
+        return case["edges"]
+
+    call = lambda: model(case["x"], case["h"], edges(), case["edge_fea"], v=case["v"],  # noqa: E731
                          loc_mean=case["loc_mean"], timesteps_out=case["t_out"])
     with torch.no_grad():
         _prewarm(call, args, dev)
@@ -386,14 +399,33 @@ def run_egno(args, world, rank, dev, backend):
             for _ in range(args.steps):
                 out = call()
             records = _lib.profile_end()
+        # host overhead per forward: with an idle GPU before each call, the host time
+        # to enqueue one forward and its synchronous wall time, against the recorded kernel time
+        enq, wall = [], []
+        for _ in range(10):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            out = call()
+            t1 = time.perf_counter()
+            torch.cuda.synchronize(dev)
+            enq.append(t1 - t0)
+            wall.append(time.perf_counter() - t0)
     el = max_over_ranks(el, dev)
     value = plan["B_global"] * args.steps / el
     cus = torch.cuda.get_device_properties(dev).multi_processor_count if dev.type == "cuda" else 0
     res = _result(args, world, plan, el / args.steps * 1e3, value,
                   f"C2: EGNO forward (4 layers, hidden 64, 2 modes), charged N={N}, T={T}, B={B} per GPU",
-                  {"n_balls": N, "num_timesteps": T, "layer_workgroups": min(T * B, cus),
+                  {"n_balls": N, "num_timesteps": T, "layer_workgroups": min(T * B, cus), "edges": args.edges,
                    "parallelism": f"batch-sharded replicas x{world} (no collective)"}, backend,
                   frames_per_s=value * T)
+    kern_ms = float(np.sum([ms for _, ms in records])) / args.steps if records else None
+    res["host_overhead"] = {
+        "enqueue_ms_median": float(np.median(enq)) * 1e3, "sync_wall_ms_median": float(np.median(wall)) * 1e3,
+        "recorded_kernel_ms_per_call": kern_ms,
+        "note": "per forward with an idle GPU before the call: enqueue = host time until the call returns; "
+                "sync_wall = until its kernels finish; recorded kernels = the layer and TimeConv launches "
+                "(hipEvents, temb_kernel not recorded). ms_per_step is the pipelined rate (host enqueues "
+                "ahead of the GPU)"}
     layer_events = [ms for kind, ms in records if kind == _lib.VARIANT_EGNO]
     tconv_ms = [ms for kind, ms in records if kind in (_lib.PROF_TCONV, _lib.PROF_TCONV_FIRST)]
     if layer_events:
@@ -419,13 +451,19 @@ def run_egno(args, world, rank, dev, backend):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import torch_ref as tr
         p = _cpu_params(model)
-        r, c = tr.full_edges(B, N)
-        inp = [_cpu(case[k]) for k in ("x", "h")] + [r, c] + [_cpu(case[k]) for k in ("edge_fea", "v", "loc_mean")]
-        t_out = _cpu(case["t_out"])
+        # a bounded sample (>= 10 timed calls in the budget): the first Bc samples of the batch
+        Bc = min(B, args.cpu_samples or 128)
+        r, c = tr.full_edges(Bc, N)
+        rows, erows = Bc * N, Bc * N * (N - 1)
+        inp = [_cpu(case["x"], rows), _cpu(case["h"], rows), r, c, _cpu(case["edge_fea"], erows),
+               _cpu(case["v"], rows), _cpu(case["loc_mean"], rows)]
+        t_out = _cpu(case["t_out"], Bc)
         with torch.no_grad():
-            med, calls, ref = cpu_baseline_time(lambda: tr.egno_forward(p, *inp, t_out, T=T), args.cpu_budget, 3)
-        res["cpu_baseline"] = _baseline(B, med, calls, f"EGNO forward at the measured batch B={B}, N={N}, T={T}")
-        res["parity"] = dict(_parity(_cpu(out[0]), ref[0]), samples_checked=B,
+            med, calls, ref = cpu_baseline_time(lambda: tr.egno_forward(p, *inp, t_out, T=T), args.cpu_budget)
+        res["cpu_baseline"] = _baseline(Bc, med, calls, f"EGNO forward on the first {Bc} samples of the measured "
+                                        f"batch (B={B}), N={N}, T={T}")
+        got = _cpu(out[0]).reshape(T, B, N, 3)[:, :Bc].reshape(-1, 3)
+        res["parity"] = dict(_parity(got, ref[0]), samples_checked=Bc,
                              bar="1e-5 max-norm relative (north_star)")
     return res
 
@@ -503,7 +541,7 @@ def run_segno(args, world, rank, dev, backend, gravity=False):
         if gravity:
             # the dense one-hot mean (gcl.py:16-23) needs 259 GB per substep here: the scatter-mean
             # variant (same values) on the first Bc samples
-            Bc = min(B, args.cpu_samples or 16)
+            Bc = min(B, args.cpu_samples or 4)
             r, c = tr.full_edges(Bc, N)
             rows, erows = Bc * N, Bc * N * (N - 1)
             args_c = (_cpu(his, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(ea, erows), steps,
@@ -517,14 +555,19 @@ def run_segno(args, world, rank, dev, backend, gravity=False):
             res["parity"] = dict(_parity(got[:1], ref[:1]), samples_checked=Bc,
                                  all_segments=_parity(got, ref), bar="1e-5 max-norm relative, first segment")
         else:
-            r, c = tr.full_edges(B, N)
-            args_c = (_cpu(his), _cpu(x), r, c, _cpu(v), _cpu(ea))
+            # the first Bc samples: the reference's dense one-hot mean costs O(B^2) per substep
+            # (34 s per call at B=512), so the sample's rate is an upper bound of the reference's at B
+            Bc = min(B, args.cpu_samples or 64)
+            r, c = tr.full_edges(Bc, N)
+            rows, erows = Bc * N, Bc * N * (N - 1)
+            args_c = (_cpu(his, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(ea, erows))
             with torch.no_grad():
                 med, calls, ref = cpu_baseline_time(lambda: tr.segno_forward_step(p, *args_c, T=steps[0], dense_mean=True),
                                            args.cpu_budget)
-            res["cpu_baseline"] = _baseline(B, med, calls, f"SEGNO embedding + forward_step at the measured batch "
-                                            f"B={B}, {steps[0]} substeps, the reference's dense one-hot mean")
-            res["parity"] = dict(_parity(_cpu(out), ref[0]), samples_checked=B,
+            res["cpu_baseline"] = _baseline(Bc, med, calls, f"SEGNO embedding + forward_step on the first {Bc} samples "
+                                            f"of the measured batch (B={B}), {steps[0]} substeps, the reference's dense "
+                                            f"one-hot mean (O(B^2): the rate at B={B} is lower)")
+            res["parity"] = dict(_parity(_cpu(out, rows), ref[0]), samples_checked=Bc,
                                  bar="1e-5 max-norm relative (north_star)")
     return res
 
@@ -603,11 +646,11 @@ def run_egno_train(args, world, rank, dev, backend):
     value = plan["B_global"] * args.steps / el
     res = _result(args, world, plan, el / args.steps * 1e3, value,
                   f"C4: EGNO training step (fwd + bwd{' + 1 all-reduce' if world > 1 else ''} + Adam), charged N={N}, T={T}, B={B} per GPU",
-                  {"n_balls": N, "num_timesteps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                  {"n_balls": N, "num_timesteps": T, "grad_buffer_bytes": fg.numel * 4,
                    "optimizer": f"torch.optim.Adam ({args.optimizer})",
                    "parallelism": (f"data-parallel x{world}, one {backend} all-reduce per step" if backend else
                                    "single GPU, no all-reduce")},
-                  backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0, loss=float(loss.detach()))
+                  backend, allreduce_bytes=fg.numel * 4 if world > 1 else 0, loss=float(loss.detach()))
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
     wl_key = "C4" if B == 512 else f"C4@B={B}"   # PMC traffic is per measured shard size
@@ -633,30 +676,39 @@ def run_egno_train(args, world, rank, dev, backend):
                            "forward_layer_avg_ms": float(np.mean(layer)) if layer else None}
     if grads0 is not None:
         from oracle import torch_ref as tr
-        Bc = min(B, args.cpu_samples or 512)
-        r, c = tr.full_edges(Bc, N)
-        rows, erows = Bc * N, Bc * N * (N - 1)
-        p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
-        copt = torch.optim.Adam(list(p.values()), lr=1e-4, weight_decay=1e-8)
-        inp = [_cpu(case["x"], rows), _cpu(case["h"], rows), r, c, _cpu(case["edge_fea"], erows),
-               _cpu(case["v"], rows), _cpu(case["loc_mean"], rows)]
-        tgt, t_out = _cpu(loc_true, Bc), _cpu(case["t_out"], Bc)
-        first = {}
 
-        def cstep():
-            copt.zero_grad()
+        def sample(Bc):
+            r, c = tr.full_edges(Bc, N)
+            rows, erows = Bc * N, Bc * N * (N - 1)
+            return ([_cpu(case["x"], rows), _cpu(case["h"], rows), r, c, _cpu(case["edge_fea"], erows),
+                     _cpu(case["v"], rows), _cpu(case["loc_mean"], rows)], _cpu(loc_true, Bc), _cpu(case["t_out"], Bc))
+
+        def cpu_step(p, opt, Bc, inp, tgt, t_out):
+            if opt is not None:
+                opt.zero_grad()
             xx, _, _ = tr.egno_forward(p, *inp, t_out, T=T)
             pred = xx.reshape(T, Bc, N, 3).permute(1, 2, 0, 3)
             loss = torch.nn.functional.mse_loss(pred, tgt, reduction="none").mean((0, 1, 3)).mean()
             loss.backward()
-            if not first:
-                first.update({k: t.grad.clone() for k, t in p.items() if t.grad is not None})
-            copt.step()
+            if opt is not None:
+                opt.step()
 
-        med, calls, _ = cpu_baseline_time(cstep, args.cpu_budget)
+        # timed: a bounded sample (>= 10 calls in the budget; 11 s per call at B=512)
+        Bc = min(B, args.cpu_samples or 64)
+        p = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+        copt = torch.optim.Adam(list(p.values()), lr=1e-4, weight_decay=1e-8)
+        s_inp, s_tgt, s_t = sample(Bc)
+        med, calls, _ = cpu_baseline_time(lambda: cpu_step(p, copt, Bc, s_inp, s_tgt, s_t), args.cpu_budget)
         res["cpu_baseline"] = _baseline(Bc, med, calls, f"EGNO training step (forward, loss, autograd backward, "
-                                        f"Adam) at B={Bc}")
-        if Bc == B:
+                                        f"Adam) on the first {Bc} samples of the measured batch (B={B})")
+        # parity (untimed): the first step's gradients at the whole batch, fp32 and float64 autograd
+        if not args.no_grad_parity:
+            inp, tgt, t_out = sample(B)
+            pf = {k: v.clone().requires_grad_(True) for k, v in p0.items()}
+            with _BaselineThreads():
+                cpu_step(pf, None, B, inp, tgt, t_out)
+            first = {k: t.grad for k, t in pf.items() if t.grad is not None}
+            Bc = B
             # parity of the first step's gradients at the initial weights: against the fp32 CPU path
             # as it runs (its own fp32 accumulation error included) and against the same ops in f64
             p64 = {k: v.double().requires_grad_(True) for k, v in p0.items()}
@@ -750,11 +802,11 @@ def run_segno_train(args, world, rank, dev, backend):
     res = _result(args, world, plan, el / args.steps * 1e3, value,
                   f"SEGNO training step (forward_step of {T} substeps + MSE + HIP reverse pass"
                   f"{' + 1 all-reduce' if world > 1 else ''} + Adam), charged N={N}, B={B} per GPU",
-                  {"n_balls": N, "substeps": T, "grad_buffer_bytes": fg.flat.numel() * 4,
+                  {"n_balls": N, "substeps": T, "grad_buffer_bytes": fg.numel * 4,
                    "optimizer": f"torch.optim.Adam ({args.optimizer})",
                    "parallelism": (f"data-parallel x{world}, one {backend} all-reduce per step" if backend else
                                    "single GPU, no all-reduce")},
-                  backend, allreduce_bytes=fg.flat.numel() * 4 if world > 1 else 0)
+                  backend, allreduce_bytes=fg.numel * 4 if world > 1 else 0)
     e0 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD0]
     e1 = [ms for kind, ms in records if kind == _lib.PROF_EDGE_BWD1]
     if e0 or e1:
@@ -871,7 +923,7 @@ def run_egno_rollout(args, world, rank, dev, backend):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import torch_ref as tr
         p = _cpu_params(model)
-        Bc = min(B, args.cpu_samples or 64)
+        Bc = min(B, args.cpu_samples or 16)
         r, c = tr.full_edges(Bc, N)
         rows, erows = Bc * N, Bc * N * (N - 1)
         args_c = (_cpu(nodes, rows), _cpu(x, rows), r, c, _cpu(v, rows), _cpu(eao, erows), _cpu(ea, erows),
@@ -1009,6 +1061,9 @@ def parse_args(argv=None):
                     help="egno = C2 (the headline line); segno = C3; segno_gravity = C5; egno_train = C4; "
                          "egno_rollout = SURVEY row f1; sim_charged = row f3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-grad-parity", action="store_true", help="skip the C4 whole-batch gradient parity check")
+    ap.add_argument("--edges", choices=["fixed", "get_edges", "fresh"], default="fixed",
+                    help="C2: the edge tensors each step gets (run_egno.edges)")
     ap.add_argument("--optimizer", choices=["fused", "foreach"], default="fused",
                     help="torch Adam implementation of the training workloads (same update rule)")
     ap.add_argument("--cpu-budget", type=float, default=25.0, help="seconds of CPU baseline work (median of calls)")

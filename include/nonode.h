@@ -456,6 +456,23 @@ int nonode_gather_batch(int S, int Tf, int N, int B, int I, int To, const float*
  * 16-byte aligned; idx device int32 in [0, S). */
 int nonode_gather_rows(int S, long long K, int B, const float* src, const int* idx, float* dst, void* stream);
 
+/* ---- the fully connected edge list at the boundary (sync-free) ---- */
+
+/* NBodyDataset.get_edges (EGNO/simulation/dataset_simple.py:101-111; SEGNO/dataset_nbody.py:84-94) on
+ * the device: rows, cols [B*N*(N-1)] int64, receiver i, sender j != i, ordered by (sample, i, j). */
+int nonode_full_edges(int B, int N, long long* rows, long long* cols, void* stream);
+
+/* Validate the `edges` argument of EGNO.forward (egno.py:37) / SEGNO.forward (model.py:53) on the
+ * device, without blocking the host: rows, cols (E indices of idx_bytes = 4 or 8 bytes) must be
+ * exactly nonode_full_edges(B, N). Any mismatch sets the device int *flag to 1 (never to 0: the
+ * caller clears it after reading it). */
+int nonode_check_full_edges(const void* rows, const void* cols, int idx_bytes, long long E, int B, int N, int* flag,
+                            void* stream);
+
+/* If *flag is set when the launch runs, fill bufs[k][0..counts[k]) (k < n_bufs <= 4, fp32) with NaN:
+ * the outputs of a forward whose edge list failed nonode_check_full_edges. */
+int nonode_poison_if_flagged(const int* flag, int n_bufs, float* const* bufs, const long long* counts, void* stream);
+
 
 /* ---- rollout metrics ---- */
 

@@ -32,6 +32,7 @@ SYMBOLS = (
     "nonode_egno_tconv_bwd_workspace_bytes", "nonode_egno_tconv_bwd",
     "nonode_pack_layers", "nonode_pack_layers_bwd", "nonode_pack_tconvs",
     "nonode_embedding_forward", "nonode_embedding_backward_workspace_bytes", "nonode_embedding_backward",
+    "nonode_full_edges", "nonode_check_full_edges", "nonode_poison_if_flagged",
 )
 
 VARIANT_EGNO = 0
@@ -175,6 +176,10 @@ def lib():
     L.nonode_gather_batch.argtypes = [_i] * 6 + [_vp] * 13
     L.nonode_gather_rows.argtypes = [_i, ctypes.c_longlong, _i, _vp, _vp, _vp, _vp]
     L.nonode_rollout_metrics.argtypes = [_i] * 3 + [_vp] * 5
+    _ll = ctypes.c_longlong
+    L.nonode_full_edges.argtypes = [_i, _i, _vp, _vp, _vp]
+    L.nonode_check_full_edges.argtypes = [_vp, _vp, _i, _ll, _i, _i, _vp, _vp]
+    L.nonode_poison_if_flagged.argtypes = [_vp, _i, ctypes.POINTER(_vp), ctypes.POINTER(_ll), _vp]
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

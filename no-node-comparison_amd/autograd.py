@@ -204,31 +204,34 @@ class SEGNOTrain(torch.autograd.Function):
     @staticmethod
     def forward(ctx, model, his, x, v, edge_attr, T, B, N, *params):
         L = _lib.lib()
+        ctx.his_dtype = his.dtype
         his = _f32(his)
         h = torch.empty(B * N, model.hidden_nf, device=x.device)
         ew, eb = _f32(model.embedding.weight), _f32(model.embedding.bias)
         _lib.check(L.nonode_embedding_forward(B * N, his.shape[1], _lib.ptr(his), _lib.ptr(ew), _lib.ptr(eb),
                                               _lib.ptr(h), _lib.stream_of(his)))
-        ctx.save_for_backward(*params)
-        ctx.his = his
+        # his through save_for_backward: autograd checks its version (an in-place edit after the
+        # forward raises instead of silently changing the embedding gradient)
+        ctx.save_for_backward(his, *params)
         return _segno_forward(ctx, model, h, x, v, edge_attr, T, B, N)
 
     @staticmethod
     def backward(ctx, gx, gh, gv):
         model = ctx.model
-        _ = ctx.saved_tensors
+        his = ctx.saved_tensors[0]
         grads, g_h, g_x, g_v = _segno_backward(ctx, gx, gh, gv, True, *ctx.needs_input_grad[2:4])
         L = _lib.lib()
-        n, din = ctx.his.shape
+        n, din = his.shape
         gw = torch.empty_like(model.embedding.weight)
         gb = torch.empty_like(model.embedding.bias)
         ws_bytes = L.nonode_embedding_backward_workspace_bytes(n, din)
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=g_h.device)
-        _lib.check(L.nonode_embedding_backward(n, din, _lib.ptr(ctx.his), _lib.ptr(g_h), _lib.ptr(gw), _lib.ptr(gb),
+        _lib.check(L.nonode_embedding_backward(n, din, _lib.ptr(his), _lib.ptr(g_h), _lib.ptr(gw), _lib.ptr(gb),
                                                _lib.ptr(ws), ws_bytes, _lib.stream_of(g_h)))
-        ctx.his = None
+        # dL/dhis of the embedding Linear (model.py:73), only when the caller's his requires grad
+        g_his = (g_h @ _f32(model.embedding.weight)).to(ctx.his_dtype) if ctx.needs_input_grad[1] else None
         out = [grads.get(nm) for nm, _ in model.module.named_parameters(prefix="module")]
-        return (None, None, g_x, g_v, None, None, None, None, gw, gb) + tuple(out)
+        return (None, g_his, g_x, g_v, None, None, None, None, gw, gb) + tuple(out)
 
 
 def segno_train(model, his, x, v, edge_attr, T, B, N):

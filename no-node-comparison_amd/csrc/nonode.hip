@@ -1587,9 +1587,23 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   const int cap = n_graphs / cus > 1 ? n_graphs / cus : 1;
   int cg = 0, cpg = 1, ct = 0;
   double best = -1.0;
-  for (int c = 1; c <= cap; ++c) {
+  // Inference launches (one step, no saved state) with few graphs per CU pick cg by the critical
+  // path instead: ceil(chunks / CUs) rounds of one chunk's tiles (a tile is N - 1 edge units and one
+  // node job) plus half a tile of per-chunk overhead. At C2's B = 512 both rules pick 4 graphs; at
+  // B = 64 (640 graphs) the fill rule's 2-graph chunks give 320 chunks, two rounds on 64 CUs, where 3
+  // graphs give one round of 214 chunks. Training forwards keep the fill rule: their chunk shape must
+  // not depend on the batch (batch-invariant sums of the data-parallel shards, §3.1 of DESIGN.md).
+  const bool crit = steps == 1 && !m_out && !sv && n_graphs < 16 * cus && !getenv_int("NONODE_FILL_CG");
+  for (int c = 1; c <= (crit ? 8 * 16 : cap); ++c) {
     const int tiles = (c * N + 15) / 16;
     if (tiles > 8 || layer_lds_floats(tiles, c * N) * 4 > LDS_MAX) break;
+    if (crit) {
+      const long long chunks = (n_graphs + c - 1) / c;
+      const long long rounds = (chunks + cus - 1) / cus;
+      const double cost = -(double)rounds * (tiles + 0.5);
+      if (cost > best + 1e-12) { best = cost; cg = c; ct = tiles; }
+      continue;
+    }
     const double fill = (double)(c * N) / (16.0 * tiles);
     if (fill >= best - 1e-12) { best = fill; cg = c; ct = tiles; }
   }
@@ -1812,8 +1826,13 @@ size_t nonode_egno_workspace_bytes(int B, int N, int T, int Bt) {
   const size_t n = (size_t)B * N * T;
   return (n * 64 + n * 3 + (size_t)Bt * T * 64 + 64) * sizeof(float);
 }
+// the flat layer's part starts at the common part rounded up to 256 bytes (its P, Q, M, F rows are
+// read and written as 16-byte vectors; (67n + 64 Bt T + 64) floats is only 8-byte aligned for n = 2 mod 4)
+static size_t flat_ws_offset(int B, int N, int T, int Bt) {
+  return (nonode_egno_workspace_bytes(B, N, T, Bt) + 255) & ~(size_t)255;
+}
 size_t nonode_egno_flat_workspace_bytes(int B, int N, int T, int Bt) {
-  return nonode_egno_workspace_bytes(B, N, T, Bt) + (size_t)B * N * T * 580 * sizeof(float);
+  return flat_ws_offset(B, N, T, Bt) + (size_t)B * N * T * 580 * sizeof(float);
 }
 
 }  // extern "C"
@@ -1856,7 +1875,7 @@ int egno_forward_impl(int frames, int flat, int B, int N, int T, int n_layers, i
   float* xB = hB + n * 64;
   float* etab = xB + n * 3;
   const int emb_ld = in_node + (t_in ? 2 : 1) * time_emb_dim;
-  float* flat_ws = (float*)((char*)workspace + nonode_egno_workspace_bytes(B, N, T, Bt));
+  float* flat_ws = (float*)((char*)workspace + flat_ws_offset(B, N, T, Bt));
   auto layer = [&](int l, const float* hi, const float* xi, float* ho, float* xo) {
     if (flat)
       return launch_flat_layer(T * B, N, n_edge_feat, frames ? T * B : B, hi, xi, v_out, edge_fea, blobs[l], ho, xo,

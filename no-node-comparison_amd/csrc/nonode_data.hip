@@ -60,9 +60,100 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(long long K, const flo
   }
 }
 
+// ---- the fully connected edge list (dataset_simple.py:64-71, 101-111) on the device ----
+// edge e = (b, i, k): b = e / (N (N-1)), receiver i, sender j = k + (k >= i); rows / cols int64
+__device__ __forceinline__ void full_edge(long long e, int N, long long& r, long long& c) {
+  const long long per = (long long)N * (N - 1);
+  const long long b = e / per;
+  const int rem = (int)(e - b * per);
+  const int i = rem / (N - 1), k = rem - i * (N - 1);
+  r = b * N + i;
+  c = b * N + k + (k >= i);
+}
+
+__global__ __launch_bounds__(256) void full_edges_kernel(long long E, int N, long long* rows, long long* cols) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < E; e += (long long)gridDim.x * 256) {
+    long long r, c;
+    full_edge(e, N, r, c);
+    rows[e] = r;
+    cols[e] = c;
+  }
+}
+
+// any edge that differs from full_edge() stores 1 to *flag (a plain vector store: every writer
+// stores the same value); the flag is never cleared here, so it accumulates over launches
+template <typename I>
+__global__ __launch_bounds__(256) void check_edges_kernel(long long E, int N, const I* rows, const I* cols, int* flag) {
+  bool bad = false;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < E; e += (long long)gridDim.x * 256) {
+    long long r, c;
+    full_edge(e, N, r, c);
+    bad |= ((long long)rows[e] != r) | ((long long)cols[e] != c);
+  }
+  if (bad) *(volatile int*)flag = 1;
+}
+
+struct PoisonArgs {
+  float* buf[4];
+  long long n[4];
+};
+
+// a forward's outputs to NaN when *flag is set (its edge list failed check_edges_kernel); every
+// workgroup reads the flag once and leaves at once when it is clear
+__global__ __launch_bounds__(256) void poison_kernel(const int* flag, PoisonArgs a) {
+  if (*(volatile const int*)flag == 0) return;
+  const float nan = __builtin_nanf("");
+  for (int k = 0; k < 4; ++k)
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < a.n[k]; i += (long long)gridDim.x * 256)
+      a.buf[k][i] = nan;
+}
+
 }  // namespace
 
 extern "C" {
+
+int nonode_full_edges(int B, int N, long long* rows, long long* cols, void* stream) {
+  if (B <= 0 || N < 2) return fail(NONODE_EINVAL, "full_edges: B=%d N=%d", B, N);
+  if (!rows || !cols) return fail(NONODE_EINVAL, "full_edges: null pointer");
+  const long long E = (long long)B * N * (N - 1);
+  long long g = (E + 255) / 256;
+  g = g < 2048 ? g : 2048;
+  hipLaunchKernelGGL(full_edges_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, E, N, rows, cols);
+  return check_launch("full_edges_kernel");
+}
+
+int nonode_check_full_edges(const void* rows, const void* cols, int idx_bytes, long long E, int B, int N, int* flag,
+                            void* stream) {
+  if (B <= 0 || N < 2 || E != (long long)B * N * (N - 1) || (idx_bytes != 4 && idx_bytes != 8))
+    return fail(NONODE_EINVAL, "check_full_edges: E=%lld B=%d N=%d idx_bytes=%d", E, B, N, idx_bytes);
+  if (!rows || !cols || !flag) return fail(NONODE_EINVAL, "check_full_edges: null pointer");
+  long long g = (E + 255) / 256;
+  g = g < 1024 ? g : 1024;
+  if (idx_bytes == 8)
+    hipLaunchKernelGGL(check_edges_kernel<long long>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, E, N,
+                       (const long long*)rows, (const long long*)cols, flag);
+  else
+    hipLaunchKernelGGL(check_edges_kernel<int>, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, E, N,
+                       (const int*)rows, (const int*)cols, flag);
+  return check_launch("check_edges_kernel");
+}
+
+int nonode_poison_if_flagged(const int* flag, int n_bufs, float* const* bufs, const long long* counts, void* stream) {
+  if (!flag || n_bufs < 0 || n_bufs > 4 || (n_bufs > 0 && (!bufs || !counts)))
+    return fail(NONODE_EINVAL, "poison_if_flagged: flag=%p n_bufs=%d", (const void*)flag, n_bufs);
+  PoisonArgs a{};
+  long long most = 0;
+  for (int k = 0; k < n_bufs; ++k) {
+    if (counts[k] < 0 || (counts[k] > 0 && !bufs[k])) return fail(NONODE_EINVAL, "poison_if_flagged: buffer %d", k);
+    a.buf[k] = bufs[k];
+    a.n[k] = counts[k];
+    most = counts[k] > most ? counts[k] : most;
+  }
+  long long g = (most + 255) / 256;
+  g = g < 1 ? 1 : (g < 256 ? g : 256);
+  hipLaunchKernelGGL(poison_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, flag, a);
+  return check_launch("poison_kernel");
+}
 
 int nonode_gather_rows(int S, long long K, int B, const float* src, const int* idx, float* dst, void* stream) {
   if (S <= 0 || K <= 0 || B <= 0) return fail(NONODE_EINVAL, "gather_rows: S=%d K=%lld B=%d", S, K, B);

@@ -12,7 +12,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .graph import check_full_graph
+from .graph import check_full_graph, finish
 
 
 class _MLP(nn.Module):
@@ -247,8 +247,8 @@ class EGNO(nn.Module):
             raise ValueError(f"edge_fea must be [{B * N * (N - 1)}, {self.in_edge_nf}], got {tuple(edge_fea.shape)}")
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) and self.training:
             from .autograd import egno_forward_train
-            return egno_forward_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N)
-        return self._forward_kernels(x, h, edge_fea, v, loc_mean, timesteps_out, B, N)
+            return finish(egno_forward_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
+        return finish(self._forward_kernels(x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
 
     def frame_inputs(self, T):
         """Input index of each of the T frames: repeat_elements_to_exact_shape (EGNO/utils.py:115-131)
@@ -287,11 +287,11 @@ class EGNO(nn.Module):
             t_out = f32(timesteps_out).contiguous()
         if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
             from .autograd import egno_forward_train
-            return egno_forward_train(self, xf, hf, eff, vf, lmf, t_out, B, N, t_in=t_in)
+            return finish(egno_forward_train(self, xf, hf, eff, vf, lmf, t_out, B, N, t_in=t_in))
         L = _lib.lib()
         with torch.no_grad():
-            return self._launch_forward(L.nonode_egno_forward_flat if self.flat else L.nonode_egno_forward_frames,
-                                        B, N, xf, hf, vf, lmf, eff, t_out, t_in=t_in)
+            return finish(self._launch_forward(L.nonode_egno_forward_flat if self.flat else L.nonode_egno_forward_frames,
+                                               B, N, xf, hf, vf, lmf, eff, t_out, t_in=t_in))
 
     def _no_flat_training(self):
         if self.flat:
@@ -302,7 +302,7 @@ class EGNO(nn.Module):
         """timesteps_out as f32 (cached per tensor/version: callers pass the same int64 tensor)."""
         if t_out.dtype == torch.float32 and t_out.is_contiguous():
             return t_out
-        key = (t_out.data_ptr(), t_out._version, tuple(t_out.shape), t_out.dtype)
+        key = (t_out.data_ptr(), t_out._version, tuple(t_out.shape), t_out.stride(), t_out.dtype, t_out.device)
         c = getattr(self, "_tcache", None)
         if c is not None and c[0] == key:
             return c[1]

@@ -149,6 +149,11 @@ def egno_rollout(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean
     if num_steps != T:
         raise ValueError("rollout_fn reshapes each segment into num_steps == model.num_timesteps frames")
     _lib.require_device(loc, nodes, vel, edge_attr, loc_mean, model.embedding.weight)
+    if model.flat:
+        # nonode_egno_rollout runs the 64-wide SiLU layer kernels on standard layer blobs only: a flat
+        # model (256-wide Tanh blobs, nonode_pack_layer_flat) rolls out segment by segment instead
+        return _egno_rollout_segments(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean, n_nodes,
+                                      traj_len, batch_size, charges, timesteps_in, timesteps_out, energy_dataset)
     B, N = batch_size, n_nodes
     BN, E = B * N, B * N * (N - 1)
     dev = loc.device
@@ -186,13 +191,45 @@ def egno_rollout(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean
 
 
 @torch.no_grad()
+def _egno_rollout_segments(model, nodes, loc, edges, vel, edge_attr_o, edge_attr, loc_mean, n_nodes, traj_len,
+                           batch_size, charges, timesteps_in, timesteps_out, energy_dataset):
+    """rollout_fn (main_simulation_simple_no.py:342-384), num_inputs == 1, as a loop of model(...)
+    segments: per segment the model's own forward (flat=True: nonode_egno_forward_flat), the frame
+    t_in - 1 of each sample re-featurised by prepare_inputs (loc_all[timesteps_in.T - 1]), and the
+    per-frame energies. Same returns as egno_rollout."""
+    T = model.num_timesteps
+    B, N = batch_size, n_nodes
+    BN = B * N
+    dev = loc.device
+    if timesteps_out is None:
+        timesteps_out = torch.arange(T * traj_len, device=dev).unsqueeze(0)
+    if timesteps_out.shape[1] != T * traj_len:
+        raise ValueError(f"timesteps_out must have {T * traj_len} columns")
+    ti = timesteps_in.reshape(-1) if timesteps_in is not None else None   # None: the last frame (t_in = T)
+    preds = torch.empty(traj_len * T, BN, 3, device=dev)
+    en_all = []
+    for i in range(traj_len):
+        t_out = timesteps_out[:, i * T:(i + 1) * T] - i * T
+        x, v, _ = model(loc, nodes, edges, edge_attr, v=vel, loc_mean=loc_mean, timesteps_out=t_out)
+        preds[i * T:(i + 1) * T] = x.reshape(T, BN, 3)
+        if energy_dataset is not None:
+            en_all.append(conserved_energy(energy_dataset, x.reshape(T, BN, 3), v.reshape(T, BN, 3), charges, B))
+        loc, vel, edge_attr, nodes, loc_mean = prepare_inputs(x.reshape(T, B, N, 3), v.reshape(T, B, N, 3),
+                                                              edge_attr_o, edges, N, 1, charges, t_in=ti)
+    if energy_dataset is None:
+        return preds, None, None
+    en_all = torch.cat(en_all).unsqueeze(-1)
+    return preds, en_all[T - 1::T], en_all
+
+
+@torch.no_grad()
 def segno_rollout(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps=10, charges=None,
                   energy_dataset=None, batch_size=None, in_steps=None):
     """rollout_fn (train_nbody.py:200-236): num_prev == 1 as one native call; several previous
     frames (loc, vel [BN, I, 3], in_steps) as a segment loop over SEGNO's multi-input forward.
 
     Returns (loc_preds [traj_len, BN, 3], energies [traj_len, B, 1] or None)."""
-    from .graph import check_full_graph
+    from .graph import check_full_graph, finish
     from .segno import SEGNO
     if not isinstance(model, SEGNO):
         raise TypeError("segno_rollout drives no_node_comparison_amd.SEGNO (its packed weights)")
@@ -226,6 +263,7 @@ def segno_rollout(model, h, loc, edge_index, vel, edge_attr, traj_len, num_steps
         _lib.ptr(ea), _lib.ptr(prod), 1, kind, _lib.ptr(q), _lib.ptr(ew), _lib.ptr(eb), _lib.ptr(blob),
         float(model.coords_weight), int(bool(model.recurrent)), _lib.ptr(preds), _lib.ptr(en), _lib.ptr(ws), ws_bytes,
         _lib.stream_of(x)))
+    finish((preds, en))
     return preds, (en.unsqueeze(-1) if en is not None else None)
 
 

@@ -20,7 +20,7 @@ import torch
 from torch import nn
 
 from . import _lib
-from .graph import check_full_graph
+from .graph import check_full_graph, finish
 
 
 class GCLParams(nn.Module):
@@ -169,7 +169,7 @@ class SEGNO(nn.Module):
             B, N = self._check_inputs(x, edges, v, edge_attr)
             _lib.require_device(his, self.embedding.weight)
             from .autograd import segno_train
-            return segno_train(self, his, x, v, edge_attr, int(T), B, N)
+            return finish(segno_train(self, his, x, v, edge_attr, int(T), B, N))
         return self._run(his, None, x, edges, v, edge_attr, int(T))
 
     def _forward_multi(self, his, x, edges, v, edge_attr, T, in_steps):
@@ -220,7 +220,7 @@ class SEGNO(nn.Module):
         _lib.require_device(h)
         B, N = self._check_inputs(x, edges, v, edge_attr)
         from .autograd import segno_step_train
-        return segno_step_train(self, h, x, v, edge_attr, T, B, N)
+        return finish(segno_step_train(self, h, x, v, edge_attr, T, B, N))
 
     def _check_inputs(self, x, edges, v, edge_attr):
         """(B, N) of a training call's fully connected graph, after the device and shape checks."""
@@ -269,4 +269,4 @@ class SEGNO(nn.Module):
             _lib.ptr(ea), _lib.ptr(ew), _lib.ptr(eb), _lib.ptr(blob), float(self.coords_weight),
             int(bool(self.recurrent)), _lib.ptr(x_out), _lib.ptr(v_out), _lib.ptr(h_out), _lib.ptr(ws),
             ws_bytes, _lib.stream_of(x)))
-        return x_out, h_out, v_out
+        return finish((x_out, h_out, v_out))

@@ -77,7 +77,13 @@ class FlatGrads:
     Every parameter's .grad is a view into one contiguous buffer (fp32 for the models), so autograd accumulates
     straight into it and the step needs a single all-reduce (sum) of the flat buffer (0.81 MB
     for EGNO) followed by a division by the world size: with equal shards this is the gradient of
-    the global mean loss. With world size 1 (or no process group) allreduce_ is a no-op."""
+    the global mean loss.
+
+    Return contract of allreduce_(): the reduced flat buffer at world size > 1; None at world size 1
+    (or without a process group), where there is nothing to exchange and the parameters keep
+    autograd's gradient tensors as they are (no copy into the buffer on the step's path). Reading
+    ``flat`` at any world size gathers first, so it always holds the gradients the optimizer will
+    step on (tests/test_sharding.py pins both)."""
 
     def __init__(self, params):
         self.params = [p for p in params if p.requires_grad]
@@ -85,20 +91,26 @@ class FlatGrads:
         dev, dt = self.params[0].device, self.params[0].dtype
         if any(p.dtype != dt or p.device != dev for p in self.params):
             raise ValueError("FlatGrads needs every parameter on one device with one dtype")
-        self.flat = torch.zeros(n, dtype=dt, device=dev)
+        self.numel = n
+        self._buf = torch.zeros(n, dtype=dt, device=dev)
         self.views = []
         off = 0
         for p in self.params:
-            self.views.append(self.flat[off:off + p.numel()].view_as(p))
+            self.views.append(self._buf[off:off + p.numel()].view_as(p))
             off += p.numel()
         self._bind()
+
+    @property
+    def flat(self):
+        """The flat gradient buffer, gathered from the parameters' current .grad first."""
+        return self.gather_()
 
     def _bind(self):
         for p, v in zip(self.params, self.views):
             p.grad = v
 
     def zero_(self):
-        self.flat.zero_()
+        self._buf.zero_()
         self._bind()
 
     def gather_(self):
@@ -110,12 +122,12 @@ class FlatGrads:
         stale = [i for i, (p, v) in enumerate(zip(self.params, self.views))
                  if p.grad is None or p.grad.data_ptr() != v.data_ptr()]
         if not stale:
-            return self.flat
+            return self._buf
         if len(stale) == len(self.params):
             # the usual case after zero_grad(): one concatenation into the buffer
             parts = [(p.grad if p.grad is not None else torch.zeros_like(v)).reshape(-1)
                      for p, v in zip(self.params, self.views)]
-            torch.cat(parts, out=self.flat)
+            torch.cat(parts, out=self._buf)
         else:
             for i in stale:
                 p, v = self.params[i], self.views[i]
@@ -124,19 +136,17 @@ class FlatGrads:
                 else:
                     v.copy_(p.grad)
         self._bind()
-        return self.flat
+        return self._buf
 
     def exchange_(self):
         """The step's one collective: sum of the flat buffer over the ranks, then / world size
         (runs at any world size; allreduce_ skips it when there is nothing to exchange)."""
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM)
-        self.flat.div_(dist.get_world_size())
-        return self.flat
+        dist.all_reduce(self._buf, op=dist.ReduceOp.SUM)
+        self._buf.div_(dist.get_world_size())
+        return self._buf
 
     def allreduce_(self):
-        """The step's exchange. With world size 1 (or no process group) there is nothing to reduce,
-        so the parameters keep autograd's gradient tensors as they are (no gather into the buffer)
-        and None is returned; otherwise the reduced flat buffer."""
+        """The step's exchange: the reduced flat buffer, or None at world size 1 (class docstring)."""
         if not _initialized() or dist.get_world_size() == 1:
             return None
         self.gather_()

@@ -13,6 +13,7 @@ import torch
 
 import no_node_comparison_amd as pkg
 from oracle import egno as oe
+from oracle import harness as oh
 from oracle import torch_ref as tr
 from tests.conftest import check_rel, load_golden, params_of
 from tests.test_gpu_parity import DEV, _dev, _egno_case
@@ -213,6 +214,66 @@ def test_egno_no_time_conv_rollout_first_segment_is_the_forward():
     torch.cuda.synchronize()
     assert torch.equal(preds[:T].reshape(-1, 3), x)
     assert bool(torch.isfinite(preds).all())
+
+
+def _rollout_case(B, N, T, seed):
+    case = _egno_case(B, N, T, seed=seed)
+    f64 = {k: (v.astype(np.float64) if v.dtype.kind == "f" else v) for k, v in case.items()}
+    eo = case["edge_fea"][:, :1].copy()          # edge_attr_o = q_i q_j (prepare_inputs appends |x_i - x_j|^2)
+    q = case["h"][:, 1:2].copy()                 # nodes = [|v|, q]
+    return case, f64, eo, q
+
+
+@pytest.mark.parametrize("name", ["flat", "flat_notc"])
+def test_egno_flat_rollout_matches_oracle(name):
+    """rollout_fn (main_simulation_simple_no.py:342-384, reachable with --flat through :231) on a
+    flat=True model. The one-call native rollout runs the 64-wide SiLU layer kernels only, so a flat
+    model rolls out segment by segment through its own forward (harness._egno_rollout_segments):
+    segment 0 is bitwise the flat forward, both segments (restarting from per-sample frames t_in - 1)
+    against the float64 oracle's rollout."""
+    B, N, T = 4, 20, 10
+    m = _egno(FLAT[name], seed=31).eval()
+    case, f64, eo, q = _rollout_case(B, N, T, seed=32)
+    inp = {k: _dev(v) for k, v in case.items()}
+    t_full = np.tile(np.arange(1, 2 * T + 1), (B, 1))
+    t_in = np.array([0, 3, 10, 7])
+    with torch.no_grad():
+        x, _, _ = _run(m, inp)
+        preds, en, en_all = pkg.harness.egno_rollout(
+            m, inp["h"], inp["x"], [inp["row"], inp["col"]], inp["v"], _dev(eo), inp["edge_fea"], inp["loc_mean"], N, 2,
+            B, charges=_dev(q), num_steps=T, timesteps_in=_dev(t_in), timesteps_out=_dev(t_full),
+            energy_dataset="charged")
+    torch.cuda.synchronize()
+    assert torch.equal(preds[:T].reshape(-1, 3), x)
+    assert en.shape == (2, B, 1) and en_all.shape == (2 * T, B, 1)
+    p = {k: v.detach().cpu().numpy().astype(np.float64) for k, v in m.state_dict().items()}
+    ref, ren, ren_all = oh.egno_rollout(p, f64["h"], f64["x"], case["row"], case["col"], f64["v"], eo.astype(np.float64),
+                                        f64["edge_fea"], f64["loc_mean"], N, 2, B, q.astype(np.float64), T=T,
+                                        t_out=t_full, t_in=t_in, **FLAT[name])
+    check_rel("flat preds[:T]", preds[:T].cpu(), ref[:T], TOL)
+    check_rel("flat preds", preds.cpu(), ref, 1e-4)     # segment 2 restarts from a random-init model's output
+    check_rel("flat en_all[:T]", en_all[:T].cpu(), ren_all[:T], 1e-5)
+
+
+def test_egno_segment_rollout_equals_native_rollout():
+    """The segment-loop rollout (the flat models' path) and the one-call native rollout compute the same
+    trajectories and energies on a standard model: same forward kernels, same featurisation kernel."""
+    B, N, T = 5, 20, 10
+    m = _egno({}, seed=33).eval()
+    case, _, eo, q = _rollout_case(B, N, T, seed=34)
+    inp = {k: _dev(v) for k, v in case.items()}
+    args = (m, inp["h"], inp["x"], [inp["row"], inp["col"]], inp["v"], _dev(eo), inp["edge_fea"], inp["loc_mean"], N,
+            3, B)
+    t_full = _dev(np.tile(np.arange(1, 3 * T + 1), (B, 1)))
+    t_in = _dev(np.array([0, 3, 10, 7, 1]))
+    with torch.no_grad():
+        a = pkg.harness.egno_rollout(*args, charges=_dev(q), num_steps=T, timesteps_in=t_in, timesteps_out=t_full,
+                                     energy_dataset="charged")
+        b = pkg.harness._egno_rollout_segments(*args, _dev(q), t_in, t_full, "charged")
+    torch.cuda.synchronize()
+    for name, u, w in zip(("preds", "energies", "energies_allsteps"), a, b):
+        assert u.shape == w.shape, name
+        check_rel(f"segments vs native {name}", w.cpu(), u.cpu().numpy(), 1e-6)
 
 
 @pytest.mark.parametrize("B,N,T", [(2, 5, 10), (16, 20, 10)])

@@ -435,9 +435,13 @@ def test_rejects_bad_inputs_loudly():
     m = _egno(params_of(fx))
     args = [_dev(fx["in::x"]), _dev(fx["in::h"]), [_dev(fx["in::col"]), _dev(fx["in::row"])],
             _dev(fx["in::edge_attr"])]
-    with pytest.raises(ValueError):
-        with torch.no_grad():
-            m(*args, v=_dev(fx["in::v"]), loc_mean=_dev(fx["in::loc_mean"]), timesteps_out=_dev(fx["in::t_out"]))
+    # swapped receiver / sender lists: checked on the device without blocking (graph.py); the call's
+    # outputs are NaN and the error is raised by the next boundary call or sync_checks()
+    with torch.no_grad():
+        out = m(*args, v=_dev(fx["in::v"]), loc_mean=_dev(fx["in::loc_mean"]), timesteps_out=_dev(fx["in::t_out"]))
+    assert all(torch.isnan(t).all() for t in out)
+    with pytest.raises(ValueError, match="fully connected"):
+        pkg.graph.sync_checks()
     with pytest.raises(ValueError):
         with torch.no_grad():
             m(*args[:2], [_dev(fx["in::row"]), _dev(fx["in::col"])], args[3], v=None,
@@ -542,3 +546,29 @@ def test_segno_multi_input_rollout_matches_reference_golden():
     check_rel("preds[0]", preds[0].cpu(), ro["out::loc_preds"][0], TOL)
     check_rel("preds", preds.cpu(), ro["out::loc_preds"], TOL)
     check_rel("en", en.cpu(), ro["out::energies"], TOL)
+
+
+@pytest.mark.parametrize("B", [64, 128, 256])
+def test_egno_small_batch_chunking_matches_f64_and_fill_rule(monkeypatch, B):
+    """The strong-scaling shards of C2 (B = 512 / 8, 4, 2 per GPU): inference forwards with few graphs
+    per CU take the critical-path chunk size (csrc/nonode.hip launch_layer; B = 64: 3-graph chunks on
+    214 workgroups instead of 2-graph chunks in two rounds). Same arithmetic per receiver, other sum
+    order: against the f64 torch path and the fill rule's result (NONODE_FILL_CG=1)."""
+    from oracle import torch_ref as tr
+    N, T = 20, 10
+    m = _egno(T=T, seed=B + 1)
+    x, nodes, edges, ea, v, lm, t, _ = _egno_full(B, N, T, seed=B + 2)
+    with torch.no_grad():
+        out = [o.clone() for o in m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)]
+        monkeypatch.setenv("NONODE_FILL_CG", "1")
+        fill = m(x, nodes, edges, ea, v=v, loc_mean=lm, timesteps_out=t)
+    for name, a, b in zip("xvh", out, fill):
+        check_rel(f"B={B} {name} critical-path vs fill chunks", a, b, 1e-6)
+    if B == 64:
+        p = {k: v_.detach().cpu().double() for k, v_ in m.state_dict().items()}
+        r, c = tr.full_edges(B, N)
+        d = lambda a: a.detach().cpu().double()  # noqa: E731
+        with torch.no_grad():
+            ref = tr.egno_forward(p, d(x), d(nodes), r, c, d(ea), d(v), d(lm), t.cpu(), T=T)
+        for name, a, b in zip("xvh", out, ref):
+            check_rel(f"B=64 {name} vs f64", a, b, TOL)

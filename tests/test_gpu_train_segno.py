@@ -227,3 +227,30 @@ def test_segno_multi_input_attn_gradients_match_f64_reference():
     lr.backward()
     assert abs(float(loss.detach()) - float(lr.detach())) <= 1e-5 * abs(float(lr.detach()))
     assert _check_grads(m, p, GTOL, "attn") == 17
+
+
+def test_segno_his_gradient_and_saved_input_version():
+    """SEGNO.forward in training (autograd.SEGNOTrain) with an input `his` that requires grad: dL/dhis
+    through the embedding Linear (model.py:73) against float64 autograd; and `his` is saved through
+    save_for_backward, so editing it in place after the forward raises instead of silently changing
+    the embedding weight gradient."""
+    B, N, T = 3, 7, 4
+    m = _segno(seed=11)
+    his, x, v, r, c, ea, target = _case(B, N, seed=12)
+    hd = _dev(his).requires_grad_(True)
+    m.zero_grad(set_to_none=True)
+    xo, _, _ = m(hd, _dev(x), [_dev(r), _dev(c)], _dev(v), _dev(ea), T=T)
+    torch.nn.functional.mse_loss(xo, _dev(target)).backward()
+    torch.cuda.synchronize()
+    dt = torch.float64
+    p = {k: q.detach().cpu().to(dt).requires_grad_(True) for k, q in m.state_dict().items()}
+    hr = his.to(dt).requires_grad_(True)
+    xr, _, _ = tr.segno_forward_step(p, hr, x.to(dt), r, c, v.to(dt), ea.to(dt), T=T, dense_mean=False)
+    torch.nn.functional.mse_loss(xr, target.to(dt)).backward()
+    check_rel("dL/dhis", hd.grad, hr.grad, GTOL)
+    assert _check_grads(m, p, GTOL, "his") == 14
+    h2 = _dev(his)
+    xo, _, _ = m(h2, _dev(x), [_dev(r), _dev(c)], _dev(v), _dev(ea), T=T)
+    h2.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        torch.nn.functional.mse_loss(xo, _dev(target)).backward()

@@ -91,6 +91,25 @@ def test_exchange_runs_at_world1_gloo():
     _run(1, _exchange_world1)
 
 
+def test_flatgrads_world1_contract():
+    """Without a process group (or at world size 1) allreduce_() exchanges nothing and returns None,
+    leaving autograd's gradient tensors in place; reading .flat still gives this step's gradients
+    (gathered on demand), also after zero_grad(set_to_none=True) dropped the views."""
+    from no_node_comparison_amd.sharding import FlatGrads
+    p = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(7))]
+    fg = FlatGrads(p)
+    assert fg.numel == 22
+    for q in p:
+        q.grad = None                       # optimizer.zero_grad() (torch 2.x default)
+    g = [torch.randn(5, 3), torch.randn(7)]
+    for q, gg in zip(p, g):
+        q.grad = gg.clone()
+    assert fg.allreduce_() is None
+    assert all(torch.equal(q.grad, gg) for q, gg in zip(p, g))
+    assert torch.equal(fg.flat, torch.cat([gg.reshape(-1) for gg in g]))
+    assert all(q.grad.data_ptr() == v.data_ptr() for q, v in zip(fg.params, fg.views))
+
+
 def _bench_shards(rank, world, B_per, N):
     import bench
     loc, vel, q = bench.rank_batch(B_per, world, rank, N, seed=99)
