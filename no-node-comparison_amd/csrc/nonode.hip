@@ -1196,6 +1196,11 @@ struct TconvArgs {
   // (column 16 tile + 4 wave + (l >> 4), channel 4 (l & 15) + q) of frame t. The backward uses these
   // decisions instead of recomputing y (a recompute near y = 0 can take the other branch).
   unsigned long long* mask_out;
+  // DFT twiddles cos / sin(2 pi m t / T), m < M, t < T, at [m * TMAX + t]: filled by launch_tconv on
+  // the host (double precision, exact at multiples of pi / 2) and read from the kernel arguments, so no
+  // workgroup computes them or waits on a barrier for them (round 5: software double cospi / sinpi per
+  // workgroup into LDS, then a barrier, ahead of the first h load)
+  float tw_cos[MMAX * TMAX], tw_sin[MMAX * TMAX];
 };
 
 // Packed mixing weights of one TimeConv (layer_no.py:80-126), as W^T fragments (f32 MFMA A operand)
@@ -1235,18 +1240,11 @@ __global__ void tconv_pack_kernel(TconvPackBatch tb, int Mfull, int M, int T) {
 template <bool FIRST, int MM, int TB>
 __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   __shared__ __attribute__((aligned(16))) float sX[2 * MM - 1][16][ROWP];
-  __shared__ float sCos[MM * TMAX], sSin[MM * TMAX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int T = p.T, M = p.M, BN = p.BN;
   const int ntiles = (BN + 15) / 16, tpx = (ntiles + 7) / 8;
   const int tile = p.xcd ? (int)(blockIdx.x % 8) * tpx + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   if (tile >= ntiles) return;   // whole workgroup, before any barrier
-  if (tid < M * T) {
-    const int m = tid / T, t = tid - (tid / T) * T;
-    const double ang = 2.0 * (double)m * (double)t / (double)T;
-    sCos[m * TMAX + t] = (float)cospi(ang);
-    sSin[m * TMAX + t] = (float)sinpi(ang);
-  }
   // x / v lanes and the mixing MFMAs: column e = lane & 15 of the tile
   const int col = tile * 16 + e;
   const bool cvalid = col < BN;
@@ -1278,7 +1276,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     if (FIRST) return *reinterpret_cast<const f4*>(et + t * 64) + (p.frames ? hin_part((size_t)t * BN + sc) : base);
     return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs);
   };
-  __syncthreads();
+
   // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
   if (wave == 3 && g < 3 && cvalid) {
     const int d = g;
@@ -1302,7 +1300,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 #pragma unroll
         for (int t = 0; t < TB; ++t) {
           if (t < T) {
-            const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
+            const float cs = p.tw_cos[m * TMAX + t], sn = p.tw_sin[m * TMAX + t];
             Xr[0] = fmaf(xs[t], cs, Xr[0]); Xi[0] = fmaf(-xs[t], sn, Xi[0]);
             Xr[1] = fmaf(vs[t], cs, Xr[1]); Xi[1] = fmaf(-vs[t], sn, Xi[1]);
           }
@@ -1330,7 +1328,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
           if (m < M) {
-            const float cs = sCos[m * TMAX + t], sn = sSin[m * TMAX + t];
+            const float cs = p.tw_cos[m * TMAX + t], sn = p.tw_sin[m * TMAX + t];
             y0 += yr[m][0] * cs - yi[m][0] * sn;
             y1 += yr[m][1] * cs - yi[m][1] * sn;
           }
@@ -1342,9 +1340,10 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     }
   }
   // ---- step 1: truncated DFT of this wave's input channels ----
-  // every frame's h is loaded once, up front and unconditionally (clamped frame index, see the x / v
-  // loads above), and kept in registers for the residual of step 3. (Issuing these loads before
-  // wave 3's x / v work measured 1 us slower per launch.)
+  // every frame's h is loaded once and unconditionally (clamped frame index, see the x / v loads
+  // above), and kept in registers for the residual of step 3. With no barrier ahead of them waves 0-2
+  // request these at the kernel's start; wave 3 after its x / v work (its loads hoisted above that work
+  // crashed LLVM's greedy register allocator on the TB = 16 instance; round 5 measured them 1 us slower)
   f4 hvs[TB];
 #pragma unroll
   for (int t = 0; t < TB; ++t) hvs[t] = hval(t < T ? t : T - 1);
@@ -1359,8 +1358,8 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
 #pragma unroll
         for (int m = 0; m < MM; ++m) {
           if (m < M) {
-            Xr[m] += hv * sCos[m * TMAX + t];
-            if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
+            Xr[m] += hv * p.tw_cos[m * TMAX + t];
+            if (m > 0) Xs[m] += hv * p.tw_sin[m * TMAX + t];
           }
         }
       }
@@ -1433,7 +1432,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       f4 y = Yr[0];
 #pragma unroll
       for (int m = 1; m < MM; ++m)
-        if (m < M) y += Yr[m] * sCos[m * TMAX + t] - Yi[m] * sSin[m * TMAX + t];
+        if (m < M) y += Yr[m] * p.tw_cos[m * TMAX + t] - Yi[m] * p.tw_sin[m * TMAX + t];
       f4 o = hvs[t];
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] += (y[q] >= 0.f ? y[q] : 0.01f * y[q]);
@@ -1594,7 +1593,16 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   // graphs give one round of 214 chunks. Training forwards keep the fill rule: their chunk shape must
   // not depend on the batch (batch-invariant sums of the data-parallel shards, §3.1 of DESIGN.md).
   const bool crit = steps == 1 && !m_out && !sv && n_graphs < 16 * cus && !getenv_int("NONODE_FILL_CG");
-  for (int c = 1; c <= (crit ? 8 * 16 : cap); ++c) {
+  const int force_cg = getenv_int("NONODE_CG");   // (diagnostic A/B switch: a fixed chunk size)
+  if (crit) best = -1e300;
+  for (int c = 1; c <= (crit || force_cg ? 8 * 16 : cap); ++c) {
+    if (force_cg) {
+      const int tiles = (c * N + 15) / 16;
+      if (tiles > 8 || layer_lds_floats(tiles, c * N) * 4 > LDS_MAX) break;
+      cg = c; ct = tiles;
+      if (c == force_cg) break;
+      continue;
+    }
     const int tiles = (c * N + 15) / 16;
     if (tiles > 8 || layer_lds_floats(tiles, c * N) * 4 > LDS_MAX) break;
     if (crit) {
@@ -1666,8 +1674,27 @@ int launch_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, const 
   return check_launch("egnn_layer_kernel");
 }
 
+// cos / sin(pi num / den) in double, exact where the angle is a multiple of pi / 2
+void cos_sin_pi(int num, int den, double& c, double& s) {
+  num %= 2 * den;
+  if ((2 * num) % den == 0) {
+    const int q = (2 * num) / den;   // quarter turns 0..3
+    const double cq[4] = {1.0, 0.0, -1.0, 0.0}, sq[4] = {0.0, 1.0, 0.0, -1.0};
+    c = cq[q]; s = sq[q];
+    return;
+  }
+  const double ang = 3.14159265358979323846 * (double)num / (double)den;
+  c = cos(ang); s = sin(ang);
+}
 int launch_tconv(bool first, const TconvArgs& a_in, hipStream_t stream) {
   TconvArgs a = a_in;
+  for (int m = 0; m < MMAX; ++m)
+    for (int t = 0; t < TMAX; ++t) {
+      double c = 0.0, sn = 0.0;
+      if (m < a.M && t < a.T) cos_sin_pi(2 * m * t, a.T, c, sn);
+      a.tw_cos[m * TMAX + t] = (float)c;
+      a.tw_sin[m * TMAX + t] = (float)sn;
+    }
   const int ntiles = (a.BN + 15) / 16;
   a.xcd = xcd_on() && ntiles >= 64;
   const int grid = a.xcd ? 8 * ((ntiles + 7) / 8) : ntiles;
