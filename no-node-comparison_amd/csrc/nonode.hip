@@ -1228,17 +1228,21 @@ __global__ void tconv_pack_kernel(TconvPackBatch tb, int Mfull, int M, int T) {
   out[d] = sgn * cm / (float)T * w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
 }
 
-// One workgroup (4 waves) per tile of 16 columns (b, n). Wave w: DFT over T of columns 4w..4w+3
+// One workgroup (4 + 1 waves) per tile of 16 columns (b, n). Wave w < 4: DFT over T of columns 4w..4w+3
 // (all 64 channels; each f4 access of the wave covers 4 whole rows), spectrum to LDS; then the
 // mixing MFMAs for output channels 16w..16w+15 of all 16 columns (lanes: column e = lane & 15,
 // channels 16w + 4g + q); the mixed spectrum goes back through LDS, and wave w finishes columns
 // 4w..4w+3: inverse DFT, LeakyReLU + residual (h kept in registers from the DFT), row stores.
+// Wave 4 does TimeConv_x (x / v, 48 lanes) beside them and only joins the barriers: with the x / v work
+// on a streaming wave (round 5: wave 3) that wave's h loads waited behind it, ~2 us on the launch's
+// critical path.
 // MM: compile-time bound on the number of modes (M <= MM), so the mode loops, the LDS spectrum and
 // the register arrays are sized for the configuration at hand
 // TB: compile-time bound on the frame count (T <= TB), so the per-frame register arrays and the
 // unconditional (clamped) loads cover only the frames a configuration can have (TB = 10 for T <= 10)
+constexpr int TC_THREADS = 320;
 template <bool FIRST, int MM, int TB>
-__global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
+__global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
   __shared__ __attribute__((aligned(16))) float sX[2 * MM - 1][16][ROWP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
   const int T = p.T, M = p.M, BN = p.BN;
@@ -1252,7 +1256,8 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   // h streaming (steps 1 and 3): wave w owns columns 4w .. 4w+3 of the tile, lane (cl = lane >> 4,
   // cq = lane & 15) channels 4cq .. 4cq+3 of column 4w + cl, so one f4 load / store instruction of a
   // wave moves 4 whole consecutive 256-byte rows (1 KB contiguous per frame)
-  const int ecol = 4 * wave + (lane >> 4), chs = 4 * (lane & 15);
+  const bool hw = wave < 4;   // the streaming waves (wave-uniform)
+  const int ecol = 4 * (hw ? wave : 0) + (lane >> 4), chs = 4 * (lane & 15);
   const int scol = tile * 16 + ecol;
   const bool svalid = scol < BN;
   const int sc = svalid ? scol : BN - 1;
@@ -1277,8 +1282,8 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     return *reinterpret_cast<const f4*>(p.h + ((size_t)t * BN + sc) * 64 + chs);
   };
 
-  // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 3, lane (d = g, column e), d < 3 ----
-  if (wave == 3 && g < 3 && cvalid) {
+  // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 4, lane (d = g, column e), d < 3 ----
+  if (wave == 4 && g < 3 && cvalid) {
     const int d = g;
     auto lm_at = [&](int t) { return p.lm[((p.frames ? (size_t)t * BN : 0) + c) * 3 + d]; };
     float xs[TB], vs[TB], lms[TB];
@@ -1341,13 +1346,16 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
   }
   // ---- step 1: truncated DFT of this wave's input channels ----
   // every frame's h is loaded once and unconditionally (clamped frame index, see the x / v loads
-  // above), and kept in registers for the residual of step 3. With no barrier ahead of them waves 0-2
-  // request these at the kernel's start; wave 3 after its x / v work (its loads hoisted above that work
-  // crashed LLVM's greedy register allocator on the TB = 16 instance; round 5 measured them 1 us slower)
+  // above), and kept in registers for the residual of step 3. With no barrier and no x / v work ahead
+  // of them, waves 0-3 request these at the kernel's start. (Placed above the x / v block in the source,
+  // their live range spans it in every wave, which crashed LLVM's greedy register allocator on the
+  // TB = 16 instance.)
   f4 hvs[TB];
+  if (hw) {
 #pragma unroll
-  for (int t = 0; t < TB; ++t) hvs[t] = hval(t < T ? t : T - 1);
-  {
+    for (int t = 0; t < TB; ++t) hvs[t] = hval(t < T ? t : T - 1);
+  }
+  if (hw) {
     f4 Xr[MM], Xs[MM];
 #pragma unroll
     for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
@@ -1374,7 +1382,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     }
   }
   __syncthreads();
-  // ---- step 2: channel mixing on MFMA (output tile mo = wave) ----
+  // ---- step 2: channel mixing on MFMA (output tile mo = wave, waves 0-3) ----
   f4 Yr[MM], Yi[MM];
   auto mix = [&](f4& acc, int mat, int vec) {
     f4 in[4];
@@ -1387,24 +1395,26 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
       for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
     }
   };
-  Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
-  mix(Yr[0], 0, 0);
+  if (hw) {
+    Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
+    mix(Yr[0], 0, 0);
 #pragma unroll
-  for (int m = 1; m < MM; ++m) {
-    if (m < M) {
-      const int mat = 1 + 3 * (m - 1);
-      Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
-      Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
-      mix(Yr[m], mat + 0, 2 * m - 1);   // A^T Xr
-      mix(Yr[m], mat + 1, 2 * m);       // B^T Xs
-      mix(Yi[m], mat + 1, 2 * m - 1);   // B^T Xr
-      mix(Yi[m], mat + 2, 2 * m);       // -A^T Xs
+    for (int m = 1; m < MM; ++m) {
+      if (m < M) {
+        const int mat = 1 + 3 * (m - 1);
+        Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
+        Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
+        mix(Yr[m], mat + 0, 2 * m - 1);   // A^T Xr
+        mix(Yr[m], mat + 1, 2 * m);       // B^T Xs
+        mix(Yi[m], mat + 1, 2 * m - 1);   // B^T Xr
+        mix(Yi[m], mat + 2, 2 * m);       // -A^T Xs
+      }
     }
   }
   // ---- the spectrum Y back through LDS into the streaming layout (sX is free once every wave's
   // mixing has read it) ----
   __syncthreads();
-  {
+  if (hw) {
     const int chm = 16 * wave + 4 * g;   // MFMA output channels of column e
     *reinterpret_cast<f4*>(&sX[0][e][chm]) = Yr[0];
 #pragma unroll
@@ -1416,6 +1426,7 @@ __global__ __launch_bounds__(256) void tconv_kernel(TconvArgs p) {
     }
   }
   __syncthreads();
+  if (!hw) return;   // (no barrier follows)
   // ---- step 3: y[t] (channels chs..chs+3 of column ecol), LeakyReLU(0.01), residual ----
   // (lanes of columns past BN compute on the clamped column sc and store nothing)
   Yr[0] = *reinterpret_cast<const f4*>(&sX[0][ecol][chs]);
@@ -1700,8 +1711,8 @@ int launch_tconv(bool first, const TconvArgs& a_in, hipStream_t stream) {
   const int grid = a.xcd ? 8 * ((ntiles + 7) / 8) : ntiles;
   ProfScope prof(first ? 3 : 2, stream);
   auto go = [&](auto kt, auto kf) {
-    if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(256), 0, stream, a);
-    else hipLaunchKernelGGL(kf, dim3(grid), dim3(256), 0, stream, a);
+    if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(TC_THREADS), 0, stream, a);
+    else hipLaunchKernelGGL(kf, dim3(grid), dim3(TC_THREADS), 0, stream, a);
   };
   if (a.T <= 10) {
     if (a.M <= 2) go(tconv_kernel<true, 2, 10>, tconv_kernel<false, 2, 10>);
