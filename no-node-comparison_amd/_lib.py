@@ -68,6 +68,30 @@ class LayerGrads(ctypes.Structure):
 _lib = None
 _packed_modules = weakref.WeakSet()
 _step_hook = None
+_param_gen = 0   # bumped whenever any module registers a parameter or a submodule (param_list)
+
+
+def _bump_param_gen(*args):
+    global _param_gen
+    _param_gen += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_param_gen)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_param_gen)
+
+
+def param_list(module, key, build):
+    """The list build() returns (a module-tree traversal such as [p for l in layers for p in
+    l.parameters()]), cached per module and key. The traversal was ~70% of the host time of a forward
+    (tools/host_profile.py); the cache is rebuilt after any parameter or submodule registration anywhere
+    (torch's global registration hooks), so a Parameter assigned to a module attribute is never missed."""
+    cache = module.__dict__.setdefault("_nonode_plists", {})
+    hit = cache.get(key)
+    if hit is not None and hit[0] == _param_gen:
+        return hit[1]
+    lst = build()
+    cache[key] = (_param_gen, lst)
+    return lst
 
 
 def track_packs(module):

@@ -152,8 +152,8 @@ class EGNO(nn.Module):
         """Packed kernel weights (layer blobs, TimeConv blobs or None without time convolutions),
         rebuilt whenever a parameter changed in place (optimizer step) or moved (flat: the flat
         layer blobs of nonode_pack_layer_flat)."""
-        params = [p for l in self.layers for p in l.parameters()] + \
-            ([m.t_conv.weights1 for m in self.time_conv_modules] if self.use_time_conv else [])
+        params = _lib.param_list(self, "pack", lambda: [p for l in self.layers for p in l.parameters()] + (
+            [m.t_conv.weights1 for m in self.time_conv_modules] if self.use_time_conv else []))
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._blobs is not None and key == self._blob_key:
             return self._blobs
@@ -193,6 +193,25 @@ class EGNO(nn.Module):
         tcx = [m.t_conv.weights1.detach().to(torch.float32).contiguous() for m in self.time_conv_x_modules]
         return (P(*[tblobs[i].data_ptr() for i in range(self.n_layers)]), P(*[t.data_ptr() for t in tcx]), tcx)
 
+    def _launch_arrays(self, blobs, tblobs):
+        """(layer blob pointers, tconv_arrays(...)) of a forward launch, cached while the packed blobs and
+        the TimeConv_x parameters' storage stay the same (the kernels read those parameters live, so an
+        in-place optimizer step needs no rebuild); rebuilt per call if a TimeConv_x weight is not fp32
+        contiguous (tconv_arrays then points at a converted copy)."""
+        tcx = _lib.param_list(self, "tcx", lambda: [m.t_conv.weights1 for m in self.time_conv_x_modules]
+                              if self.use_time_conv else [])
+        if not all(t.dtype == torch.float32 and t.is_contiguous() for t in tcx):
+            P = ctypes.c_void_p * self.n_layers
+            return P(*[blobs[i].data_ptr() for i in range(self.n_layers)]), self.tconv_arrays(tblobs)
+        key = (blobs.data_ptr(), tblobs.data_ptr() if tblobs is not None else 0, tuple(t.data_ptr() for t in tcx))
+        c = getattr(self, "_larrays", None)
+        if c is not None and c[0] == key and c[1] is blobs:
+            return c[2]
+        P = ctypes.c_void_p * self.n_layers
+        arrays = (P(*[blobs[i].data_ptr() for i in range(self.n_layers)]), self.tconv_arrays(tblobs))
+        self._larrays = (key, blobs, arrays)
+        return arrays
+
     def layer_param_names(self, i):
         """Parameter names of layer i in nonode_layer_weights / nonode_layer_grads field order."""
         pre = f"layers.{i}."
@@ -201,7 +220,7 @@ class EGNO(nn.Module):
 
     def _packed_bwd(self):
         """Backward fragments (unscaled forward + transposed) per layer, rebuilt like _packed()."""
-        params = [p for l in self.layers for p in l.parameters()]
+        params = _lib.param_list(self, "pack_bwd", lambda: [p for l in self.layers for p in l.parameters()])
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._bblobs is not None and key == self._bblob_key:
             return self._bblobs
@@ -228,7 +247,7 @@ class EGNO(nn.Module):
         if v is None or (loc_mean is None and self.use_time_conv):
             raise ValueError("EGNO.forward needs v and loc_mean (the time convolution stacks "
                              "x - loc_mean with v, egno.py:103-105)")
-        if self.flat and self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+        if self.flat and self._trains():
             self._no_flat_training()
         if self.num_inputs > 1:
             return self._forward_multi(x, h, edge_index, edge_fea, v, loc_mean, timesteps_in, timesteps_out)
@@ -245,10 +264,15 @@ class EGNO(nn.Module):
         B, N = check_full_graph(edge_index, BN)
         if edge_fea.shape != (B * N * (N - 1), self.in_edge_nf):
             raise ValueError(f"edge_fea must be [{B * N * (N - 1)}, {self.in_edge_nf}], got {tuple(edge_fea.shape)}")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) and self.training:
+        if self._trains():
             from .autograd import egno_forward_train
             return finish(egno_forward_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
         return finish(self._forward_kernels(x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
+
+    def _trains(self):
+        """Training forward: train mode, gradients enabled and a parameter that requires grad."""
+        return self.training and torch.is_grad_enabled() and any(
+            p.requires_grad for p in _lib.param_list(self, "all", lambda: list(self.parameters())))
 
     def frame_inputs(self, T):
         """Input index of each of the T frames: repeat_elements_to_exact_shape (EGNO/utils.py:115-131)
@@ -285,7 +309,7 @@ class EGNO(nn.Module):
             xf, hf, vf, lmf, eff = (per_frame(t) for t in (x, h, v, loc_mean, edge_fea))
             t_in = f32(timesteps_in)[:, fidx].contiguous()
             t_out = f32(timesteps_out).contiguous()
-        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+        if self._trains():
             from .autograd import egno_forward_train
             return finish(egno_forward_train(self, xf, hf, eff, vf, lmf, t_out, B, N, t_in=t_in))
         L = _lib.lib()
@@ -332,10 +356,8 @@ class EGNO(nn.Module):
         ws_bytes = (L.nonode_egno_flat_workspace_bytes if self.flat else L.nonode_egno_workspace_bytes)(
             B, N, T, tt.shape[0])
         ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=dev)
-        P = ctypes.c_void_p * self.n_layers
-        blob_p = P(*[blobs[i].data_ptr() for i in range(self.n_layers)])
-        tcw_p, tcx_p, _keep = self.tconv_arrays(tblobs)
-        f32 = lambda t: t.detach().to(torch.float32).contiguous()  # noqa: E731
+        blob_p, (tcw_p, tcx_p, _keep) = self._launch_arrays(blobs, tblobs)
+        f32 = lambda t: t if t.dtype == torch.float32 and t.is_contiguous() else t.detach().to(torch.float32).contiguous()  # noqa: E731,E501
         ew, eb = f32(self.embedding.weight), f32(self.embedding.bias)
         tail = (_lib.ptr(ew), _lib.ptr(eb), blob_p, tcw_p, tcx_p, _lib.ptr(x_out), _lib.ptr(v_out),
                 _lib.ptr(h_out), _lib.ptr(ws), ws_bytes, _lib.stream_of(x))

@@ -117,7 +117,7 @@ class SEGNO(nn.Module):
 
     def _packed_bwd(self):
         """Backward fragments of the GCL (unscaled forward + transposed), rebuilt like _packed()."""
-        params = list(self.module.parameters())
+        params = _lib.param_list(self, "gcl", lambda: list(self.module.parameters()))
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._bblob is not None and key == self._bblob_key:
             return self._bblob
@@ -133,10 +133,11 @@ class SEGNO(nn.Module):
         return _lib.VARIANT_SEGNO | (_lib.LAYER_TANH_COORD if self.tanh else 0)
 
     def _training(self):
-        return self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+        return self.training and torch.is_grad_enabled() and any(
+            p.requires_grad for p in _lib.param_list(self, "all", lambda: list(self.parameters())))
 
     def _packed(self):
-        params = list(self.module.parameters())
+        params = _lib.param_list(self, "gcl", lambda: list(self.module.parameters()))
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._blob is not None and key == self._blob_key:
             return self._blob

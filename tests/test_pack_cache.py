@@ -47,3 +47,21 @@ def test_unrelated_optimizer_keeps_packs():
     m._blob_key = ("kept",)
     _step(torch.optim.SGD(other.parameters(), lr=0.1), list(other.parameters()))
     assert m._blob_key == ("kept",)
+
+
+def test_cached_parameter_lists_follow_parameter_replacement():
+    """The host path caches its module-tree traversals (_lib.param_list: the packed-weight key's parameter
+    list); assigning a new Parameter or submodule anywhere invalidates every cache, so the pack key then
+    covers the new tensor (a stale list would keep packing the replaced one)."""
+    from no_node_comparison_amd import _lib
+    m = _egno()
+    build = lambda: [p for l in m.layers for p in l.parameters()]  # noqa: E731
+    a = _lib.param_list(m, "t", build)
+    assert _lib.param_list(m, "t", build) is a                      # cached
+    new = torch.nn.Parameter(torch.zeros_like(m.layers[0].coord_net.mlp[0].weight))
+    m.layers[0].coord_net.mlp[0].weight = new
+    b = _lib.param_list(m, "t", build)
+    assert b is not a and any(p is new for p in b)
+    m.layers[1] = type(m.layers[1])(2, 64)                          # a replaced submodule
+    c = _lib.param_list(m, "t", build)
+    assert c is not b and any(p is m.layers[1].node_net.mlp[0].weight for p in c)
