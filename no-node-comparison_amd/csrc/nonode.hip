@@ -1015,8 +1015,14 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)
         load_sx(xI, vI, ns0, nS);
       }
       const int J = ctc + (has_next ? proj_jobs(nrb, nne, nS) : 0);
-      constexpr int C_COST = 4;
-      const int A_COST = p.cpg == 1 ? 2 : 1;
+#ifndef NONODE_C_COST
+#define NONODE_C_COST 4   // (A/B builds: the node-update job's modelled cost in projection-job units x 2)
+#endif
+#ifndef NONODE_A_COST
+#define NONODE_A_COST 2
+#endif
+      constexpr int C_COST = NONODE_C_COST;
+      const int A_COST = p.cpg == 1 ? NONODE_A_COST : 1;
       int ld[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) ld[i] = 0;

@@ -19,8 +19,15 @@ constexpr size_t tconv_bwd_lds_bytes(int MM) {
   return ((size_t)tb_groups(MM) * (4 * MM - 1) * 16 * ROWP + 2 * (size_t)MM * TMAX +
           (tb_wlds(MM) ? (size_t)2 * MM * 4096 : 0)) * sizeof(float);
 }
-template <int MM>
+// TB: compile-time frame bound (10 for T <= 10, else TMAX), in chunks of TC frames: each chunk's loads
+// (h, the output gradient and its LeakyReLU mask words) are issued together, unconditionally with the
+// frame index clamped to T - 1, before any of them is used. (Round 5's loads sat under `if (t < T)`
+// inside a TMAX-frame loop: every frame became a branch, a single load and a wait, i.e. one memory
+// latency per frame in steps 3 and 4.)
+template <int MM, int TB>
 __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwdArgs p) {
+  constexpr int TC = TB % 5 == 0 ? 5 : 4;
+  static_assert(TB % TC == 0, "whole frame chunks");
   constexpr int NG = tb_groups(MM);
   static_assert(NG == 1 || 4096 <= (size_t)NG * (4 * MM - 1) * 16 * ROWP, "accumulator hand-off space");
   extern __shared__ __attribute__((aligned(16))) float tb_smem[];
@@ -67,13 +74,19 @@ __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwd
 #pragma unroll
       for (int m = 0; m < MM; ++m) { Xr[m] = f4{0.f, 0.f, 0.f, 0.f}; Xs[m] = Xr[m]; }
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          const f4 hv = hval(p.h, t);
+      for (int t0 = 0; t0 < TB; t0 += TC) {
+        f4 hv[TC];
 #pragma unroll
-          for (int m = 0; m < MM; ++m) {
-            Xr[m] += hv * sCos[m * TMAX + t];
-            if (m > 0) Xs[m] += hv * sSin[m * TMAX + t];
+        for (int i = 0; i < TC; ++i) hv[i] = hval(p.h, t0 + i < T ? t0 + i : T - 1);
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int t = t0 + i;
+          if (t < T) {
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+              Xr[m] += hv[i] * sCos[m * TMAX + t];
+              if (m > 0) Xs[m] += hv[i] * sSin[m * TMAX + t];
+            }
           }
         }
       }
@@ -108,15 +121,27 @@ __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwd
 #pragma unroll
       for (int m = 0; m < MM; ++m) { gR[m] = f4{0.f, 0.f, 0.f, 0.f}; gI[m] = gR[m]; }
 #pragma unroll
-      for (int t = 0; t < TMAX; ++t) {
-        if (t < T) {
-          f4 gy = hval(p.gout, t);
+      for (int t0 = 0; t0 < TB; t0 += TC) {
+        f4 gy[TC];
+        unsigned long long mw[TC][4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) gy[q] *= ((mrow[t * mstride + q] >> mbit) & 1) ? 1.f : 0.01f;
+        for (int i = 0; i < TC; ++i) {
+          const int tc = t0 + i < T ? t0 + i : T - 1;
+          gy[i] = hval(p.gout, tc);
 #pragma unroll
-          for (int m = 0; m < MM; ++m) {
-            gR[m] += gy * sCos[m * TMAX + t];
-            gI[m] -= gy * sSin[m * TMAX + t];
+          for (int q = 0; q < 4; ++q) mw[i][q] = mrow[tc * mstride + q];
+        }
+#pragma unroll
+        for (int i = 0; i < TC; ++i) {
+          const int t = t0 + i;
+          if (t < T) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gy[i][q] *= ((mw[i][q] >> mbit) & 1) ? 1.f : 0.01f;
+#pragma unroll
+            for (int m = 0; m < MM; ++m) {
+              gR[m] += gy[i] * sCos[m * TMAX + t];
+              gI[m] -= gy[i] * sSin[m * TMAX + t];
+            }
           }
         }
       }
@@ -145,12 +170,18 @@ __global__ __launch_bounds__(256 * tb_groups(MM)) void tconv_bwd_kernel(TconvBwd
       }
       if (cvalid) {
 #pragma unroll
-        for (int t = 0; t < TMAX; ++t) {
-          if (t < T) {
-            f4 o = hval(p.gout, t);
+        for (int t0 = 0; t0 < TB; t0 += TC) {
+          f4 o[TC];
 #pragma unroll
-            for (int m = 0; m < MM; ++m) o += gXr[m] * sCos[m * TMAX + t] - gXi[m] * sSin[m * TMAX + t];
-            *reinterpret_cast<f4*>(p.gh + ((size_t)t * BN + c) * 64 + ch) = o;
+          for (int i = 0; i < TC; ++i) o[i] = hval(p.gout, t0 + i < T ? t0 + i : T - 1);
+#pragma unroll
+          for (int i = 0; i < TC; ++i) {
+            const int t = t0 + i;
+            if (t < T) {
+#pragma unroll
+              for (int m = 0; m < MM; ++m) o[i] += gXr[m] * sCos[m * TMAX + t] - gXi[m] * sSin[m * TMAX + t];
+              *reinterpret_cast<f4*>(p.gh + ((size_t)t * BN + c) * 64 + ch) = o[i];
+            }
           }
         }
       }
@@ -222,10 +253,15 @@ int launch_tconv_bwd(int M, TconvBwdArgs a, int G, hipStream_t s) {
     constexpr int MM = decltype(mm)::value;
     static std::once_flag once;
     std::call_once(once, [] {
-      hipFuncSetAttribute((const void*)tconv_bwd_kernel<MM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute((const void*)tconv_bwd_kernel<MM, 10>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)tconv_bwd_lds_bytes(MM));
+      hipFuncSetAttribute((const void*)tconv_bwd_kernel<MM, TMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)tconv_bwd_lds_bytes(MM));
     });
-    hipLaunchKernelGGL(tconv_bwd_kernel<MM>, dim3(G), dim3(256 * tb_groups(MM)), tconv_bwd_lds_bytes(MM), s, a);
+    if (a.T <= 10)
+      hipLaunchKernelGGL((tconv_bwd_kernel<MM, 10>), dim3(G), dim3(256 * tb_groups(MM)), tconv_bwd_lds_bytes(MM), s, a);
+    else
+      hipLaunchKernelGGL((tconv_bwd_kernel<MM, TMAX>), dim3(G), dim3(256 * tb_groups(MM)), tconv_bwd_lds_bytes(MM), s, a);
   };
   switch (M) {
     case 1: go(std::integral_constant<int, 1>{}); break;

@@ -1497,8 +1497,12 @@ __device__ __forceinline__ void tconvx_grad_finish(const float* part, int nb, in
 // TimeConv_x: X0 = [x - lm, v] per spatial dim, 2 channels, no activation. Writes gx, gv.
 // One thread per (column c, coordinate d); the block sums its threads' weight-gradient terms in a
 // fixed order and writes one row of 2*2*MMAX_T*2 partials (tconvx_grad_finish adds the blocks' rows).
+// TB: compile-time frame bound (10 for T <= 10, else TMAX): the per-frame arrays are registers indexed
+// by unrolled loops, and every frame's loads are issued up front, unconditionally with the frame index
+// clamped to T - 1 (round 5 looped over a runtime T: per-frame loads behind a loop the compiler could not
+// unroll, one memory latency per frame)
 constexpr int TX_THREADS = 128;
-template <int MM>
+template <int MM, int TB>
 __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, int M, int Mfull, const float* x,
                                                                 const float* v, const float* lm, const float* gxo,
                                                                 const float* gvo, const float* w, float* gx,
@@ -1527,20 +1531,35 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
 #pragma unroll
   for (int k = 0; k < CNT; ++k) pp[k] = 0.f;
   if (valid) {
-    float X[2][TMAX], G[2][TMAX], GO[2][TMAX];
-    for (int t = 0; t < T; ++t) {
-      const size_t row = (size_t)t * BN + c;
+    float X[2][TB], G[2][TB], GO[2][TB];
+#pragma unroll
+    for (int t = 0; t < TB; ++t) {
+      const size_t row = (size_t)(t < T ? t : T - 1) * BN + c;
       X[0][t] = x[row * 3 + d] - lm[(frames ? row : (size_t)c) * 3 + d];
       X[1][t] = v[row * 3 + d];
       GO[0][t] = G[0][t] = gxo[row * 3 + d];
       GO[1][t] = G[1][t] = gvo[row * 3 + d];
     }
+    // the 2 x 2 complex weights of every mode, requested before the mode loop (m clamped to M - 1)
+    float wre[2][2][MM], wim[2][2][MM];
+#pragma unroll
+    for (int m = 0; m < MM; ++m)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const int mc = m < M ? m : M - 1;
+          wre[i][o][m] = w[((i * 2 + o) * Mfull + mc) * 2 + 0];
+          wim[i][o][m] = w[((i * 2 + o) * Mfull + mc) * 2 + 1];
+        }
 #pragma unroll
     for (int m = 0; m < MM; ++m) {
       if (m >= M) break;
       const float cm = ((m == 0 || 2 * m == T) ? 1.f : 2.f) / (float)T;
       float Xr[2] = {0.f, 0.f}, Xi[2] = {0.f, 0.f}, gYr[2] = {0.f, 0.f}, gYi[2] = {0.f, 0.f};
-      for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int t = 0; t < TB; ++t) {
+        if (t >= T) break;
         const float cs = sCs[m * TMAX + t], sn = sSn[m * TMAX + t];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1553,16 +1572,22 @@ __global__ __launch_bounds__(TX_THREADS) void tconvx_bwd_kernel(int BN, int T, i
         float gxr = 0.f, gxi = 0.f;
 #pragma unroll
         for (int o = 0; o < 2; ++o) {
-          const float wr = w[((i * 2 + o) * Mfull + m) * 2 + 0], wi = w[((i * 2 + o) * Mfull + m) * 2 + 1];
+          const float wr = wre[i][o][m], wi = wim[i][o][m];
           gxr += gYr[o] * wr + gYi[o] * wi;
           gxi += -gYr[o] * wi + gYi[o] * wr;
           pp[((i * 2 + o) * MM + m) * 2 + 0] = Xr[i] * gYr[o] + Xi[i] * gYi[o];
           pp[((i * 2 + o) * MM + m) * 2 + 1] = -Xi[i] * gYr[o] + Xr[i] * gYi[o];
         }
-        for (int t = 0; t < T; ++t) G[i][t] += gxr * sCs[m * TMAX + t] - gxi * sSn[m * TMAX + t];
+#pragma unroll
+        for (int t = 0; t < TB; ++t) {
+          if (t >= T) break;
+          G[i][t] += gxr * sCs[m * TMAX + t] - gxi * sSn[m * TMAX + t];
+        }
       }
     }
-    for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int t = 0; t < TB; ++t) {
+      if (t >= T) break;
       const size_t row = (size_t)t * BN + c;
       gx[row * 3 + d] = G[0][t];
       gv[row * 3 + d] = G[1][t];
@@ -2161,7 +2186,8 @@ int tconv_reverse(const TconvRev& r, const BwdWs& w, hipStream_t s, const Deferr
   // g_txw [2][2][Mfull][2]: one partial row per tconvx block, added in block order (modes >= M zero)
   const int nbx = (BN * 3 + TX_THREADS - 1) / TX_THREADS;
   // mode-bound builds: 2 (C4), 4, 9 (registers of the per-thread partials)
-  auto txk = M <= 2 ? tconvx_bwd_kernel<2> : (M <= 4 ? tconvx_bwd_kernel<4> : tconvx_bwd_kernel<MMAX_T>);
+  auto txk = T <= 10 ? (M <= 2 ? tconvx_bwd_kernel<2, 10> : (M <= 4 ? tconvx_bwd_kernel<4, 10> : tconvx_bwd_kernel<MMAX_T, 10>))
+                    : (M <= 2 ? tconvx_bwd_kernel<2, TMAX> : (M <= 4 ? tconvx_bwd_kernel<4, TMAX> : tconvx_bwd_kernel<MMAX_T, TMAX>));
   // (+ the workgroups that pack the TimeConv backward's fragments, tconv_pack_bwd)
   const int npack = (M * 2 * 4096 + TX_THREADS - 1) / TX_THREADS;
   hipLaunchKernelGGL(txk, dim3(nbx + npack), dim3(TX_THREADS), 0, s, BN, T, M, modes, r.xs, r.vs,
