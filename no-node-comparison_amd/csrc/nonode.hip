@@ -1197,6 +1197,7 @@ struct TconvArgs {
   // repeat_elements_to_exact_shape does); 0: x, v, h_in, loc_mean are [BN] rows replicated over T
   int frames;
   int xcd;   // 1: workgroup k runs tile (k % 8) * ceil(tiles / 8) + k / 8 (XCD-aware order)
+  int xw;    // 1: TimeConv_x on a fifth wave (launch_tconv: fewer tiles than CUs), else on wave 3
   // training forward only (else null): the LeakyReLU decision of every h element, y > 0, as the
   // wave ballots of step 3: mask[((t * ntiles + tile) * 4 + wave) * 4 + q] bit l = element
   // (column 16 tile + 4 wave + (l >> 4), channel 4 (l & 15) + q) of frame t. The backward uses these
@@ -1239,9 +1240,11 @@ __global__ void tconv_pack_kernel(TconvPackBatch tb, int Mfull, int M, int T) {
 // mixing MFMAs for output channels 16w..16w+15 of all 16 columns (lanes: column e = lane & 15,
 // channels 16w + 4g + q); the mixed spectrum goes back through LDS, and wave w finishes columns
 // 4w..4w+3: inverse DFT, LeakyReLU + residual (h kept in registers from the DFT), row stores.
-// Wave 4 does TimeConv_x (x / v, 48 lanes) beside them and only joins the barriers: with the x / v work
-// on a streaming wave (round 5: wave 3) that wave's h loads waited behind it, ~2 us on the launch's
-// critical path.
+// TimeConv_x (x / v, 48 lanes) runs on wave 3 after its h loads are issued, or, for launches with fewer
+// tiles than CUs (TconvArgs::xw, the strong-scaling shards), on a fifth wave that only joins the
+// barriers: there wave 3's h loads waiting behind the x / v work were on the launch's critical path
+// (C2 at B = 64: 0.2213 -> 0.2183 ms per forward); at B = 512, where every CU holds 2-3 tiles, the
+// fifth wave measured +15 us per forward (0.915 -> 0.931 ms, profiles/r06/ab_tconv_waves.txt).
 // MM: compile-time bound on the number of modes (M <= MM), so the mode loops, the LDS spectrum and
 // the register arrays are sized for the configuration at hand
 // TB: compile-time bound on the frame count (T <= TB), so the per-frame register arrays and the
@@ -1263,6 +1266,7 @@ __global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
   // cq = lane & 15) channels 4cq .. 4cq+3 of column 4w + cl, so one f4 load / store instruction of a
   // wave moves 4 whole consecutive 256-byte rows (1 KB contiguous per frame)
   const bool hw = wave < 4;   // the streaming waves (wave-uniform)
+  const int xvw = p.xw ? 4 : 3;   // the TimeConv_x wave
   const int ecol = 4 * (hw ? wave : 0) + (lane >> 4), chs = 4 * (lane & 15);
   const int scol = tile * 16 + ecol;
   const bool svalid = scol < BN;
@@ -1289,7 +1293,7 @@ __global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
   };
 
   // ---- x / v channels (TimeConv_x, egno.py:103-108): wave 4, lane (d = g, column e), d < 3 ----
-  if (wave == 4 && g < 3 && cvalid) {
+  if (wave == xvw && g < 3 && cvalid) {
     const int d = g;
     auto lm_at = [&](int t) { return p.lm[((p.frames ? (size_t)t * BN : 0) + c) * 3 + d]; };
     float xs[TB], vs[TB], lms[TB];
@@ -1352,10 +1356,10 @@ __global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
   }
   // ---- step 1: truncated DFT of this wave's input channels ----
   // every frame's h is loaded once and unconditionally (clamped frame index, see the x / v loads
-  // above), and kept in registers for the residual of step 3. With no barrier and no x / v work ahead
-  // of them, waves 0-3 request these at the kernel's start. (Placed above the x / v block in the source,
-  // their live range spans it in every wave, which crashed LLVM's greedy register allocator on the
-  // TB = 16 instance.)
+  // above), and kept in registers for the residual of step 3. With no barrier ahead of them, the waves
+  // without x / v work request these at the kernel's start. (Placed above the x / v block in the
+  // source, their live range spans it in every wave, which crashed LLVM's greedy register allocator on
+  // the TB = 16 instance.)
   f4 hvs[TB];
   if (hw) {
 #pragma unroll
@@ -1714,11 +1718,13 @@ int launch_tconv(bool first, const TconvArgs& a_in, hipStream_t stream) {
     }
   const int ntiles = (a.BN + 15) / 16;
   a.xcd = xcd_on() && ntiles >= 64;
+  a.xw = ntiles < num_cus() && !getenv_int("NONODE_TC_NOXW");
   const int grid = a.xcd ? 8 * ((ntiles + 7) / 8) : ntiles;
   ProfScope prof(first ? 3 : 2, stream);
   auto go = [&](auto kt, auto kf) {
-    if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(TC_THREADS), 0, stream, a);
-    else hipLaunchKernelGGL(kf, dim3(grid), dim3(TC_THREADS), 0, stream, a);
+    const int threads = a.xw ? TC_THREADS : 256;
+    if (first) hipLaunchKernelGGL(kt, dim3(grid), dim3(threads), 0, stream, a);
+    else hipLaunchKernelGGL(kf, dim3(grid), dim3(threads), 0, stream, a);
   };
   if (a.T <= 10) {
     if (a.M <= 2) go(tconv_kernel<true, 2, 10>, tconv_kernel<false, 2, 10>);
