@@ -456,6 +456,30 @@ int nonode_gather_batch(int S, int Tf, int N, int B, int I, int To, const float*
  * 16-byte aligned; idx device int32 in [0, S). */
 int nonode_gather_rows(int S, long long K, int B, const float* src, const int* idx, float* dst, void* stream);
 
+/* ---- EGNO(flat=True) training (main_simulation_simple_no.py --flat; basic.py:38-40) ---- */
+
+/* One flat EGNN layer forward (EGNN_Layer.forward, basic.py:167-186, every BaseMLP 256 wide with
+ * Tanh) that keeps its state for the reverse pass: state [nonode_egnn_layer_flat_state_floats] holds
+ * the per-node projections P, Q [n][256], message sums M [n][64] and force sums F [n][4]. */
+size_t nonode_egnn_layer_flat_state_floats(int n_graphs, int N);
+int nonode_egnn_layer_flat(int n_graphs, int N, int n_edge_feat, int ef_mod, const float* h, const float* x,
+                           const float* v, const float* edge_fea, const float* blob, float* h_out, float* x_out,
+                           float* state, void* stream);
+/* Transposed fragments of a flat layer's 256-wide matrices for the reverse pass. */
+size_t nonode_flat_bwd_blob_floats(void);
+int nonode_pack_layer_flat_bwd(const nonode_layer_weights* w, int n_edge_feat, float* bblob, void* stream);
+/* Reverse of nonode_egnn_layer_flat (autograd of basic.py:107-186 with flat=True) given the gradients of
+ * its outputs: per node (node_ops [n][1676]: h part of dL/dh, dL/dM, dL/dF, dL/dx, the receiver / sender
+ * sums GA, GB [256] of dL/d(first Linear output), and the node MLPs' activations and gradients) and per
+ * edge (edge_ops [n (N-1)][1160]: the edge MLPs' activations and gradients, the scalar inputs) the operands of every
+ * weight gradient (each one a GEMM over nodes or edges, the caller's), and dL/dv of the input. */
+size_t nonode_egnn_layer_flat_bwd_node_floats(int n_graphs, int N);
+size_t nonode_egnn_layer_flat_bwd_edge_floats(int n_graphs, int N);
+int nonode_egnn_layer_flat_bwd(int n_graphs, int N, int n_edge_feat, int ef_mod, const float* h, const float* x,
+                               const float* v, const float* edge_fea, const float* blob, const float* bblob,
+                               const float* state, const float* g_x, const float* g_v, const float* g_h,
+                               float* node_ops, float* edge_ops, float* g_v_in, void* stream);
+
 /* ---- the fully connected edge list at the boundary (sync-free) ---- */
 
 /* NBodyDataset.get_edges (EGNO/simulation/dataset_simple.py:101-111; SEGNO/dataset_nbody.py:84-94) on

@@ -33,6 +33,9 @@ SYMBOLS = (
     "nonode_pack_layers", "nonode_pack_layers_bwd", "nonode_pack_tconvs",
     "nonode_embedding_forward", "nonode_embedding_backward_workspace_bytes", "nonode_embedding_backward",
     "nonode_full_edges", "nonode_check_full_edges", "nonode_poison_if_flagged",
+    "nonode_egnn_layer_flat_state_floats", "nonode_egnn_layer_flat", "nonode_flat_bwd_blob_floats",
+    "nonode_pack_layer_flat_bwd", "nonode_egnn_layer_flat_bwd_node_floats", "nonode_egnn_layer_flat_bwd_edge_floats",
+    "nonode_egnn_layer_flat_bwd",
 )
 
 VARIANT_EGNO = 0
@@ -204,6 +207,16 @@ def lib():
     L.nonode_full_edges.argtypes = [_i, _i, _vp, _vp, _vp]
     L.nonode_check_full_edges.argtypes = [_vp, _vp, _i, _ll, _i, _i, _vp, _vp]
     L.nonode_poison_if_flagged.argtypes = [_vp, _i, ctypes.POINTER(_vp), ctypes.POINTER(_ll), _vp]
+    L.nonode_egnn_layer_flat_state_floats.argtypes = [_i, _i]
+    L.nonode_egnn_layer_flat_state_floats.restype = _sz
+    L.nonode_egnn_layer_flat.argtypes = [_i] * 4 + [_vp] * 9
+    L.nonode_flat_bwd_blob_floats.restype = _sz
+    L.nonode_pack_layer_flat_bwd.argtypes = [ctypes.POINTER(LayerWeights), _i, _vp, _vp]
+    L.nonode_egnn_layer_flat_bwd_node_floats.argtypes = [_i, _i]
+    L.nonode_egnn_layer_flat_bwd_node_floats.restype = _sz
+    L.nonode_egnn_layer_flat_bwd_edge_floats.argtypes = [_i, _i]
+    L.nonode_egnn_layer_flat_bwd_edge_floats.restype = _sz
+    L.nonode_egnn_layer_flat_bwd.argtypes = [_i] * 4 + [_vp] * 14
     L.nonode_profile_begin.argtypes = [_i]
     L.nonode_profile_end.argtypes = [ctypes.POINTER(_f), ctypes.POINTER(_i), _i]
     for s in SYMBOLS:

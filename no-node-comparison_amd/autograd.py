@@ -238,3 +238,144 @@ def segno_train(model, his, x, v, edge_attr, T, B, N):
     """SEGNO.forward (one input, training): embedding + T substeps on the autograd tape."""
     params = [model.embedding.weight, model.embedding.bias] + [p for _, p in model.module.named_parameters()]
     return SEGNOTrain.apply(model, his, x, v, edge_attr, T, B, N, *params)
+
+
+# ---- EGNO(flat=True) training (main_simulation_simple_no.py --flat; basic.py:38-40) ------------------
+# One autograd node per layer: TimeConv + TimeConv_x (nonode_egno_tconv / nonode_egno_tconv_bwd) and the
+# flat EGNN layer (nonode_egnn_layer_flat / nonode_egnn_layer_flat_bwd: the per-node and per-edge reverse
+# of the 256-wide Tanh MLPs as HIP kernels). The weight gradients are sums over nodes or edges of the
+# operand rows the reverse kernels write, i.e. plain GEMMs (torch.mm on the device: hipBLASLt / rocBLAS).
+# The embedding Linear and the T-fold replication (egno.py:63-96) stay torch ops on the tape.
+_FN = dict(GHP=0, GM=64, GF=128, GX=132, GA=136, GB=392, T=648, GT=904, U=1160, GU=1416, GPHI=1672, STRIDE=1676)
+_FE = dict(A=0, M=256, C1=320, GZ3=576, GZ2=832, GPRE=896, GC=1152, S=1153, FE=1154, STRIDE=1160)
+
+
+def _flat_layer_params(model, i):
+    lay = model.layers[i]
+    e, c, v, n = (lay.edge_message_net.scalar_net.mlp, lay.coord_net.mlp, lay.node_v_net.mlp, lay.node_net.mlp)
+    return [e[0].weight, e[0].bias, e[2].weight, e[2].bias, c[0].weight, c[0].bias, c[2].weight, c[2].bias,
+            v[0].weight, v[0].bias, v[2].weight, v[2].bias, n[0].weight, n[0].bias, n[2].weight, n[2].bias]
+
+
+class FlatLayerTrain(torch.autograd.Function):
+    """TimeConv (+ TimeConv_x) of layer i, then its flat EGNN layer (egno.py:99-111 with flat=True)."""
+
+    @staticmethod
+    def forward(ctx, model, i, B, N, h, x, v, loc_mean, ef, *params):
+        L = _lib.lib()
+        T = model.num_timesteps
+        dev = h.device
+        BN, n = B * N, T * B * N
+        h, x, v, ef = _f32(h), _f32(x), _f32(v), _f32(ef)
+        blobs, tblobs = model._packed()
+        s = _lib.stream_of(h)
+        if model.use_time_conv:
+            lm = _f32(loc_mean)
+            tcx = _f32(model.time_conv_x_modules[i].t_conv.weights1)
+            ht, xt, vt = torch.empty(n, 64, device=dev), torch.empty(n, 3, device=dev), torch.empty(n, 3, device=dev)
+            _lib.check(L.nonode_egno_tconv(BN, T, model.num_modes, _lib.ptr(h), _lib.ptr(x), _lib.ptr(v), _lib.ptr(lm),
+                                           _lib.ptr(tblobs[i]), _lib.ptr(tcx), _lib.ptr(ht), _lib.ptr(xt), _lib.ptr(vt),
+                                           s))
+        else:
+            lm, ht, xt, vt = None, h, x, v
+        state = torch.empty(L.nonode_egnn_layer_flat_state_floats(T * B, N), device=dev)
+        h_out, x_out = torch.empty(n, 64, device=dev), torch.empty(n, 3, device=dev)
+        _lib.check(L.nonode_egnn_layer_flat(T * B, N, model.in_edge_nf, B, _lib.ptr(ht), _lib.ptr(xt), _lib.ptr(vt),
+                                            _lib.ptr(ef), _lib.ptr(blobs[i]), _lib.ptr(h_out), _lib.ptr(x_out),
+                                            _lib.ptr(state), s))
+        ctx.set_materialize_grads(False)
+        ctx.model, ctx.i, ctx.B, ctx.N = model, i, B, N
+        ctx.keep = (h, x, v, lm, ef, ht, xt, vt, state)
+        ctx.save_for_backward(*params)
+        return h_out, x_out, vt.clone() if vt is v else vt
+
+    @staticmethod
+    def backward(ctx, gh, gx, gv):
+        model, i, B, N = ctx.model, ctx.i, ctx.B, ctx.N
+        params = ctx.saved_tensors
+        h, x, v, lm, ef, ht, xt, vt, state = ctx.keep
+        ctx.keep = None
+        L = _lib.lib()
+        T = model.num_timesteps
+        dev = h.device
+        n, E = T * B * N, T * B * N * (N - 1)
+        z = lambda k: torch.zeros(n, k, device=dev)  # noqa: E731
+        gh = _f32(gh) if gh is not None else z(64)
+        gx = _f32(gx) if gx is not None else z(3)
+        gv = _f32(gv) if gv is not None else z(3)
+        blobs, _ = model._packed()
+        bb = model._packed_flat_bwd()
+        nops = torch.empty(n, _FN["STRIDE"], device=dev)
+        eops = torch.empty(E, _FE["STRIDE"], device=dev)
+        gvt = torch.empty(n, 3, device=dev)
+        s = _lib.stream_of(gh)
+        _lib.check(L.nonode_egnn_layer_flat_bwd(T * B, N, model.in_edge_nf, B, _lib.ptr(ht), _lib.ptr(xt), _lib.ptr(vt),
+                                                _lib.ptr(ef), _lib.ptr(blobs[i]), _lib.ptr(bb[i]), _lib.ptr(state),
+                                                _lib.ptr(gx), _lib.ptr(gv), _lib.ptr(gh), _lib.ptr(nops), _lib.ptr(eops),
+                                                _lib.ptr(gvt), s))
+        cols = lambda a, k, w: a[:, k:k + w]  # noqa: E731
+        F_, E_ = _FN, _FE
+        GA, GB = cols(nops, F_["GA"], 256), cols(nops, F_["GB"], 256)
+        gpre, a_, m_ = cols(eops, E_["GPRE"], 256), cols(eops, E_["A"], 256), cols(eops, E_["M"], 64)
+        gz3, gz2, c1 = cols(eops, E_["GZ3"], 256), cols(eops, E_["GZ2"], 64), cols(eops, E_["C1"], 256)
+        gc, sr = eops[:, E_["GC"]], eops[:, E_["S"]]
+        gt, t_ = cols(nops, F_["GT"], 256), cols(nops, F_["T"], 256)
+        gu, u_ = cols(nops, F_["GU"], 256), cols(nops, F_["U"], 256)
+        gphi = nops[:, F_["GPHI"]]
+        M = state[n * 512:n * 576].view(n, 64)
+        w1 = params[0]
+        ne = model.in_edge_nf
+        # the first Linear's columns [s, h_i, h_j, e] (EGNO order): GA / GB carry its h_i / h_j parts
+        dw1 = torch.cat([(gpre.t() @ sr)[:, None], GA.t() @ ht, GB.t() @ ht] +
+                        ([gpre.t() @ eops[:, E_["FE"]:E_["FE"] + ne]] if ne else []), 1)
+        grads = [dw1, GA.sum(0), gz2.t() @ a_, gz2.sum(0),              # edge MLP
+                 gz3.t() @ m_, gz3.sum(0), (gc @ c1)[None], gc.sum()[None],   # coord MLP
+                 gt.t() @ ht, gt.sum(0), (gphi @ t_)[None], gphi.sum()[None],  # node_v MLP
+                 gu.t() @ torch.cat([ht, M], 1), gu.sum(0), gh.t() @ u_, gh.sum(0)]   # node MLP
+        ght = cols(nops, F_["GHP"], 64) + GA @ w1[:, 1:65] + GB @ w1[:, 65:129]
+        gxt = cols(nops, F_["GX"], 3).contiguous()
+        ght = ght.contiguous()
+        grads = [g.reshape(p.shape).to(p.dtype) for g, p in zip(grads, params[:16])]
+        if not model.use_time_conv:
+            return (None,) * 4 + (ght, gxt, gvt, None, None) + tuple(grads)
+        g_h, g_x, g_v = torch.empty_like(h), torch.empty_like(x), torch.empty_like(v)
+        tw, txw = _f32(params[16]), _f32(params[17])      # kept alive over the call
+        g_tw, g_txw = torch.empty_like(tw), torch.empty_like(txw)
+        ws_bytes = L.nonode_egno_tconv_bwd_workspace_bytes(B * N, T, model.num_modes)
+        ws = torch.empty((ws_bytes + 3) // 4, device=dev)
+        _, tblobs = model._packed()
+        _lib.check(L.nonode_egno_tconv_bwd(B * N, T, model.num_modes, _lib.ptr(h), _lib.ptr(x), _lib.ptr(v), _lib.ptr(lm),
+                                           _lib.ptr(tblobs[i]), _lib.ptr(tw), _lib.ptr(txw), _lib.ptr(ght),
+                                           _lib.ptr(gxt), _lib.ptr(gvt), _lib.ptr(g_h), _lib.ptr(g_x), _lib.ptr(g_v),
+                                           _lib.ptr(g_tw), _lib.ptr(g_txw), _lib.ptr(ws), ws_bytes, s))
+        sink = getattr(model, "_train_bwd_sink", None)
+        if sink is not None:   # tests: the workspace head holds the LeakyReLU decisions the reverse used
+            sink.append((i, ws))
+        return (None,) * 4 + (g_h, g_x, g_v, None, None) + tuple(grads) + (g_tw.to(params[16].dtype),
+                                                                             g_txw.to(params[17].dtype))
+
+
+def egno_flat_train(model, x, h, edge_fea, v, loc_mean, t_out, B, N):
+    """EGNO(flat=True).forward in training (egno.py:37-111, num_inputs == 1): the time embedding and the
+    embedding Linear as torch ops, then one FlatLayerTrain node per layer."""
+    import math
+    T = model.num_timesteps
+    BN = B * N
+    dim, half = model.time_emb_dim, model.time_emb_dim // 2
+    # get_timestep_embedding (layer_no.py:8-17)
+    freqs = torch.exp(torch.arange(half, dtype=torch.float32, device=x.device) * -(math.log(10000) / (half - 1)))
+    ang = t_out.float()[..., None] * freqs
+    temb = torch.cat([torch.sin(ang), torch.cos(ang)], dim=-1)
+    if dim % 2 == 1:
+        temb = torch.nn.functional.pad(temb, (0, 1))
+    Bt = temb.shape[0]
+    temb = temb.permute(1, 0, 2)[:, None].repeat(1, BN // Bt, 1, 1).reshape(T, BN, -1)   # egno.py:66
+    hh = model.embedding(torch.cat([h.float()[None].expand(T, -1, -1), temb], -1).reshape(T * BN, -1))
+    xx, vv = x.float().repeat(T, 1), v.float().repeat(T, 1)                             # egno.py:89-96
+    lm = loc_mean.float() if model.use_time_conv else None
+    for i in range(model.n_layers):
+        params = _flat_layer_params(model, i)
+        if model.use_time_conv:
+            params += [model.time_conv_modules[i].t_conv.weights1, model.time_conv_x_modules[i].t_conv.weights1]
+        hh, xx, vv = FlatLayerTrain.apply(model, i, B, N, hh, xx, vv, lm, edge_fea, *params)
+    return xx, vv, hh

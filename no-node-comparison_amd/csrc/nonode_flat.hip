@@ -287,6 +287,258 @@ int launch_flat_layer(int n_graphs, int N, int ne, int ef_mod, const float* h, c
   return check_launch("flat_node_kernel");
 }
 
+// ---- the reverse pass of one flat layer (EGNO(flat=True) training; basic.py:38-40, 107-186 reversed) ----
+// Parity-first like the forward (exact f32 MFMAs): the per-node and per-edge reverse of the 256-wide
+// Tanh MLPs runs in two kernels; the weight gradients are plain GEMMs over the nodes / edges of the
+// operands these kernels write (dW = G^T A, summed by the host with a BLAS GEMM).
+// Transposed fragments (flat backward blob): 64 x 256 matrices as 16 k-steps of mfma_dense<16>, 256 x 64
+// matrices as 4 row blocks of mfma_dense<4>.
+constexpr int FB_WV1T = 0;                   // WV1^T  [64][256]
+constexpr int FB_WN1HT = FB_WV1T + 16384;    // WN1[:, :64]^T [64][256]
+constexpr int FB_WN1MT = FB_WN1HT + 16384;   // WN1[:, 64:]^T [64][256]
+constexpr int FB_WC1T = FB_WN1MT + 16384;    // Wc1^T  [64][256]
+constexpr int FB_W2T = FB_WC1T + 16384;      // W2^T   [256][64]: 4 row blocks
+constexpr int FB_WN2T = FB_W2T + 16384;      // WN2^T  [256][64]: 4 row blocks
+constexpr int FB_FLOATS = FB_WN2T + 16384;
+// per-node / per-edge operand rows of the reverse pass (floats)
+constexpr int FN_GHP = 0, FN_GM = 64, FN_GF = 128, FN_GX = 132, FN_GA = 136, FN_GB = 392, FN_T = 648, FN_GT = 904,
+              FN_U = 1160, FN_GU = 1416, FN_GPHI = 1672, FN_STRIDE = 1676;
+constexpr int FE_A = 0, FE_M = 256, FE_C1 = 320, FE_GZ3 = 576, FE_GZ2 = 832, FE_GPRE = 896, FE_GC = 1152,
+              FE_S = 1153, FE_FE = 1154, FE_STRIDE = 1160;   // FE_S: the radial input as used; FE_FE: e (4)
+
+// fragment of a transposed source: value (row o, column i) = W[(col_off + i) ld + row_off + o]
+__device__ __forceinline__ void pack_frag_tt(float* dst, const float* W, int ld, int row_off, int KT, int d) {
+  const int q = d & 3, l = (d >> 2) & 63, rest = d >> 8;
+  const int mt = rest % KT, mo = rest / KT;
+  const int o = 16 * mo + (l & 15), i = 16 * mt + 4 * (l >> 4) + q;
+  dst[d] = W[(size_t)i * ld + row_off + o];
+}
+__global__ void flat_pack_bwd_kernel(FlatPackArgs a, float* bb) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= FB_FLOATS) return;
+  const int sec = d >> 14, dd = d & 16383;
+  switch (sec) {
+    case 0: pack_frag_tt(bb + FB_WV1T, a.vw1, 64, 0, 16, dd); break;
+    case 1: pack_frag_tt(bb + FB_WN1HT, a.nw1, 128, 0, 16, dd); break;
+    case 2: pack_frag_tt(bb + FB_WN1MT, a.nw1, 128, 64, 16, dd); break;
+    case 3: pack_frag_tt(bb + FB_WC1T, a.cw1, 64, 0, 16, dd); break;
+    case 4: pack_frag_tt(bb + FB_W2T + (dd >> 12) * 4096, a.w2, 256, 64 * (dd >> 12), 4, dd & 4095); break;
+    case 5: pack_frag_tt(bb + FB_WN2T + (dd >> 12) * 4096, a.nw2, 256, 64 * (dd >> 12), 4, dd & 4095); break;
+  }
+}
+
+struct FlatBwdArgs {
+  int n_total, N, ne, ef_mod;
+  const float* h; const float* x; const float* v; const float* ef; const float* blob; const float* bb;
+  const float* P; const float* Q; const float* M; const float* F;   // the forward's workspace rows
+  const float* gx; const float* gv; const float* gh;                // gradients of the layer's outputs
+  float* nops;   // [n][FN_STRIDE]
+  float* eops;   // [n (N - 1)][FE_STRIDE], edge (r, k) at r (N - 1) + k - 1
+  float* gv_in;  // [n][3]
+};
+__device__ __forceinline__ void dtanh16(f4 (&g)[16], const f4 (&t)[16]) {   // g *= 1 - t^2
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[i][q] *= 1.f - t[i][q] * t[i][q];
+}
+
+// node reverse (basic.py:174-185), 16 rows per wave: gF, gM, the h part that does not go through the
+// edges, dL/dv, and the operands of the node-level weight gradients
+__global__ __launch_bounds__(256) void flat_node_bwd_kernel(FlatBwdArgs p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, e = lane & 15;
+  const int r0 = (blockIdx.x * 4 + wave) * 16;
+  if (r0 >= p.n_total) return;
+  const bool rvalid = r0 + e < p.n_total;
+  const int r = rvalid ? r0 + e : p.n_total - 1;
+  const float* vec = p.blob + FL_VEC;
+  float* no = p.nops + (size_t)r * FN_STRIDE;
+  f4 in8[8];
+  load_ecl(*reinterpret_cast<f4(*)[4]>(&in8[0]), p.h + (size_t)r * HID, g);
+  load_ecl(*reinterpret_cast<f4(*)[4]>(&in8[4]), p.M + (size_t)r * HID, g);
+  const float gx0 = p.gx[(size_t)r * 3 + 0], gx1 = p.gx[(size_t)r * 3 + 1], gx2 = p.gx[(size_t)r * 3 + 2];
+  const float v0 = p.v[(size_t)r * 3 + 0], v1 = p.v[(size_t)r * 3 + 1], v2 = p.v[(size_t)r * 3 + 2];
+  // node_v: t = Tanh(WV1 h + bv1), phi = wv2 . t + bv2; x_out = x + phi v + clamp(F / (N - 1))
+  f4 t[16];
+  load_ecl16(t, vec + FV_BV1 * 256, g);
+  mm256<4>(t, p.blob + FL_WV1, in8, lane);
+  tanh16(t);
+  const float phi = dot256(t, vec + FV_WV2 * 256, g) + p.blob[FL_SCAL + 1];
+  const float gphi = gx0 * v0 + gx1 * v1 + gx2 * v2;
+  if (rvalid) store_ecl16(no + FN_T, t, g);
+  f4 gt[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) gt[i] = *reinterpret_cast<const f4*>(vec + FV_WV2 * 256 + 16 * i + 4 * g) * gphi;
+  dtanh16(gt, t);
+  if (rvalid) store_ecl16(no + FN_GT, gt, g);
+  f4 ghp[4] = {};
+  mfma_dense<16>(ghp, p.bb + FB_WV1T, gt, lane);   // WV1^T gt
+  // node MLP: u = Tanh(WN1 [h, M] + bn1), h_out = WN2 u + bn2
+  f4 u[16];
+  load_ecl16(u, vec + FV_BN1 * 256, g);
+  mm256<8>(u, p.blob + FL_WN1, in8, lane);
+  tanh16(u);
+  if (rvalid) store_ecl16(no + FN_U, u, g);
+  f4 gho[4];
+  load_ecl(gho, p.gh + (size_t)r * HID, g);
+  f4 gu[16] = {};
+  mm256<4>(gu, p.bb + FB_WN2T, gho, lane);           // WN2^T gh_out
+  dtanh16(gu, u);
+  if (rvalid) store_ecl16(no + FN_GU, gu, g);
+  mfma_dense<16>(ghp, p.bb + FB_WN1HT, gu, lane);    // + WN1[:, :64]^T gu
+  f4 gm[4] = {};
+  mfma_dense<16>(gm, p.bb + FB_WN1MT, gu, lane);     // WN1[:, 64:]^T gu
+  if (rvalid) {
+    store_ecl(no + FN_GHP, ghp, g);
+    store_ecl(no + FN_GM, gm, g);
+    const float inv = 1.f / (float)(p.N - 1);
+    const f4 Fr = *reinterpret_cast<const f4*>(p.F + (size_t)r * 4);
+    if (g == 0) {
+      // clamp(F / (N - 1), +-100) passes the gradient inside the range (torch.clamp: bounds included)
+      f4 gF;
+      gF[0] = fabsf(Fr[0] * inv) <= 100.f ? gx0 * inv : 0.f;
+      gF[1] = fabsf(Fr[1] * inv) <= 100.f ? gx1 * inv : 0.f;
+      gF[2] = fabsf(Fr[2] * inv) <= 100.f ? gx2 * inv : 0.f;
+      gF[3] = 0.f;
+      *reinterpret_cast<f4*>(no + FN_GF) = gF;
+      *reinterpret_cast<f4*>(no + FN_GX) = f4{gx0, gx1, gx2, 0.f};   // the edges add their terms here
+      no[FN_GPHI] = gphi;
+      p.gv_in[(size_t)r * 3 + 0] = p.gv[(size_t)r * 3 + 0] + phi * gx0;
+      p.gv_in[(size_t)r * 3 + 1] = p.gv[(size_t)r * 3 + 1] + phi * gx1;
+      p.gv_in[(size_t)r * 3 + 2] = p.gv[(size_t)r * 3 + 2] + phi * gx2;
+    }
+  }
+}
+
+// edge reverse (basic.py:107-173), one wave per 16-receiver tile walking the N - 1 sender offsets as the
+// forward does: the receiver sums GA (registers) and dL/dx (receiver side), the sender sums GB and
+// dL/dx (sender side) by float atomics, and every edge's operands for the edge-level weight gradients
+__global__ __launch_bounds__(256) void flat_edge_bwd_kernel(FlatBwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float fsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, e = lane & 15, g = lane >> 4;
+  for (int i = tid; i < FL_EDGE_LDS / 4; i += 256)
+    reinterpret_cast<f4*>(fsm)[i] = reinterpret_cast<const f4*>(p.blob + FL_W2)[i];   // W2 | Wc1
+  __syncthreads();
+  const float* sW2 = fsm;
+  const float* sWc1 = fsm + 16384;
+  const float* vec = p.blob + FL_VEC;
+  const float bc2 = p.blob[FL_SCAL + 0];
+  const bool norm = p.blob[FL_SCAL + 2] != 0.f;
+  const int N = p.N, Nm1 = N - 1;
+  const int r0 = (blockIdx.x * 4 + wave) * 16;
+  if (r0 >= p.n_total) return;
+  const bool rvalid = r0 + e < p.n_total;
+  const int r = rvalid ? r0 + e : p.n_total - 1;
+  const int gr = r / N, n = r - gr * N;
+  float* nor = p.nops + (size_t)r * FN_STRIDE;
+  const float x0 = p.x[(size_t)r * 3 + 0], x1 = p.x[(size_t)r * 3 + 1], x2 = p.x[(size_t)r * 3 + 2];
+  const f4 gF = *reinterpret_cast<const f4*>(nor + FN_GF);
+  f4 gMr[4];
+  load_ecl(gMr, nor + FN_GM, g);
+  const float* efr = p.ef + ((size_t)(gr % p.ef_mod) * N + n) * Nm1 * p.ne;
+  f4 GA[16] = {};
+  float gxr0 = 0.f, gxr1 = 0.f, gxr2 = 0.f;
+#pragma unroll 1
+  for (int k = 1; k < N; ++k) {
+    int j = n + k;
+    j = j >= N ? j - N : j;
+    const int jj = j < n ? j : j - 1;
+    const size_t s = (size_t)gr * N + j;
+    float* eo = p.eops + ((size_t)r * Nm1 + (k - 1)) * FE_STRIDE;
+    const float q0 = x0 - p.x[s * 3 + 0], q1 = x1 - p.x[s * 3 + 1], q2 = x2 - p.x[s * 3 + 2];
+    const float s2 = fmaf(q0, q0, fmaf(q1, q1, q2 * q2));
+    const float sr = norm ? radial_norm(s2) : s2;
+    float fe[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int f = 0; f < p.ne; ++f) fe[f] = efr[(size_t)jj * p.ne + f];
+    // forward recompute: a = Tanh(P_r + Q_s + W1[:, s] s + W1[:, e] e), m, c1, c
+    f4 a[16];
+    load_ecl16(a, p.Q + s * 256, g);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = 16 * i + 4 * g;
+      f4 tt = *reinterpret_cast<const f4*>(p.P + (size_t)r * 256 + c) + a[i] +
+              *reinterpret_cast<const f4*>(vec + FV_WS * 256 + c) * sr;
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        if (f < p.ne) tt += *reinterpret_cast<const f4*>(vec + (FV_WE0 + f) * 256 + c) * fe[f];
+      a[i] = tt;
+    }
+    tanh16(a);
+    f4 m[4];
+    load_ecl(m, p.blob + FL_VEC64, g);
+    mfma_dense<16>(m, sW2, a, lane);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[mt][q] = tanhf(m[mt][q]);
+    f4 c1[16];
+    load_ecl16(c1, vec + FV_BC1 * 256, g);
+    mm256<4>(c1, sWc1, m, lane);
+    tanh16(c1);
+    const float c = dot256(c1, vec + FV_WC2 * 256, g) + bc2;
+    // reverse: f = r c (gF_r is the gradient of every edge of receiver r: EGNO clamps the mean)
+    const float gc = rvalid ? gF[0] * q0 + gF[1] * q1 + gF[2] * q2 : 0.f;
+    if (rvalid) {
+      store_ecl16(eo + FE_A, a, g);
+      store_ecl(eo + FE_M, m, g);
+      store_ecl16(eo + FE_C1, c1, g);
+      if (g == 0) {
+        eo[FE_GC] = gc;
+        eo[FE_S] = sr;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) eo[FE_FE + f] = fe[f];
+      }
+    }
+    // gz3 = gc wc2 (1 - c1^2) (in c1's registers); gm = Wc1^T gz3 + gM_r; gz2 = gm (1 - m^2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const f4 w = *reinterpret_cast<const f4*>(vec + FV_WC2 * 256 + 16 * i + 4 * g);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c1[i][q] = gc * w[q] * (1.f - c1[i][q] * c1[i][q]);
+    }
+    if (rvalid) store_ecl16(eo + FE_GZ3, c1, g);
+    f4 gz2[4] = {gMr[0], gMr[1], gMr[2], gMr[3]};
+    if (!rvalid) zero4(gz2);
+    mfma_dense<16>(gz2, p.bb + FB_WC1T, c1, lane);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gz2[mt][q] *= 1.f - m[mt][q] * m[mt][q];
+    if (rvalid) store_ecl(eo + FE_GZ2, gz2, g);
+    // gpre = W2^T gz2 (1 - a^2)
+    f4 gp[16] = {};
+    mm256<4>(gp, p.bb + FB_W2T, gz2, lane);
+    dtanh16(gp, a);
+    if (rvalid) store_ecl16(eo + FE_GPRE, gp, g);
+    float gs = dot256(gp, vec + FV_WS * 256, g);
+    if (norm) gs = s2 < 1e-12f ? gs * 1e12f : 0.f;   // d normalize(s) / ds
+    const float gr0 = fmaf(2.f * gs, q0, gF[0] * c), gr1 = fmaf(2.f * gs, q1, gF[1] * c),
+                gr2 = fmaf(2.f * gs, q2, gF[2] * c);
+    if (rvalid) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        GA[i] += gp[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) atomicAdd(p.nops + s * FN_STRIDE + FN_GB + 16 * i + 4 * g + q, gp[i][q]);
+      }
+      gxr0 += gr0; gxr1 += gr1; gxr2 += gr2;
+      if (g == 0) {
+        atomicAdd(p.nops + s * FN_STRIDE + FN_GX + 0, -gr0);
+        atomicAdd(p.nops + s * FN_STRIDE + FN_GX + 1, -gr1);
+        atomicAdd(p.nops + s * FN_STRIDE + FN_GX + 2, -gr2);
+      }
+    }
+  }
+  if (rvalid) {
+    store_ecl16(nor + FN_GA, GA, g);
+    if (g == 0) {
+      atomicAdd(nor + FN_GX + 0, gxr0);
+      atomicAdd(nor + FN_GX + 1, gxr1);
+      atomicAdd(nor + FN_GX + 2, gxr2);
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -310,6 +562,69 @@ int nonode_pack_layer_flat(const nonode_layer_weights* w, int variant, int hidde
                  2 * HID + 1 + n_edge_feat, n_edge_feat, (flags & NONODE_LAYER_NORM_RADIAL) ? 1 : 0, blob};
   hipLaunchKernelGGL(flat_pack_kernel, dim3((FL_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("flat_pack_kernel");
+}
+
+size_t nonode_flat_bwd_blob_floats(void) { return FB_FLOATS; }
+
+int nonode_pack_layer_flat_bwd(const nonode_layer_weights* w, int n_edge_feat, float* bblob, void* stream) {
+  if (!w || !bblob || !w->edge_w2 || !w->coord_w1 || !w->vel_w1 || !w->node_w1 || !w->node_w2)
+    return fail(NONODE_EINVAL, "pack_layer_flat_bwd: null pointer");
+  FlatPackArgs a{w->edge_w1, w->edge_b1, w->edge_w2, w->edge_b2, w->coord_w1, w->coord_b1, w->coord_w2, w->coord_b2,
+                 w->vel_w1, w->vel_b1, w->vel_w2, w->vel_b2, w->node_w1, w->node_b1, w->node_w2, w->node_b2,
+                 2 * HID + 1 + n_edge_feat, n_edge_feat, 0, nullptr};
+  hipLaunchKernelGGL(flat_pack_bwd_kernel, dim3((FB_FLOATS + 255) / 256), dim3(256), 0, (hipStream_t)stream, a, bblob);
+  return check_launch("flat_pack_bwd_kernel");
+}
+
+size_t nonode_egnn_layer_flat_state_floats(int n_graphs, int N) { return (size_t)n_graphs * N * 580; }
+
+int nonode_egnn_layer_flat(int n_graphs, int N, int n_edge_feat, int ef_mod, const float* h, const float* x,
+                           const float* v, const float* edge_fea, const float* blob, float* h_out, float* x_out,
+                           float* state, void* stream) {
+  if (n_graphs <= 0 || N < 2 || ef_mod <= 0 || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "egnn_layer_flat: n_graphs=%d N=%d ef_mod=%d ne=%d", n_graphs, N, ef_mod,
+                n_edge_feat);
+  if (!h || !x || !v || !blob || !h_out || !x_out || !state || (n_edge_feat > 0 && !edge_fea))
+    return fail(NONODE_EINVAL, "egnn_layer_flat: null pointer");
+  return launch_flat_layer(n_graphs, N, n_edge_feat, ef_mod, h, x, v, edge_fea, blob, h_out, x_out, state,
+                           (hipStream_t)stream);
+}
+
+size_t nonode_egnn_layer_flat_bwd_node_floats(int n_graphs, int N) { return (size_t)n_graphs * N * FN_STRIDE; }
+size_t nonode_egnn_layer_flat_bwd_edge_floats(int n_graphs, int N) {
+  return (size_t)n_graphs * N * (N - 1) * FE_STRIDE;
+}
+
+int nonode_egnn_layer_flat_bwd(int n_graphs, int N, int n_edge_feat, int ef_mod, const float* h, const float* x,
+                               const float* v, const float* edge_fea, const float* blob, const float* bblob,
+                               const float* state, const float* g_x, const float* g_v, const float* g_h,
+                               float* node_ops, float* edge_ops, float* g_v_in, void* stream) {
+  if (n_graphs <= 0 || N < 2 || ef_mod <= 0 || n_edge_feat < 0 || n_edge_feat > 4)
+    return fail(NONODE_EUNSUPPORTED, "egnn_layer_flat_bwd: n_graphs=%d N=%d ef_mod=%d ne=%d", n_graphs, N, ef_mod,
+                n_edge_feat);
+  if (!h || !x || !v || !blob || !bblob || !state || !g_x || !g_v || !g_h || !node_ops || !edge_ops || !g_v_in ||
+      (n_edge_feat > 0 && !edge_fea))
+    return fail(NONODE_EINVAL, "egnn_layer_flat_bwd: null pointer");
+  static std::once_flag once;
+  std::call_once(once, [] {
+    hipFuncSetAttribute((const void*)flat_edge_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FL_EDGE_LDS * 4);
+  });
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)n_graphs * N;
+  FlatBwdArgs a;
+  a.n_total = (int)n; a.N = N; a.ne = n_edge_feat; a.ef_mod = ef_mod;
+  a.h = h; a.x = x; a.v = v; a.ef = n_edge_feat ? edge_fea : blob; a.blob = blob; a.bb = bblob;
+  a.P = state; a.Q = state + n * 256; a.M = state + n * 512; a.F = state + n * 576;
+  a.gx = g_x; a.gv = g_v; a.gh = g_h;
+  a.nops = node_ops; a.eops = edge_ops; a.gv_in = g_v_in;
+  // GB and the sender side of dL/dx are float-atomic sums: zeroed first (the whole node rows)
+  if (hipMemsetAsync(node_ops, 0, n * FN_STRIDE * sizeof(float), s) != hipSuccess)
+    return fail(NONODE_ELAUNCH, "egnn_layer_flat_bwd: memset");
+  const int blocks = (int)((n + 63) / 64);
+  hipLaunchKernelGGL(flat_node_bwd_kernel, dim3(blocks), dim3(256), 0, s, a);
+  if (int rc = check_launch("flat_node_bwd_kernel")) return rc;
+  hipLaunchKernelGGL(flat_edge_bwd_kernel, dim3(blocks), dim3(256), FL_EDGE_LDS * 4, s, a);
+  return check_launch("flat_edge_bwd_kernel");
 }
 
 }  // extern "C"

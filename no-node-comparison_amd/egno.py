@@ -85,7 +85,8 @@ class EGNO(nn.Module):
     with_v=False builds the reference's module tree (no node_v_net) but, as in the reference, cannot
     run forward (egno.py:95 / basic.py:180-181 need v and node_v_net). flat=True (every BaseMLP 4x
     wide with Tanh, basic.py:38-40; main_simulation_simple_no.py --flat) runs forward on its own layer
-    kernels (csrc/nonode_flat.hip); its training (a 256-wide reverse pass) raises NotImplementedError.
+    kernels (csrc/nonode_flat.hip); its training (num_inputs=1) runs one autograd node per layer
+    (autograd.FlatLayerTrain: HIP reverse kernels write the operands, weight gradients are GEMMs).
     """
 
     def __init__(self, n_layers, in_node_nf, in_edge_nf, hidden_nf, activation=nn.SiLU(), device='cpu',
@@ -237,6 +238,22 @@ class EGNO(nn.Module):
         self._bblobs, self._bblob_key = bb, key
         return bb
 
+    def _packed_flat_bwd(self):
+        """Transposed 256-wide fragments per flat layer (nonode_pack_layer_flat_bwd), rebuilt like _packed()."""
+        params = _lib.param_list(self, "pack_bwd", lambda: [p for l in self.layers for p in l.parameters()])
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._bblobs is not None and key == self._bblob_key:
+            return self._bblobs
+        L = _lib.lib()
+        bb = torch.empty(self.n_layers, L.nonode_flat_bwd_blob_floats(), dtype=torch.float32,
+                         device=self.embedding.weight.device)
+        stream = _lib.stream_of(bb)
+        for i, layer in enumerate(self.layers):
+            w = layer.weight_struct()
+            _lib.check(L.nonode_pack_layer_flat_bwd(ctypes.byref(w), self.in_edge_nf, bb[i].data_ptr(), stream))
+        self._bblobs, self._bblob_key = bb, key
+        return bb
+
     def forward(self, x, h, edge_index, edge_fea, v=None, loc_mean=None, timesteps_in=None, timesteps_out=None):
         """egno.py:37-111. x, v, loc_mean: [BN, 3]; h: [BN, in_node_nf]; edge_index: 2 x [E]
         (fully connected, the dataset's edge order); edge_fea: [E, in_edge_nf];
@@ -247,8 +264,8 @@ class EGNO(nn.Module):
         if v is None or (loc_mean is None and self.use_time_conv):
             raise ValueError("EGNO.forward needs v and loc_mean (the time convolution stacks "
                              "x - loc_mean with v, egno.py:103-105)")
-        if self.flat and self._trains():
-            self._no_flat_training()
+        if self.flat and self._trains() and self.num_inputs > 1:
+            raise NotImplementedError("EGNO(flat=True) training runs the single-input model (num_inputs=1)")
         if self.num_inputs > 1:
             return self._forward_multi(x, h, edge_index, edge_fea, v, loc_mean, timesteps_in, timesteps_out)
         _lib.require_device(x, h, v, loc_mean, edge_fea, self.embedding.weight)
@@ -265,6 +282,9 @@ class EGNO(nn.Module):
         if edge_fea.shape != (B * N * (N - 1), self.in_edge_nf):
             raise ValueError(f"edge_fea must be [{B * N * (N - 1)}, {self.in_edge_nf}], got {tuple(edge_fea.shape)}")
         if self._trains():
+            if self.flat:
+                from .autograd import egno_flat_train
+                return finish(egno_flat_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
             from .autograd import egno_forward_train
             return finish(egno_forward_train(self, x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
         return finish(self._forward_kernels(x, h, edge_fea, v, loc_mean, timesteps_out, B, N))
@@ -316,11 +336,6 @@ class EGNO(nn.Module):
         with torch.no_grad():
             return finish(self._launch_forward(L.nonode_egno_forward_flat if self.flat else L.nonode_egno_forward_frames,
                                                B, N, xf, hf, vf, lmf, eff, t_out, t_in=t_in))
-
-    def _no_flat_training(self):
-        if self.flat:
-            raise NotImplementedError("EGNO(flat=True) training: the MI355X reverse pass is built for the "
-                                      "64-wide SiLU MLPs only (flat=True runs forward / eval)")
 
     def _t_out_f32(self, t_out):
         """timesteps_out as f32 (cached per tensor/version: callers pass the same int64 tensor)."""

@@ -2,7 +2,7 @@
 EGNO norm=True (radial input normalised, basic.py:140-141), EGNO use_time_conv=False
 (egno.py:27-33, 99-107 skipped), SEGNO tanh=True (coord_mlp ends in nn.Tanh, gcl.py:57-59) --
 forward and training gradients through the HIP kernels; EGNO flat=True (basic.py:38-40, 256-wide
-Tanh MLPs, csrc/nonode_flat.hip) -- forward.
+Tanh MLPs, csrc/nonode_flat.hip) -- forward and training (autograd.FlatLayerTrain).
 
 Bars (max-norm relative): 1e-5 against the reference's own outputs / autograd gradients
 (egno_norm / egno_notc / segno_tanh fixtures) and against float64 references on other shapes.
@@ -17,6 +17,7 @@ from oracle import harness as oh
 from oracle import torch_ref as tr
 from tests.conftest import check_rel, load_golden, params_of
 from tests.test_gpu_parity import DEV, _dev, _egno_case
+from tests.test_gpu_train import _hip_lrelu_masks
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -141,9 +142,11 @@ FLAT = {"flat": dict(flat=True), "flat_norm": dict(flat=True, norm=True),
         "flat_notc": dict(flat=True, use_time_conv=False)}
 
 
-def test_egno_flat_forward_matches_reference_golden():
-    """flat=True against the reference's own outputs (egno_flat fixture); training is refused."""
+def test_egno_flat_forward_and_gradients_match_reference_golden():
+    """flat=True against the reference's own outputs, loss and autograd gradients (egno_flat fixture):
+    one training step of main_simulation_simple_no.py:267-280 with --flat."""
     fx = load_golden("egno_flat")
+    B, N, T = int(fx["cfg::B"]), int(fx["cfg::N"]), int(fx["cfg::T"])
     m = _egno(FLAT["flat"], params_of(fx)).eval()
     inp = _golden_inputs(fx)
     with torch.no_grad():
@@ -151,8 +154,106 @@ def test_egno_flat_forward_matches_reference_golden():
     check_rel("flat x", x.cpu(), fx["out::x"], TOL)
     check_rel("flat v", v.cpu(), fx["out::v"], TOL)
     check_rel("flat h", h.cpu(), fx["out::h"], TOL)
-    with pytest.raises(NotImplementedError, match="flat=True"):
-        _run(m.train(), inp)
+    m.train()
+    m.zero_grad(set_to_none=True)
+    xt, vt, ht = _run(m, inp)
+    check_rel("flat train x", xt.detach().cpu(), fx["out::x"], TOL)
+    check_rel("flat train h", ht.detach().cpu(), fx["out::h"], TOL)
+    pred = xt.reshape(T, B, N, 3).permute(1, 2, 0, 3)
+    loss = ((pred - _dev(fx["in::loc_true"])) ** 2).mean((0, 1, 3)).mean()
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(float(loss.detach()) - float(fx["out::loss"])) <= 1e-5 * abs(float(fx["out::loss"]))
+    n = 0
+    for k, p in m.named_parameters():
+        ref = fx["grad::" + k]
+        if np.abs(ref).max() == 0:
+            assert p.grad is None or float(p.grad.abs().max()) <= 1e-6, k
+            continue
+        n += 1
+        check_rel(f"flat grad {k}", p.grad, ref, TOL)
+    assert n >= 16 * 4 - 4 + 2 + 8
+
+
+@pytest.mark.parametrize("name", sorted(FLAT))
+@pytest.mark.parametrize("B,N", [(6, 20), (3, 7)])
+def test_egno_flat_gradients_match_f64_autograd(name, B, N):
+    """flat=True training against float64 torch autograd of the restatement, every option pairing and
+    ragged receiver tiles; the loss also reads v and h so every output's reverse is exercised. As in
+    test_gpu_train's B=512 case, TimeConv's LeakyReLU kink: the float64 reference is evaluated at the
+    HIP reverse's own branch decisions (the head of nonode_egno_tconv_bwd's workspace, the layout of
+    the training state's), and every element whose decision differs from float64's lies at the kink
+    (|y| tiny against the layer's scale: layer 1 of the (6, 20) case holds one at |y| = 2.5e-8 max)."""
+    T = 10
+    m = _egno(FLAT[name], seed=B + 3 * N).train()
+    case = _egno_case(B, N, T, seed=N + 5)
+    rng = np.random.default_rng(B)
+    target = rng.standard_normal((B, N, T, 3)).astype(np.float32)
+    wv, wh = rng.standard_normal((T * B * N, 3)).astype(np.float32), rng.standard_normal((T * B * N, 64)).astype(np.float32)
+    m.zero_grad(set_to_none=True)
+    m._train_bwd_sink = []
+    x, v, h = _run(m, {k: _dev(val) for k, val in case.items()})
+    loss = ((x.reshape(T, B, N, 3).permute(1, 2, 0, 3) - _dev(target)) ** 2).mean((0, 1, 3)).mean() + \
+        1e-3 * (v * _dev(wv)).sum() + 1e-4 * (h * _dev(wh)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    sink = dict(m._train_bwd_sink)
+    del m._train_bwd_sink
+    dt = torch.float64
+    t = {k: torch.tensor(val).to(dt) if val.dtype.kind == "f" else torch.tensor(val) for k, val in case.items()}
+    tw, tv = torch.tensor(wv).to(dt), torch.tensor(wh).to(dt)
+
+    def f64(**kw):
+        p = {k: q.detach().cpu().to(dt).requires_grad_(True) for k, q in m.state_dict().items()}
+        xr, vr, hr = tr.egno_forward(p, t["x"], t["h"], t["row"], t["col"], t["edge_fea"], t["v"], t["loc_mean"],
+                                     t["t_out"], T=T, **FLAT[name], **kw)
+        lr = ((xr.reshape(T, B, N, 3).permute(1, 2, 0, 3) - torch.tensor(target).to(dt)) ** 2).mean((0, 1, 3)).mean() + \
+            1e-3 * (vr * tw).sum() + 1e-4 * (hr * tv).sum()
+        lr.backward()
+        return lr, p
+
+    ys = []
+    lr, p = f64(lrelu_record=ys)
+    assert abs(float(loss.detach()) - float(lr.detach())) <= 1e-5 * abs(float(lr.detach()))
+    if FLAT[name].get("use_time_conv", True):
+        assert sorted(sink) == list(range(m.n_layers))
+        masks = [_hip_lrelu_masks(sink[i], 1, T, B * N)[0] for i in range(m.n_layers)]
+        for i, (mk, y) in enumerate(zip(masks, ys)):
+            flip = mk != (y > 0)
+            assert int(flip.sum()) <= 16, (i, int(flip.sum()))
+            if flip.any():
+                assert float(y[flip].abs().max()) <= 1e-5 * float(y.abs().max()), i   # at the kink
+        _, p = f64(lrelu_masks=masks)
+    for k, q in m.named_parameters():
+        ref = p[k].grad
+        if ref is None or float(ref.abs().max()) == 0:
+            assert q.grad is None or float(q.grad.abs().max()) <= 1e-6, k
+            continue
+        check_rel(f"{name} grad {k}", q.grad, ref, TOL)
+
+
+def test_egno_flat_training_step_updates_and_repacks():
+    """Three optimizer steps (the reference loop's Adam) on a flat model: each forward sees the updated
+    weights (re-packed blobs, forward and reverse), and the training forward (torch embedding, one
+    autograd node per layer) equals the one-call eval forward."""
+    B, N, T = 4, 20, 10
+    m = _egno(FLAT["flat"], seed=51).train()
+    inp = {k: _dev(v) for k, v in _egno_case(B, N, T, seed=52).items()}
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(3):
+        opt.zero_grad()
+        x, _, _ = _run(m, inp)
+        loss = ((x - inp["x"].repeat(T, 1)) ** 2).mean()
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    assert all(np.isfinite(losses)) and losses[2] != losses[0]
+    with torch.no_grad():
+        xe, ve, he = _run(m.eval(), inp)
+    xt, vt, ht = _run(m.train(), inp)
+    for name, a, b in (("x", xt, xe), ("v", vt, ve), ("h", ht, he)):
+        check_rel(f"train vs eval {name}", a.detach(), b.cpu().numpy(), 1e-6)
 
 
 @pytest.mark.parametrize("name", sorted(FLAT))

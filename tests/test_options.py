@@ -131,21 +131,30 @@ def test_egno_with_v_false_builds_reference_tree_and_cannot_run():
         m(z, torch.zeros(10, 2), pkg.graph.full_edges(2, 5), torch.zeros(40, 2), v=z, loc_mean=z)
 
 
-def test_egno_flat_is_forward_only_and_packs_egno_layers_only():
-    """flat=True (basic.py:38-40: every BaseMLP 4x wide with Tanh) builds the reference tree and runs
-    forward on its own kernels (tests/test_gpu_options.py); training stops before any device work, and
-    the flat packer refuses SEGNO layers and unknown option bits without touching the device."""
+def test_egno_flat_training_is_device_only_and_packs_egno_layers_only():
+    """flat=True (basic.py:38-40: every BaseMLP 4x wide with Tanh) builds the reference tree; its forward
+    and training run on their own kernels (tests/test_gpu_options.py). On the CPU both stop at the device
+    check; multi-input flat training is refused before any device work; the flat packers refuse SEGNO
+    layers, unknown option bits and null pointers without touching the device."""
     m = _egno(0, flat=True)
     e = m.layers[0].edge_message_net.scalar_net.mlp
     assert e[0].weight.shape == (256, 2 * 64 + 1 + 2) and isinstance(e[1], torch.nn.Tanh)
     z = torch.zeros(10, 3)
-    with pytest.raises(NotImplementedError, match="flat=True"):
+    with pytest.raises(pkg._lib.NonodeError, match="no CPU path"):
         m.train()(z, torch.zeros(10, 2), pkg.graph.full_edges(2, 5), torch.zeros(40, 2), v=z, loc_mean=z)
+    torch.manual_seed(0)
+    mi = pkg.EGNO(n_layers=2, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_timesteps=10,
+                  num_inputs=2, flat=True)
+    with pytest.raises(NotImplementedError, match="num_inputs=1"):
+        mi.train()(z[None].repeat(2, 1, 1), torch.zeros(2, 10, 2), pkg.graph.full_edges(2, 5),
+                   torch.zeros(2, 40, 2), v=z[None].repeat(2, 1, 1), loc_mean=z[None].repeat(2, 1, 1))
     L = pkg._lib.lib()
     w = pkg._lib.LayerWeights(*([16] * 16))   # never dereferenced: the variant check fails first
     for variant in (pkg._lib.VARIANT_SEGNO, pkg._lib.VARIANT_EGNO | pkg._lib.LAYER_TANH_COORD):
         assert L.nonode_pack_layer_flat(w, variant, 64, 2, 16, None) == 1
+    assert L.nonode_pack_layer_flat_bwd(w, 2, None, None) == 1
     assert L.nonode_flat_blob_floats() > L.nonode_layer_blob_floats()
+    assert L.nonode_egnn_layer_flat_bwd(0, 5, 2, 1, *([None] * 14)) != 0
 
 
 def test_pack_rejects_option_bits_of_the_other_variant():
