@@ -133,7 +133,7 @@ def test_unsupported_configs_raise():
         _egno_ctor(hidden_nf=32)
     # num_inputs > 1 is supported (inference): the embedding takes both time embeddings (egno.py:12-16)
     assert _egno_ctor(num_inputs=3).embedding.weight.shape == (64, 2 + 2 * 32)
-    _egno_ctor(flat=True)   # flat=True: forward only (tests/test_options.py)
+    _egno_ctor(flat=True)   # flat=True: forward and single-input training (tests/test_options.py)
     with pytest.raises(NotImplementedError):
         pkg.SEGNO(in_node_nf=1, in_edge_nf=2, hidden_nf=32)
     with pytest.raises(ValueError):
