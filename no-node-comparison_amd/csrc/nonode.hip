@@ -278,6 +278,9 @@ size_t layer_lds_floats(int ct, int s_rows, int keep = 0) {
 // hot loop carries no per-edge select; the kernel picks the copy once from the blob's flag.
 // SAVE: the saved-state substeps (LayerArgs::sv_h, SEGNO training), its own copy so the inference
 // instances carry none of it (one runtime branch cost C3 +4.5%)
+#ifndef NONODE_NODE_PAIR
+#define NONODE_NODE_PAIR 1   // EGNO 4-wave layer: node-update and (whole-graph) projection jobs two tiles at a time
+#endif
 template <int VARIANT, int KF, int NW, bool OPT, bool SAVE = false>
 __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)[NW + 1]) {
   constexpr bool PAIR = NW == 4;
@@ -409,6 +412,58 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)
     if (valid) store_ecl((isP ? sP : sQ) + local * ROWP, acc, g);
     if (valid && !isP && g == 0) sX[local * 4 + 3] = __builtin_isfinite(sa) ? 1.f : 0.f;   // sender flag
   };
+  // two whole-graph tiles' projections (cpg = 1): the fp16x3 path shares the WA / WB fragment reads;
+  // a tile past the fp16 hi range sends both through proj_tile (each tile's result is proj_tile's)
+  auto proj_job2 = [&](const float* __restrict__ hI, const float* blob, int rbase, int nend, int job0)
+      __attribute__((always_inline)) {
+    int joff = 0;
+    asm volatile("" : "+s"(joff));   // weight reads stay in the job (LICM would pin them in VGPRs)
+    blob += joff;
+    const int l0 = job0 * 16 + e, l1 = l0 + 16;
+    const bool v0 = rbase + l0 < nend, v1 = rbase + l1 < nend;
+    f4 h0[4], h1[4];
+    load_ecl(h0, hI + (size_t)(v0 ? rbase + l0 : nend - 1) * HID, g);
+    load_ecl(h1, hI + (size_t)(v1 ? rbase + l1 : nend - 1) * HID, g);
+    if (keep && v0) store_ecl(sH + l0 * ROWP, h0, g);
+    if (keep && v1) store_ecl(sH + l1 * ROWP, h1, g);
+    if (__builtin_expect(__any(fmaxf(amax_ecl(h0), amax_ecl(h1)) > H16_LIMIT), 0)) {
+      proj_tile(h0, blob, l0, v0);
+      proj_tile(h1, blob, l1, v1);
+      return;
+    }
+    f4 ap0[4], aq0[4], ap1[4], aq1[4];
+    load_vp(ap0, blob + OFF_VEC + V_B1 * 64, g);
+    load_vp(ap1, blob + OFF_VEC + V_B1 * 64, g);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) aq0[mt] = aq1[mt] = f4{0.f, 0.f, 0.f, 0.f};
+    h8 ah[2], al[2], bh[2], bl[2];
+    h16_split(h0, ah, al);
+    h16_split(h1, bh, bl);
+    mfma_h16x2(ap0, ap1, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WA * 4096), ah, al, bh, bl, lane,
+               h16_us(blob + OFF_SCAL, HS_N + H_WA));
+    mfma_h16x2(aq0, aq1, reinterpret_cast<const h8*>(blob + OFF_H16N + H_WB * 4096), ah, al, bh, bl, lane,
+               h16_us(blob + OFF_SCAL, HS_N + H_WB));
+    float sa0 = 0.f, sa1 = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sa0 += fabsf(ap0[mt][q]) + fabsf(aq0[mt][q]);
+        sa1 += fabsf(ap1[mt][q]) + fabsf(aq1[mt][q]);
+      }
+    sa0 = group_sum(sa0);
+    sa1 = group_sum(sa1);
+    if (v0) {
+      store_ecl(sP + l0 * ROWP, ap0, g);
+      store_ecl(sQ + l0 * ROWP, aq0, g);
+      if (g == 0) sX[l0 * 4 + 3] = __builtin_isfinite(sa0) ? 1.f : 0.f;
+    }
+    if (v1) {
+      store_ecl(sP + l1 * ROWP, ap1, g);
+      store_ecl(sQ + l1 * ROWP, aq1, g);
+      if (g == 0) sX[l1 * 4 + 3] = __builtin_isfinite(sa1) ? 1.f : 0.f;
+    }
+  };
   auto load_sx = [&](const float* __restrict__ xI, const float* __restrict__ vI, int s0, int S) __attribute__((always_inline)) {
     for (int i = tid; i < S * 3; i += NW * 64) {
       const int s = i / 3, d = i - 3 * s;
@@ -435,8 +490,16 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)
     chunk_at(ch0, rbase, nend, s0, S);
     load_sx(xI, vI, s0, S);
     const int J = proj_jobs(rbase, nend, S);
-    #pragma unroll 1
-    for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job);
+    if (NONODE_NODE_PAIR && NW == 4 && VARIANT == EGNO && p.cpg == 1) {   // two tiles per job (phase C below)
+      #pragma unroll 1
+      for (int job = 2 * wave; job < J; job += 2 * NW) {
+        if (job + 1 < J) proj_job2(hI, p.blob, rbase, nend, job);
+        else proj_job(hI, p.blob, rbase, nend, s0, S, job);
+      }
+    } else {
+      #pragma unroll 1
+      for (int job = wave; job < J; job += NW) proj_job(hI, p.blob, rbase, nend, s0, S, job);
+    }
     STAMP(6);
     __syncthreads();
     STAMP(7);
@@ -1014,147 +1077,214 @@ __device__ __forceinline__ void egnn_layer_body(const LayerArgs& p, int (*s_cut)
         chunk_at(ci + 1, nrb, nne, ns0, nS);
         load_sx(xI, vI, ns0, nS);
       }
-      const int J = ctc + (has_next ? proj_jobs(nrb, nne, nS) : 0);
 #ifndef NONODE_C_COST
 #define NONODE_C_COST 4   // (A/B builds: the node-update job's modelled cost in projection-job units x 2)
 #endif
 #ifndef NONODE_A_COST
 #define NONODE_A_COST 2
 #endif
+#ifndef NONODE_CP_COST
+#define NONODE_CP_COST 8     // a paired node-update job (two tiles; 6 / 8 measured equal, r06 A/B)
+#endif
+#ifndef NONODE_AP_COST
+#define NONODE_AP_COST 4     // a paired projection job
+#endif
+      // Jobs of two tiles: each fragment read (global / L2) feeds both tiles' MFMAs and the wave has
+      // two independent chains to issue from (a single tile's job is one dependent chain of L2 reads
+      // and MFMAs: latency-bound at one wave per SIMD). Each tile's arithmetic is unchanged (bitwise).
+      constexpr bool PAIR = NONODE_NODE_PAIR != 0 && NW == 4 && VARIANT == EGNO;   // (8 waves: 256 VGPRs, no room)
+      const int PJ = has_next ? proj_jobs(nrb, nne, nS) : 0;
+      const bool ppair = PAIR && p.cpg == 1;
+      const int NJN = PAIR ? (ctc + 1) >> 1 : ctc;
+      const int J = NJN + (ppair ? (PJ + 1) >> 1 : PJ);
       constexpr int C_COST = NONODE_C_COST;
       const int A_COST = p.cpg == 1 ? NONODE_A_COST : 1;
       int ld[NW];
 #pragma unroll
       for (int i = 0; i < NW; ++i) ld[i] = 0;
+      // node update of tiles tau0 .. tau0 + U - 1 (U = 1 or 2)
+      auto node_job = [&](auto U_, const float* bj, int tau0) __attribute__((always_inline)) {
+        constexpr int U = decltype(U_)::value;
+        int rl[U], r[U], lc[U];
+        bool rvalid[U];
+        f4 hr[U][4], Mr[U][4];
+        float F0[U], F1[U], F2[U], x0[U], x1[U], x2[U], v0[U], v1[U], v2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          rl[u] = 16 * (tau0 + u) + e;
+          r[u] = rbase + rl[u];
+          rvalid[u] = r[u] < nend;
+          const int rc = rvalid[u] ? r[u] : nend - 1;
+          lc[u] = rc - rbase;   // the row in the chunk tables (fused: whole-graph chunk)
+          f4 Mb[4];
+          if (keep) load_ecl(hr[u], sH + lc[u] * ROWP, g);
+          else load_ecl(hr[u], hI + (size_t)rc * HID, g);
+          load_ecl(Mr[u], sM + rl[u] * ROWP, g);
+          load_ecl(Mb, sM + slotM + rl[u] * ROWP, g);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) Mr[u][mt] += Mb[mt];
+          const float* fa = sF + rl[u] * 4;
+          const float* fb = sF + slotF + rl[u] * 4;
+          F0[u] = fa[0] + fb[0]; F1[u] = fa[1] + fb[1]; F2[u] = fa[2] + fb[2];
+          {   // the rows are consumed: zero both slots for the next chunk's edge phase
+            const f4 z4[4] = {};
+            store_ecl(sM + rl[u] * ROWP, z4, g);
+            store_ecl(sM + slotM + rl[u] * ROWP, z4, g);
+            if (g == 0) {
+              *reinterpret_cast<f4*>(sF + rl[u] * 4) = z4[0];
+              *reinterpret_cast<f4*>(sF + slotF + rl[u] * 4) = z4[0];
+            }
+          }
+          if (fused) { x0[u] = sX[lc[u] * 4 + 0]; x1[u] = sX[lc[u] * 4 + 1]; x2[u] = sX[lc[u] * 4 + 2]; }
+          else { const size_t gr3 = (size_t)rc * 3; x0[u] = xI[gr3 + 0]; x1[u] = xI[gr3 + 1]; x2[u] = xI[gr3 + 2]; }
+          if (keep) { v0[u] = sVl[lc[u] * 4 + 0]; v1[u] = sVl[lc[u] * 4 + 1]; v2[u] = sVl[lc[u] * 4 + 2]; }
+          else { const size_t gr3 = (size_t)rc * 3; v0[u] = vI[gr3 + 0]; v1[u] = vI[gr3 + 1]; v2[u] = vI[gr3 + 2]; }
+        }
+        float nx0[U], nx1[U], nx2[U], nv0[U], nv1[U], nv2[U];
+        if (VARIANT == EGNO) {
+          // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
+          f4 t[U][4];
+#pragma unroll
+          for (int u = 0; u < U; ++u) load_vp(t[u], bj + OFF_VEC + V_BV1 * 64, g);
+          const h8* wv1 = reinterpret_cast<const h8*>(bj + OFF_H16N + H_WV1 * 4096);
+          if constexpr (U == 2) mm64x2(t[0], t[1], wv1, bj + OFF_WV1, hr[0], hr[1], lane, h16_us(bj + OFF_SCAL, HS_N + H_WV1));
+          else mm64(t[0], wv1, bj + OFF_WV1, hr[0], lane, h16_us(bj + OFF_SCAL, HS_N + H_WV1));
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            silu_ecl(t[u]);
+            const float phi = dot_vp(t[u], bj + OFF_VEC + V_WV2 * 64, g) + bv2;
+            nx0[u] = x0[u] + phi * v0[u] + fminf(fmaxf(F0[u] * p.inv_deg, -100.f), 100.f);
+            nx1[u] = x1[u] + phi * v1[u] + fminf(fmaxf(F1[u] * p.inv_deg, -100.f), 100.f);
+            nx2[u] = x2[u] + phi * v2[u] + fminf(fmaxf(F2[u] * p.inv_deg, -100.f), 100.f);
+            nv0[u] = v0[u]; nv1[u] = v1[u]; nv2[u] = v2[u];
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            // v <- v + agg/T ; x <- x + v/T   (gcl.py:255-257 with coords_weight, gcl.py:242)
+            nv0[u] = v0[u] + (F0[u] * p.inv_deg * p.cw) * p.dt;
+            nv1[u] = v1[u] + (F1[u] * p.inv_deg * p.cw) * p.dt;
+            nv2[u] = v2[u] + (F2[u] * p.inv_deg * p.cw) * p.dt;
+            nx0[u] = x0[u] + nv0[u] * p.dt;
+            nx1[u] = x1[u] + nv1[u] * p.dt;
+            nx2[u] = x2[u] + nv2[u] * p.dt;
+          }
+        }
+        // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
+        f4 z[U][4];
+        bool big[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          load_vp(z[u], bj + OFF_VEC + V_BN1 * 64, g);
+          big[u] = __any(fmaxf(amax_ecl(hr[u]), amax_ecl(Mr[u])) > H16_LIMIT);
+        }
+        const h8* wn1a = reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1A * 4096);
+        const h8* wn1b = reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1B * 4096);
+        const unsigned usa = h16_us(bj + OFF_SCAL, HS_N + H_WN1A), usb = h16_us(bj + OFF_SCAL, HS_N + H_WN1B);
+        bool anybig = big[0];
+        if constexpr (U == 2) anybig = anybig || big[1];
+        if (U == 2 && !__builtin_expect(anybig, 0)) {
+          h8 ah[2], al[2], bh[2], bl[2];
+          h16_split(hr[0], ah, al);
+          h16_split(hr[U - 1], bh, bl);
+          mfma_h16x2(z[0], z[U - 1], wn1a, ah, al, bh, bl, lane, usa);
+          h16_split(Mr[0], ah, al);
+          h16_split(Mr[U - 1], bh, bl);
+          mfma_h16x2(z[0], z[U - 1], wn1b, ah, al, bh, bl, lane, usb);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (__builtin_expect(big[u], 0)) {
+              f4 in8[8];
+#pragma unroll
+              for (int mt = 0; mt < 4; ++mt) { in8[mt] = hr[u][mt]; in8[4 + mt] = Mr[u][mt]; }
+              mfma_dense<8>(z[u], bj + OFF_WN1, in8, lane);
+            } else {
+              h8 xh[2], xl[2];
+              h16_split(hr[u], xh, xl);
+              mfma_h16(z[u], wn1a, xh, xl, lane, usa);
+              h16_split(Mr[u], xh, xl);
+              mfma_h16(z[u], wn1b, xh, xl, lane, usb);
+            }
+          }
+        }
+        f4 hn[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          silu_ecl(z[u]);
+          load_vp(hn[u], bj + OFF_VEC + V_BN2 * 64, g);
+        }
+        const h8* wn2 = reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN2 * 4096);
+        if constexpr (U == 2) mm64x2(hn[0], hn[1], wn2, bj + OFF_WN2, z[0], z[1], lane, h16_us(bj + OFF_SCAL, HS_N + H_WN2));
+        else mm64(hn[0], wn2, bj + OFF_WN2, z[0], lane, h16_us(bj + OFF_SCAL, HS_N + H_WN2));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) hn[u][mt] += hr[u][mt];
+          }
+          if (rvalid[u] && mO) {
+            f4 mt4[4];
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[u][mt] * NEG_LN2;    // sM holds -log2e * sum m
+            store_ecl(mO + (size_t)r[u] * HID, mt4, g);
+            if (g == 0 && p.f_out) *reinterpret_cast<f4*>(p.f_out + (size_t)r[u] * 4) = f4{F0[u], F1[u], F2[u], 0.f};
+          }
+          const bool next = fused && step + 1 < p.steps;   // fused: this tile's rows of step + 1 in LDS
+          if (rvalid[u] && (save || !(keep && next))) {
+            const size_t ro = (size_t)r[u];
+            store_ecl(hO + ro * HID, hn[u], g);
+            if (save && last) store_ecl(p.h_out + ro * HID, hn[u], g);
+            if (g == 0) {
+              float* xo = xO + ro * 3;
+              xo[0] = nx0[u]; xo[1] = nx1[u]; xo[2] = nx2[u];
+              if (VARIANT == SEGNO) {
+                float* vo = vO + ro * 3;
+                vo[0] = nv0[u]; vo[1] = nv1[u]; vo[2] = nv2[u];
+                if (save && last) {
+                  float* xo2 = p.x_out + ro * 3;
+                  float* vo2 = p.v_out + ro * 3;
+                  xo2[0] = nx0[u]; xo2[1] = nx1[u]; xo2[2] = nx2[u];
+                  vo2[0] = nv0[u]; vo2[1] = nv1[u]; vo2[2] = nv2[u];
+                }
+              }
+            }
+          }
+          if (next) {
+            if (rvalid[u]) {
+              if (keep) store_ecl(sH + rl[u] * ROWP, hn[u], g);
+              if (g == 0) {
+                sX[rl[u] * 4 + 0] = nx0[u]; sX[rl[u] * 4 + 1] = nx1[u]; sX[rl[u] * 4 + 2] = nx2[u];
+                if (keep) { sVl[rl[u] * 4 + 0] = nv0[u]; sVl[rl[u] * 4 + 1] = nv1[u]; sVl[rl[u] * 4 + 2] = nv2[u]; }
+              }
+            }
+            proj_tile(hn[u], bj, rl[u], rvalid[u]);
+          }
+        }
+      };
       #pragma unroll 1
       for (int j = 0; j < J; ++j) {
         int w = 0, lw = ld[0];
 #pragma unroll
         for (int i = 1; i < NW; ++i)
           if (ld[i] < lw) { lw = ld[i]; w = i; }
-        const int c = j < ctc ? C_COST : A_COST;
+        const bool nodej = j < NJN;
+        const int first = nodej ? (PAIR ? 2 * j : j) : (ppair ? 2 * (j - NJN) : j - NJN);
+        const bool two = nodej ? (PAIR && first + 1 < ctc) : (ppair && first + 1 < PJ);
+        const int c = nodej ? (two ? NONODE_CP_COST : C_COST) : (two ? NONODE_AP_COST : A_COST);
 #pragma unroll
         for (int i = 0; i < NW; ++i) ld[i] += i == w ? c : 0;
         if (w != wave) continue;
         int joff = 0;
         asm volatile("" : "+s"(joff));   // weight reads stay in the job (LICM would pin them in VGPRs)
         const float* bj = blob + joff;
-        if (j >= ctc) {
-          proj_job(hI, bj, nrb, nne, ns0, nS, j - ctc);
+        if (!nodej) {
+          if (two) proj_job2(hI, bj, nrb, nne, first);
+          else proj_job(hI, bj, nrb, nne, ns0, nS, first);
           continue;
         }
-        const int tau = j;
-        const int rl = 16 * tau + e;
-        const int r = rbase + rl;
-        const bool rvalid = r < nend;
-        const int rc = rvalid ? r : nend - 1;
-        const int lc = rc - rbase;   // the row in the chunk tables (fused: whole-graph chunk)
-        f4 in8[8];
-        f4 hr[4], Mr[4], Mb[4];
-        if (keep) load_ecl(hr, sH + lc * ROWP, g);
-        else load_ecl(hr, hI + (size_t)rc * HID, g);
-        load_ecl(Mr, sM + rl * ROWP, g);
-        load_ecl(Mb, sM + slotM + rl * ROWP, g);
-  #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) { Mr[mt] += Mb[mt]; in8[mt] = hr[mt]; in8[4 + mt] = Mr[mt]; }
-        const float* fa = sF + rl * 4;
-        const float* fb = sF + slotF + rl * 4;
-        const float F0 = fa[0] + fb[0], F1 = fa[1] + fb[1], F2 = fa[2] + fb[2];
-        {   // the rows are consumed: zero both slots for the next chunk's edge phase
-          const f4 z4[4] = {};
-          store_ecl(sM + rl * ROWP, z4, g);
-          store_ecl(sM + slotM + rl * ROWP, z4, g);
-          if (g == 0) {
-            *reinterpret_cast<f4*>(sF + rl * 4) = z4[0];
-            *reinterpret_cast<f4*>(sF + slotF + rl * 4) = z4[0];
-          }
-        }
-        float x0, x1, x2, v0, v1, v2;
-        if (fused) { x0 = sX[lc * 4 + 0]; x1 = sX[lc * 4 + 1]; x2 = sX[lc * 4 + 2]; }
-        else { const size_t gr3 = (size_t)rc * 3; x0 = xI[gr3 + 0]; x1 = xI[gr3 + 1]; x2 = xI[gr3 + 2]; }
-        if (keep) { v0 = sVl[lc * 4 + 0]; v1 = sVl[lc * 4 + 1]; v2 = sVl[lc * 4 + 2]; }
-        else { const size_t gr3 = (size_t)rc * 3; v0 = vI[gr3 + 0]; v1 = vI[gr3 + 1]; v2 = vI[gr3 + 2]; }
-        float nx0, nx1, nx2, nv0 = v0, nv1 = v1, nv2 = v2;
-        if (VARIANT == EGNO) {
-          // x <- x + phi_v(h) * v + clamp(mean_j f_ij, +-100)   (basic.py:174-178)
-          f4 t[4];
-          load_vp(t, bj + OFF_VEC + V_BV1 * 64, g);
-          mm64(t, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WV1 * 4096), bj + OFF_WV1, hr, lane,
-               h16_us(bj + OFF_SCAL, HS_N + H_WV1));
-          silu_ecl(t);
-          const float phi = dot_vp(t, bj + OFF_VEC + V_WV2 * 64, g) + bv2;
-          nx0 = x0 + phi * v0 + fminf(fmaxf(F0 * p.inv_deg, -100.f), 100.f);
-          nx1 = x1 + phi * v1 + fminf(fmaxf(F1 * p.inv_deg, -100.f), 100.f);
-          nx2 = x2 + phi * v2 + fminf(fmaxf(F2 * p.inv_deg, -100.f), 100.f);
-        } else {
-          // v <- v + agg/T ; x <- x + v/T   (gcl.py:255-257 with coords_weight, gcl.py:242)
-          nv0 = v0 + (F0 * p.inv_deg * p.cw) * p.dt;
-          nv1 = v1 + (F1 * p.inv_deg * p.cw) * p.dt;
-          nv2 = v2 + (F2 * p.inv_deg * p.cw) * p.dt;
-          nx0 = x0 + nv0 * p.dt;
-          nx1 = x1 + nv1 * p.dt;
-          nx2 = x2 + nv2 * p.dt;
-        }
-        // h <- node_mlp([h, sum_j m_ij]) (+ h if recurrent)   (basic.py:182-185, gcl.py:85-95)
-        f4 z[4];
-        load_vp(z, bj + OFF_VEC + V_BN1 * 64, g);
-        if (__builtin_expect(__any(fmaxf(amax_ecl(hr), amax_ecl(Mr)) > H16_LIMIT), 0)) {
-          mfma_dense<8>(z, bj + OFF_WN1, in8, lane);
-        } else {
-          h8 xh[2], xl[2];
-          h16_split(hr, xh, xl);
-          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1A * 4096), xh, xl, lane,
-                   h16_us(bj + OFF_SCAL, HS_N + H_WN1A));
-          h16_split(Mr, xh, xl);
-          mfma_h16(z, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN1B * 4096), xh, xl, lane,
-                   h16_us(bj + OFF_SCAL, HS_N + H_WN1B));
-        }
-        silu_ecl(z);
-        f4 hn[4];
-        load_vp(hn, bj + OFF_VEC + V_BN2 * 64, g);
-        mm64(hn, reinterpret_cast<const h8*>(bj + OFF_H16N + H_WN2 * 4096), bj + OFF_WN2, z, lane,
-             h16_us(bj + OFF_SCAL, HS_N + H_WN2));
-        if (VARIANT == SEGNO && p.recurrent) {   // gcl.py:93-94
-  #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) hn[mt] += hr[mt];
-        }
-        if (rvalid && mO) {
-          f4 mt4[4];
-  #pragma unroll
-          for (int mt = 0; mt < 4; ++mt) mt4[mt] = Mr[mt] * NEG_LN2;    // sM holds -log2e * sum m
-          store_ecl(mO + (size_t)r * HID, mt4, g);
-          if (g == 0 && p.f_out) *reinterpret_cast<f4*>(p.f_out + (size_t)r * 4) = f4{F0, F1, F2, 0.f};
-        }
-        const bool next = fused && step + 1 < p.steps;   // fused: this tile's rows of step + 1 in LDS
-        if (rvalid && (save || !(keep && next))) {
-          const size_t ro = (size_t)r;
-          store_ecl(hO + ro * HID, hn, g);
-          if (save && last) store_ecl(p.h_out + ro * HID, hn, g);
-          if (g == 0) {
-            float* xo = xO + ro * 3;
-            xo[0] = nx0; xo[1] = nx1; xo[2] = nx2;
-            if (VARIANT == SEGNO) {
-              float* vo = vO + ro * 3;
-              vo[0] = nv0; vo[1] = nv1; vo[2] = nv2;
-              if (save && last) {
-                float* xo2 = p.x_out + ro * 3;
-                float* vo2 = p.v_out + ro * 3;
-                xo2[0] = nx0; xo2[1] = nx1; xo2[2] = nx2;
-                vo2[0] = nv0; vo2[1] = nv1; vo2[2] = nv2;
-              }
-            }
-          }
-        }
-        if (next) {
-          if (rvalid) {
-            if (keep) store_ecl(sH + rl * ROWP, hn, g);
-            if (g == 0) {
-              sX[rl * 4 + 0] = nx0; sX[rl * 4 + 1] = nx1; sX[rl * 4 + 2] = nx2;
-              if (keep) { sVl[rl * 4 + 0] = nv0; sVl[rl * 4 + 1] = nv1; sVl[rl * 4 + 2] = nv2; }
-            }
-          }
-          proj_tile(hn, bj, rl, rvalid);
-        }
+        if (two) node_job(std::integral_constant<int, 2>{}, bj, first);
+        else node_job(std::integral_constant<int, 1>{}, bj, first);
       }
     }
     STAMP(12);

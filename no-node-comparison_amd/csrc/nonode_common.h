@@ -356,6 +356,44 @@ __device__ __forceinline__ void mfma_h16r3(f4 (&acc0)[4], f4 (&acc1)[4], f4 (&ac
   }
 }
 
+// two units (or tiles) through one fp16x3 matrix read from LDS or L2: each fragment read feeds both
+// units' MFMAs, and each accumulator sees the same MFMA sequence as mfma_h16 (bitwise the same sums)
+__device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
+                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2], int lane,
+                                           unsigned us) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    h8 ah[4], al[4];
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) {
+      ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
+      al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
+    }
+    const h8 x0s = h8_scale(x0h[s], us), x1s = h8_scale(x1h[s], us);
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1h[s], acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(al[mo], x0s, acc0[mo]); acc1[mo] = mfma16(al[mo], x1s, acc1[mo]); }
+#pragma unroll
+    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1l[s], acc1[mo]); }
+  }
+}
+// mm64 for two tiles: the fp16x3 path shares every fragment read between them. The range guard stays
+// per tile (a tile past the fp16 hi range takes mm64's exact f32 path, and so, in that rare case, does
+// its partner through its own mm64), so each tile's result is bitwise mm64's.
+__device__ __forceinline__ void mm64x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wh, const float* wf, const f4 (&x0)[4],
+                                       const f4 (&x1)[4], int lane, unsigned us) {
+  if (__builtin_expect(__any(fmaxf(amax_ecl(x0), amax_ecl(x1)) > H16_LIMIT), 0)) {
+    mm64(acc0, wh, wf, x0, lane, us);
+    mm64(acc1, wh, wf, x1, lane, us);
+  } else {
+    h8 x0h[2], x0l[2], x1h[2], x1l[2];
+    h16_split(x0, x0h, x0l);
+    h16_split(x1, x1h, x1l);
+    mfma_h16x2(acc0, acc1, wh, x0h, x0l, x1h, x1l, lane, us);
+  }
+}
+
 // f4 sum as four plain v_add_f32: the backend would emit two v_pk_add_f32, which cost more than the
 // plain ops they replace when issued beside MFMAs (MI355X_MICROARCH.md constants table)
 __device__ __forceinline__ f4 add4(f4 a, f4 b) {

@@ -439,27 +439,6 @@ __device__ __forceinline__ void wgrad_pair(f4 (&acc)[4][4], float& sc, const f4 
   }
   __builtin_amdgcn_wave_barrier();
 }
-// two units through one LDS-resident fp16x3 matrix: each fragment read feeds both units' MFMAs
-__device__ __forceinline__ void mfma_h16x2(f4 (&acc0)[4], f4 (&acc1)[4], const h8* wf, const h8 (&x0h)[2],
-                                           const h8 (&x0l)[2], const h8 (&x1h)[2], const h8 (&x1l)[2], int lane,
-                                           unsigned us) {
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    h8 ah[4], al[4];
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) {
-      ah[mo] = wf[((s * 4 + mo) * 2 + 0) * 64 + lane];
-      al[mo] = wf[((s * 4 + mo) * 2 + 1) * 64 + lane];
-    }
-    const h8 x0s = h8_scale(x0h[s], us), x1s = h8_scale(x1h[s], us);
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0h[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1h[s], acc1[mo]); }
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(al[mo], x0s, acc0[mo]); acc1[mo] = mfma16(al[mo], x1s, acc1[mo]); }
-#pragma unroll
-    for (int mo = 0; mo < 4; ++mo) { acc0[mo] = mfma16(ah[mo], x0l[s], acc0[mo]); acc1[mo] = mfma16(ah[mo], x1l[s], acc1[mo]); }
-  }
-}
 // out0/1 += W x0/1 for two gradient column sets, each column scaled to [2^11, 2^12) before the split
 // (mm64_cs for two units sharing the fragment reads)
 __device__ __forceinline__ void mm64_cs2(f4 (&out0)[4], f4 (&out1)[4], const h8* wh, const f4 (&x0)[4],
