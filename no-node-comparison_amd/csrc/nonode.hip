@@ -1345,7 +1345,15 @@ struct TconvArgs {
 // B_m = c_m Wi_m / T, -A_m. With Xr_m = sum_t h cos, Xs_m = sum_t h sin (so X_m = Xr_m - i Xs_m):
 //   Yr_m = A_m^T Xr_m + B_m^T Xs_m,  Yi_m = B_m^T Xr_m - A_m^T Xs_m,
 //   y[t] = sum_m (Yr_m cos(2 pi m t/T) - Yi_m sin(2 pi m t/T))   (= irfft(pad(Y), n=T)).
-size_t tconv_blob_floats(int modes) { return (size_t)(1 + 3 * (modes - 1)) * 4096; }
+// After the f32 fragments (tconv_mats(M) x 4096 floats) the blob holds the same matrices as fp16 hi / lo
+// fragments for the fp16x3 mixing (round 6; pack_h16 layout, 4096 floats each), each scaled by a power of
+// two 2^e that brings its largest |entry| into [1, 2) (the weights are ~1e-4: unscaled, their hi parts
+// would be fp16 subnormals), then a table of 2 x 64 floats: [mat] the lo shift's packed half2 (2^-k, 2^-k)
+// (h8_scale), [64 + mat] 2^-e, the factor that takes a product back to the unscaled matrix.
+constexpr int tconv_mats(int M) { return 1 + 3 * (M - 1); }
+size_t tconv_blob_floats(int modes) { return (size_t)tconv_mats(modes) * 8192 + 128; }
+__device__ __forceinline__ size_t tconv_h16_off(int M) { return (size_t)tconv_mats(M) * 4096; }
+__device__ __forceinline__ size_t tconv_scal_off(int M) { return (size_t)tconv_mats(M) * 8192; }
 
 struct TconvPackBatch { const float* w[PACK_MAX]; float* out[PACK_MAX]; };
 __global__ void tconv_pack_kernel(TconvPackBatch tb, int Mfull, int M, int T) {
@@ -1363,6 +1371,41 @@ __global__ void tconv_pack_kernel(TconvPackBatch tb, int Mfull, int M, int T) {
   else { m = 1 + (mat - 1) / 3; const int kind = (mat - 1) % 3; c = (kind == 1) ? 1 : 0; sgn = (kind == 2) ? -1.f : 1.f; }
   const float cm = (m == 0 || 2 * m == T) ? 1.f : 2.f;
   out[d] = sgn * cm / (float)T * w[(((size_t)i * 64 + o) * Mfull + m) * 2 + c];
+}
+// fp16 hi / lo fragments of matrix blockIdx.x from the f32 fragments tconv_pack_kernel wrote (same stream)
+__global__ __launch_bounds__(256) void tconv_pack_h16_kernel(TconvPackBatch tb, int M) {
+  float* blob = tb.out[blockIdx.y];
+  const int mat = blockIdx.x;
+  const float* f32 = blob + (size_t)mat * 4096;
+  // A[o][i] (output o, input i) sits at f32[((o / 16 * 4 + i / 16) * 64 + o % 16 + 16 (i / 4 % 4)) * 4 + i % 4]
+  auto at = [&](int o, int i) {
+    return f32[(((o >> 4) * 4 + (i >> 4)) * 64 + (o & 15) + 16 * ((i >> 2) & 3)) * 4 + (i & 3)];
+  };
+  __shared__ float red[4];
+  float mx = 0.f;
+  for (int i = threadIdx.x; i < 4096; i += 256) mx = fmaxf(mx, fabsf(f32[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const bool ok = mx > 0.f && __builtin_isfinite(mx);
+  const int e = ok ? min(max(1 - __builtin_amdgcn_frexp_expf(mx), -60), 60) : 0;   // max |A| 2^e in [1, 2)
+  const int k = ok ? min(max(H16_LO_TARGET + 1 - __builtin_amdgcn_frexp_expf(__builtin_ldexpf(mx, e)), 0), 14) : 0;
+  _Float16* dst = reinterpret_cast<_Float16*>(blob + tconv_h16_off(M) + (size_t)mat * 4096);
+  for (int d = threadIdx.x; d < 8192; d += 256) {
+    const int j = d & 7, lane = (d >> 3) & 63, hl = (d >> 9) & 1, mo = (d >> 10) & 3, s2 = d >> 12;
+    const int row = 16 * mo + (lane & 15);
+    const int col = 16 * (2 * s2 + (j >> 2)) + 4 * (lane >> 4) + (j & 3);
+    const float w = __builtin_ldexpf(at(row, col), e);   // exact (a power of two)
+    const _Float16 h = (_Float16)w;
+    dst[d] = hl == 0 ? h : (_Float16)__builtin_ldexpf(w - (float)h, k);   // (see pack_h16)
+  }
+  if (threadIdx.x == 0) {
+    float* sc = blob + tconv_scal_off(M);
+    sc[mat] = h16_us_bits(k);
+    sc[64 + mat] = __builtin_ldexpf(1.f, -e);
+  }
 }
 
 // One workgroup (4 + 1 waves) per tile of 16 columns (b, n). Wave w < 4: DFT over T of columns 4w..4w+3
@@ -1535,19 +1578,75 @@ __global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
       for (int q = 0; q < 4; ++q) acc = mfma(a[q], in[mt][q], acc);
     }
   };
-  if (hw) {
-    Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
-    mix(Yr[0], 0, 0);
+  // fp16x3 (round 6): 6 v_mfma_f32_16x16x32_f16 per matrix instead of 16 f32 MFMAs of 4x the cycles;
+  // acc += 2^-e (A 2^e)^T x, the product in a fresh accumulator (exact rescale, one rounding more)
+  const h8* wh16 = reinterpret_cast<const h8*>(p.wp + tconv_h16_off(M));
+  const float* wsc = p.wp + tconv_scal_off(M);
+  auto mix16 = [&](f4& acc, int mat, const h8 (&xh)[2], const h8 (&xl)[2]) {
+    const h8* wf = wh16 + (size_t)mat * 1024;
+    const unsigned us = __float_as_uint(wsc[mat]);
+    f4 t = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int m = 1; m < MM; ++m) {
-      if (m < M) {
-        const int mat = 1 + 3 * (m - 1);
-        Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
-        Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
-        mix(Yr[m], mat + 0, 2 * m - 1);   // A^T Xr
-        mix(Yr[m], mat + 1, 2 * m);       // B^T Xs
-        mix(Yi[m], mat + 1, 2 * m - 1);   // B^T Xr
-        mix(Yi[m], mat + 2, 2 * m);       // -A^T Xs
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const h8 ah = wf[((s2 * 4 + wave) * 2 + 0) * 64 + lane], al = wf[((s2 * 4 + wave) * 2 + 1) * 64 + lane];
+      t = mfma16(ah, xh[s2], t);
+      t = mfma16(al, h8_scale(xh[s2], us), t);
+      t = mfma16(ah, xl[s2], t);
+    }
+    acc += t * wsc[64 + mat];
+  };
+  if (hw) {
+    // a spectrum past the fp16 hi range (a diverged rollout) takes the exact f32 mixing
+    bool big = false;
+    {
+      f4 in[4];
+      load_ecl(in, &sX[0][e][0], g);
+      big = amax_ecl(in) > H16_LIMIT;
+#pragma unroll
+      for (int v = 1; v < 2 * MM - 1; ++v) {
+        if (v < 2 * M - 1) {
+          load_ecl(in, &sX[v][e][0], g);
+          big = big || amax_ecl(in) > H16_LIMIT;
+        }
+      }
+    }
+    if (__builtin_expect(__any(big), 0)) {
+      Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
+      mix(Yr[0], 0, 0);
+#pragma unroll
+      for (int m = 1; m < MM; ++m) {
+        if (m < M) {
+          const int mat = 1 + 3 * (m - 1);
+          Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
+          Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
+          mix(Yr[m], mat + 0, 2 * m - 1);   // A^T Xr
+          mix(Yr[m], mat + 1, 2 * m);       // B^T Xs
+          mix(Yi[m], mat + 1, 2 * m - 1);   // B^T Xr
+          mix(Yi[m], mat + 2, 2 * m);       // -A^T Xs
+        }
+      }
+    } else {
+      f4 in[4];
+      h8 rh[2], rl[2], sh[2], sl[2];
+      load_ecl(in, &sX[0][e][0], g);
+      h16_split(in, rh, rl);
+      Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
+      mix16(Yr[0], 0, rh, rl);
+#pragma unroll
+      for (int m = 1; m < MM; ++m) {
+        if (m < M) {
+          const int mat = 1 + 3 * (m - 1);
+          load_ecl(in, &sX[2 * m - 1][e][0], g);
+          h16_split(in, rh, rl);
+          load_ecl(in, &sX[2 * m][e][0], g);
+          h16_split(in, sh, sl);
+          Yr[m] = f4{0.f, 0.f, 0.f, 0.f};
+          Yi[m] = f4{0.f, 0.f, 0.f, 0.f};
+          mix16(Yr[m], mat + 0, rh, rl);   // A^T Xr
+          mix16(Yr[m], mat + 1, sh, sl);   // B^T Xs
+          mix16(Yi[m], mat + 1, rh, rl);   // B^T Xr
+          mix16(Yi[m], mat + 2, sh, sl);   // -A^T Xs
+        }
       }
     }
   }
@@ -1950,7 +2049,7 @@ int nonode_pack_tconvs(const float* const* tconv_w, int n_layers, int modes, int
   if (modes < 1 || modes > MMAX || T < 1 || T > TMAX)
     return fail(NONODE_EUNSUPPORTED, "pack_tconv: modes=%d T=%d", modes, T);
   const int M = effective_modes(T, modes);
-  const int n = (int)tconv_blob_floats(M);
+  const int n = tconv_mats(M) * 4096;   // the f32 fragments (tconv_pack_kernel)
   for (int l = 0; l < n_layers; ++l)   // validated before the first launch
     if (!tconv_w[l] || !blobs[l]) return fail(NONODE_EINVAL, "pack_tconv: null pointer");
   for (int l0 = 0; l0 < n_layers; l0 += PACK_MAX) {
@@ -1963,6 +2062,8 @@ int nonode_pack_tconvs(const float* const* tconv_w, int n_layers, int modes, int
     hipLaunchKernelGGL(tconv_pack_kernel, dim3((n + 255) / 256, cnt), dim3(256), 0, (hipStream_t)stream, tb, modes,
                        M, T);
     if (int rc = check_launch("tconv_pack_kernel")) return rc;
+    hipLaunchKernelGGL(tconv_pack_h16_kernel, dim3(tconv_mats(M), cnt), dim3(256), 0, (hipStream_t)stream, tb, M);
+    if (int rc = check_launch("tconv_pack_h16_kernel")) return rc;
   }
   return NONODE_OK;
 }
