@@ -1610,7 +1610,9 @@ __global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
         }
       }
     }
-    if (__builtin_expect(__any(big), 0)) {
+    // (the 4- and 9-mode builds keep the f32 mixing: their fp16x3 form measured 2.8e-4 off at the h
+    // level for 5 modes, T = 8, cause not found; the 2-mode build is within the f32 path's rounding)
+    if (MM > 2 || __builtin_expect(__any(big), 0)) {
       Yr[0] = f4{0.f, 0.f, 0.f, 0.f};
       mix(Yr[0], 0, 0);
 #pragma unroll
