@@ -1708,40 +1708,54 @@ __global__ __launch_bounds__(TC_THREADS) void tconv_kernel(TconvArgs p) {
 // trig_out (training forward, else null): the [Bt][T][ncol] time-embedding values themselves
 // multi-input (t_in != null, egno.py:44-49, 77-79): emb_w columns are [h | temb(t_in) | temb(t_out)]
 // and t_in[b][t] is the input time of frame t's input
+constexpr int TEMB_ROWS = 16;   // (b, t) rows per 256-thread block (4 per wave)
 __global__ __launch_bounds__(256) void temb_kernel(int Bt, int T, int din, int dim, const float* t_out,
                                                    const float* emb_w, int emb_ld, const float* emb_b,
                                                    float* etab, const float* t_in = nullptr,
                                                    float* trig_out = nullptr) {
-  // a 256-thread block owns 4 (b, t) rows x 64 outputs; each row's sin / cos table (<= 2 * 64
-  // values, dim <= 64 is checked by the host) is computed once into LDS instead of once per output
-  __shared__ float trig[4][128];
-  const int row = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int bt = blockIdx.x * 4 + row;
-  const bool live = bt < Bt * T;
+  // a 256-thread block owns TEMB_ROWS (b, t) rows x 64 outputs; each row's sin / cos table (<= 2 * 64
+  // values, dim <= 64 is checked by the host) is computed once into LDS, and each wave reads its lane's
+  // weight row once for its 4 rows (round 6: 4 rows per block re-read the whole matrix per row, 6.7 us)
+  __shared__ float trig[TEMB_ROWS][128];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r0 = blockIdx.x * TEMB_ROWS;
+  const int nrows = Bt * T;
   const int half = dim / 2;
   const int ncol = (t_in ? 2 : 1) * dim;
   const float scale = (float)(log(10000.0) / (double)(half - 1));
-  if (live) {
-    for (int c = lane; c < ncol; c += 64) {
-      const int seg = c / dim, k = c % dim;           // seg 0: t_in (if given) else t_out
-      const float tv = (t_in && seg == 0) ? t_in[bt] : t_out[bt];
-      const float fk = expf((float)(k % half) * -scale);
-      const float arg = tv * fk;
-      trig[row][c] = k < half ? sinf(arg) : cosf(arg);
-      if (trig_out) trig_out[(size_t)bt * ncol + c] = trig[row][c];   // training: the embedding's inputs
-    }
+  for (int i = threadIdx.x; i < TEMB_ROWS * ncol; i += 256) {
+    const int row = i / ncol, c = i - row * ncol, bt = r0 + row;
+    if (bt >= nrows) continue;
+    const int seg = c / dim, k = c % dim;           // seg 0: t_in (if given) else t_out
+    const float tv = (t_in && seg == 0) ? t_in[bt] : t_out[bt];
+    const float fk = expf((float)(k % half) * -scale);
+    const float arg = tv * fk;
+    trig[row][c] = k < half ? sinf(arg) : cosf(arg);
+    if (trig_out) trig_out[(size_t)bt * ncol + c] = trig[row][c];   // training: the embedding's inputs
   }
   __syncthreads();
-  if (!live) return;
   const int o = lane;
-  float acc = emb_b[o];
   const float* w = emb_w + o * emb_ld + din;
+  const float b = emb_b[o];
+  constexpr int RW = TEMB_ROWS / 4;
+  float acc[RW];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) acc[j] = b;
   for (int seg = 0; seg < ncol / dim; ++seg)
+#pragma unroll 8
     for (int k = 0; k < half; ++k) {
-      acc = fmaf(w[seg * dim + k], trig[row][seg * dim + k], acc);
-      acc = fmaf(w[seg * dim + half + k], trig[row][seg * dim + half + k], acc);
+      const float w0 = w[seg * dim + k], w1 = w[seg * dim + half + k];
+#pragma unroll
+      for (int j = 0; j < RW; ++j) {   // (the per-row sum order of the one-row form)
+        acc[j] = fmaf(w0, trig[wave * RW + j][seg * dim + k], acc[j]);
+        acc[j] = fmaf(w1, trig[wave * RW + j][seg * dim + half + k], acc[j]);
+      }
     }
-  etab[(size_t)bt * 64 + o] = acc;
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int bt = r0 + wave * RW + j;
+    if (bt < nrows) etab[(size_t)bt * 64 + o] = acc[j];
+  }
 }
 
 // out[n][o] = b[o] + sum_k W[o][k] in[n][k]   (SEGNO embedding, model.py:73)
@@ -2167,8 +2181,7 @@ int egno_forward_impl(int frames, int flat, int B, int N, int T, int n_layers, i
                               0, ho, xo, nullptr, s, 1, nullptr, nullptr, nullptr, BN);
   };
   {
-    const int tot = Bt * T * 64;
-    hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim,
+    hipLaunchKernelGGL(temb_kernel, dim3((Bt * T + TEMB_ROWS - 1) / TEMB_ROWS), dim3(256), 0, s, Bt, T, in_node, time_emb_dim,
                        t_out, emb_w, emb_ld, emb_b, etab, t_in);
     if (int rc = check_launch("temb_kernel")) return rc;
   }

@@ -1994,8 +1994,7 @@ int egno_forward_train_impl(int frames, int B, int N, int T, int n_layers, int i
   {
     // temb_kernel also saves the raw time-embedding table and h0_kernel the h_in rows: the inputs of the
     // embedding's weight gradient (emb_grad_kernel)
-    const int tot = Bt * T * 64;
-    hipLaunchKernelGGL(temb_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, Bt, T, in_node, time_emb_dim, t_out,
+    hipLaunchKernelGGL(temb_kernel, dim3((Bt * T + TEMB_ROWS - 1) / TEMB_ROWS), dim3(256), 0, s, Bt, T, in_node, time_emb_dim, t_out,
                        emb_w, emb_ld, emb_b, etab, t_in, st.ein + n * in_node);
     if (int rc = check_launch("temb_kernel")) return rc;
     hipLaunchKernelGGL(h0_kernel, dim3((BN * 64 + 255) / 256), dim3(256), 0, s, BN, T, in_node, Bt, h, emb_w, emb_ld,
