@@ -11,7 +11,7 @@ from oracle import torch_ref as tr  # noqa: E402
 
 DEV = "cuda"
 L = pkg._lib.lib()
-for T, modes, BN in [(T, m, 1024) for T in (8, 10, 16) for m in (1, 2, 3, 4, 5, 9)]:
+for T, modes, BN in [(T, m, bn) for bn in (1024, 10240) for T in (8, 16) for m in (2, 3, 4, 5, 9)]:
     torch.manual_seed(0)
     m = pkg.EGNO(n_layers=1, in_node_nf=2, in_edge_nf=2, hidden_nf=64, with_v=True, num_modes=modes,
                  num_timesteps=T, time_emb_dim=32, device=DEV).eval()
@@ -34,5 +34,5 @@ for T, modes, BN in [(T, m, 1024) for T in (8, 10, 16) for m in (1, 2, 3, 4, 5, 
     dy = (ho.cpu().double() - h.double())
     yh = torch.where(dy >= 0, dy, dy / 0.01)
     err = (yh - y).abs()
-    print(f"T={T} modes={modes}: max|y| {float(y.abs().max()):.3e}  max|y_hip - y| {float(err.max()):.3e}  "
+    print(f"BN={BN} T={T} modes={modes}: max|y| {float(y.abs().max()):.3e}  max|y_hip - y| {float(err.max()):.3e}  "
           f"rel {float(err.max() / y.abs().max()):.3e}  (h-level rel {float((ho.cpu().double() - h.double() - torch.nn.functional.leaky_relu(y)).abs().max() / (h.double() + torch.nn.functional.leaky_relu(y)).abs().max()):.2e})", flush=True)
